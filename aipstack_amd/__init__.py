@@ -1,0 +1,40 @@
+"""aipstack_amd -- MI355X-native Internet-checksum engine for aipstack's packet path.
+
+The product is ``aipstack_amd/lib/libaipstack_chksum.so`` (host C++ + CDNA4 HIP
+kernels) behind the C-ABI in ``include/aipstack_amd/chksum.h``; this package is its
+Python host-side mirror (``chksum``) plus synthetic-batch plumbing (``synth``).
+Importing it loads the native library and fails loudly if it was not built.
+"""
+from . import _lib
+
+_lib.load()
+
+from .chksum import (  # noqa: E402
+    AIPSTACK_CHKSUM_EHIP,
+    AIPSTACK_CHKSUM_EINVAL,
+    AIPSTACK_CHKSUM_ENODEV,
+    AIPSTACK_CHKSUM_FINAL,
+    AIPSTACK_CHKSUM_MAX_LEN,
+    AIPSTACK_CHKSUM_OK,
+    ChksumError,
+    IpBufNode,
+    IpBufRef,
+    IpChksum,
+    IpChksumAccumulator,
+    IpChksumInverted,
+    chksum_batch_csr,
+    chksum_batch_seeded_csr,
+    chksum_batch_strided,
+    device_check,
+    ipBufProcessBytes,
+)
+
+LIB_PATH = _lib.LIB_PATH
+
+__all__ = [
+    "AIPSTACK_CHKSUM_EHIP", "AIPSTACK_CHKSUM_EINVAL", "AIPSTACK_CHKSUM_ENODEV",
+    "AIPSTACK_CHKSUM_FINAL", "AIPSTACK_CHKSUM_MAX_LEN", "AIPSTACK_CHKSUM_OK", "ChksumError",
+    "IpBufNode", "IpBufRef", "IpChksum", "IpChksumAccumulator", "IpChksumInverted",
+    "chksum_batch_csr", "chksum_batch_seeded_csr", "chksum_batch_strided", "device_check",
+    "ipBufProcessBytes", "LIB_PATH",
+]

@@ -1,0 +1,64 @@
+"""Loader for the in-tree product library ``aipstack_amd/lib/libaipstack_chksum.so``.
+
+The library is the C-ABI of ``include/aipstack_amd/chksum.h`` (+ ``synth.h``). There is
+no pure-Python or CPU fallback for the batch entry points: if the library is missing
+this module raises ``ImportError`` loudly (build it with ``make -C aipstack_amd/csrc`` or
+``python -c "import __graft_entry__ as g; g.build()"``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libaipstack_chksum.so")
+
+# Every symbol include/aipstack_amd/*.h declares, with its ctypes signature.
+_c_u16 = ctypes.c_uint16
+_c_u32 = ctypes.c_uint32
+_c_u64 = ctypes.c_uint64
+_c_int = ctypes.c_int
+_c_vp = ctypes.c_void_p
+_c_size = ctypes.c_size_t
+
+SIGNATURES = {
+    # chksum.h
+    "IpChksumInverted": (_c_u16, [_c_vp, _c_size]),
+    "aipstack_chksum_batch_strided": (_c_int, [_c_vp, _c_u64, _c_u32, _c_u64, _c_vp, _c_u32, _c_vp]),
+    "aipstack_chksum_batch_csr": (_c_int, [_c_vp, _c_vp, _c_u64, _c_vp, _c_u32, _c_vp]),
+    "aipstack_chksum_batch_seeded_csr": (_c_int, [_c_vp, _c_vp, _c_vp, _c_u64, _c_vp, _c_vp]),
+    "aipstack_chksum_strerror": (ctypes.c_char_p, [_c_int]),
+    "aipstack_chksum_last_hip_error": (_c_int, []),
+    "aipstack_chksum_device_check": (_c_int, [_c_int]),
+    "aipstack_chksum_abi_version": (_c_int, []),
+    # synth.h
+    "aipstack_synth_fill_host": (None, [_c_vp, _c_u64, _c_u64, _c_u64]),
+    "aipstack_synth_mixed_offsets_host": (_c_u64, [_c_vp, _c_u64, _c_u64]),
+    "aipstack_synth_apply_classes_host": (None, [_c_vp, _c_vp, _c_u64, _c_u64, _c_u64]),
+    "aipstack_synth_fill_device": (_c_int, [_c_vp, _c_u64, _c_u64, _c_u64, _c_vp]),
+    "aipstack_synth_apply_classes_device": (_c_int, [_c_vp, _c_vp, _c_u64, _c_u64, _c_u64, _c_vp]),
+}
+
+ABI_VERSION = 1
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load (once) and return the product library; raise ImportError if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"aipstack_amd: native library not built: {LIB_PATH} is missing "
+            "(run `make -C aipstack_amd/csrc`). There is no CPU fallback.")
+    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)  # AttributeError = library/header mismatch: loud
+        fn.restype = res
+        fn.argtypes = args
+    if lib.aipstack_chksum_abi_version() != ABI_VERSION:
+        raise ImportError("aipstack_amd: library ABI version mismatch")
+    _lib = lib
+    return lib

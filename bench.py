@@ -1,0 +1,326 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident Internet checksum throughput on MI355X (GiB/s).
+
+A "step" is one pass of the hot path -- one batched checksum launch
+(aipstack_chksum_batch_strided / _csr of libaipstack_chksum.so) over one batch of
+synthetic packets already resident in HBM. Default workload = BASELINE.json configs[1]
+(config A): 1 M x 1500-byte packets per GPU.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config A|B|C]
+    torchrun --nproc-per-node N ... bench.py --gpus N     (one rank per GPU)
+
+Multi-GPU: rank r owns a disjoint shard (packets [r*M, (r+1)*M) of one global batch,
+generated in place on its own GPU); there is NO data-path collective. A gloo process
+group is used only for the control plane (barriers around the timed region, max of the
+per-rank times). value = bytes of all ranks x K / max-over-ranks time ("scaling": weak).
+
+Prints ONE JSON line on stdout (everything else goes to stderr).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "GiB/s checksummed (device-resident), 1M×1500B packets, 1/2/4/8 GPUs"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md chip table), GB/s
+
+CONFIGS = {
+    # name: (layout, packets per GPU, packet bytes (strided) / None (mixed))
+    "A": ("strided", 1 << 20, 1500),
+    "B": ("strided", 256 << 10, 9000),
+    "C": ("csr", 2 << 20, None),
+}
+WORKLOAD_NAMES = {
+    "A": "1M x 1500B Ethernet-MTU packets per GPU, IP checksum (BASELINE configs[1]; x8 = configs[4])",
+    "B": "256K x 9000B jumbo packets per GPU, IP checksum (BASELINE configs[2])",
+    "C": "2M mixed 64-1500B packets per GPU incl. odd lengths/starts, CSR (BASELINE configs[3])",
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--config", default="A", choices=sorted(CONFIGS))
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-reps", type=int, default=15,
+                   help="timed single-thread passes of the CPU baseline sample")
+    p.add_argument("--no-parity", action="store_true")
+    return p.parse_args()
+
+
+def algorithmic_bytes(layout, n, total_payload):
+    """L bytes read + 2 bytes written per packet (+8 B offset for CSR)."""
+    b = total_payload + 2 * n
+    if layout == "csr":
+        b += 8 * (n + 1)
+    return b
+
+
+def cpu_baseline(layout, n, plen, off_host, data_seed, byte_offset, first_packet):
+    """Reference scalar path on the host, bounded sample = this rank's whole batch."""
+    from aipstack_amd import synth
+    total = int(off_host[-1]) if layout == "csr" else n * plen
+    host = np.empty(total, dtype=np.uint8)
+    synth.fill_host(host, data_seed, byte_offset)
+    if layout == "csr":
+        synth.apply_classes_host(host, off_host, first_packet=first_packet)
+    out = np.empty(n, dtype=np.uint16)
+    ref_path = os.path.join(ROOT, "oracle", "_ref", "libref_chksum.so")
+    cores_all = min(16, os.cpu_count() or 1)
+    if os.path.exists(ref_path):
+        kind = "reference"
+        lib = ctypes.CDLL(ref_path)
+        lib.ref_time_batch_strided.restype = ctypes.c_double
+        lib.ref_time_batch_strided.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                               ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
+                                               ctypes.c_void_p]
+        lib.ref_time_batch_csr.restype = ctypes.c_double
+        lib.ref_time_batch_csr.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                           ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+
+        def timed(threads, reps):
+            if layout == "csr":
+                o = off_host.astype(np.uint64)
+                return lib.ref_time_batch_csr(threads, reps, host.ctypes.data, o.ctypes.data, n,
+                                              out.ctypes.data)
+            return lib.ref_time_batch_strided(threads, reps, host.ctypes.data, plen, plen, n,
+                                              out.ctypes.data)
+    else:  # the C restatement (oracle/), single thread
+        kind = "port"
+        lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "libchksum_oracle.so"))
+        lib.oracle_batch_strided.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                                             ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32]
+        lib.oracle_batch_csr.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                         ctypes.c_void_p, ctypes.c_uint32]
+        cores_all = 1
+
+        def timed(threads, reps):
+            ts = []
+            o = off_host.astype(np.uint64) if layout == "csr" else None
+            for _ in range(reps + 1):
+                t0 = time.perf_counter()
+                if layout == "csr":
+                    lib.oracle_batch_csr(host.ctypes.data, o.ctypes.data, n, out.ctypes.data, 0)
+                else:
+                    lib.oracle_batch_strided(host.ctypes.data, plen, plen, n, out.ctypes.data, 0)
+                ts.append(time.perf_counter() - t0)
+            return float(np.median(ts[1:]))
+    t1 = timed(1, CPU_REPS)
+    res = {
+        "value": round(total / t1 / 2**30, 3),
+        "unit": "GiB/s",
+        "cores": 1,
+        "kind": kind,
+        "sample": f"this rank's whole batch ({n} packets, {total} B) in host memory, "
+                  f"median of {CPU_REPS} passes after 1 warm-up, 1 thread"
+                  + (" (reference Chksum.h:77-99 compiled -O2 from /root/reference)"
+                     if kind == "reference" else " (oracle/chksum_oracle.c port)"),
+    }
+    if cores_all > 1:
+        tn = timed(cores_all, 5)
+        res["all_cores"] = {"value": round(total / tn / 2**30, 3), "cores": cores_all}
+    res["cpu_model"] = _cpu_model()
+    return res, out
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor()
+
+
+CPU_REPS = 15
+
+
+def main():
+    global CPU_REPS
+    args = parse()
+    CPU_REPS = max(1, args.cpu_reps)
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    import torch.distributed as dist
+
+    import aipstack_amd as A
+    from aipstack_amd import synth
+
+    if world > 1:
+        # control plane only (barriers + max of times); no data-path collective
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if A.device_check(local_rank) != A.AIPSTACK_CHKSUM_OK:
+        raise SystemExit(f"rank {rank}: device {local_rank} is not a usable gfx950 device")
+
+    layout, n, plen = CONFIGS[args.config]
+    stream = torch.cuda.current_stream()
+
+    # ---- this rank's shard, generated in place (global packets [rank*n, (rank+1)*n))
+    off_host = None
+    if layout == "strided":
+        total = n * plen
+        byte_offset = rank * total
+        buf = torch.empty(total, dtype=torch.uint8, device=dev)
+        synth.fill_device(buf, synth.SEED_DATA, byte_offset)
+    else:
+        # mixed lengths of the GLOBAL batch, this rank's slice, rebased to 0
+        off_all = synth.mixed_offsets(n * world)
+        off_host = off_all[rank * n:(rank + 1) * n + 1] - off_all[rank * n]
+        byte_offset = int(off_all[rank * n])
+        total = int(off_host[-1])
+        buf = torch.empty(total, dtype=torch.uint8, device=dev)
+        synth.fill_device(buf, synth.SEED_DATA, byte_offset)
+        d_off = torch.from_numpy(off_host).to(dev)
+        synth.apply_classes_device(buf, d_off, first_packet=rank * n)
+    out = torch.empty(n, dtype=torch.uint16, device=dev)
+    torch.cuda.synchronize()
+
+    def step():
+        if layout == "strided":
+            A.chksum_batch_strided(buf, plen, plen, n, out=out, stream=stream)
+        else:
+            A.chksum_batch_csr(buf, d_off, out=out, stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # ---- timed region: barrier + synchronize on both sides, per-launch HIP events
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        starts[i].record(stream)
+        step()
+        ends[i].record(stream)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    kernel_ms = [s.elapsed_time(e) for s, e in zip(starts, ends)]
+    avg_kernel_s = float(np.mean(kernel_ms)) / 1e3
+
+    t = torch.tensor([elapsed], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    max_elapsed = float(t.item())
+
+    payload = total
+    alg = algorithmic_bytes(layout, n, payload)
+
+    # ---- parity of this run's output against the oracle / reference (rank 0 sample)
+    parity = None
+    cpu = None
+    if rank == 0:
+        host_out = out.cpu().numpy()
+        if not args.no_cpu_baseline and world == 1:
+            cpu, want = cpu_baseline(layout, n, plen, off_host, synth.SEED_DATA, byte_offset,
+                                     rank * n)
+            if not args.no_parity:
+                parity = "bit-exact" if np.array_equal(host_out, want) else "MISMATCH"
+        elif not args.no_parity:
+            parity = _oracle_sample_check(layout, n, plen, off_host, byte_offset, host_out)
+
+    bytes_all = payload * world  # weak scaling: every rank holds the same-size shard
+    value = bytes_all * args.steps / max_elapsed / 2**30
+    achieved = alg / avg_kernel_s / 1e9
+    result = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(max_elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u16",
+        "data": "synthetic (counter-based splitmix64 bytes, seed 42; generated on device)",
+        "config": {
+            "workload": WORKLOAD_NAMES[args.config],
+            "config": args.config,
+            "packets_per_gpu": n,
+            "packet_bytes": plen if plen else "64-1500 (mixed)",
+            "payload_bytes_per_gpu": payload,
+            "layout": layout,
+            "parallelism": f"disjoint packet shards x{world}, no collective",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": _pmc_traffic(args.config),
+            "kernel_us": round(avg_kernel_s * 1e6, 2),
+            "algorithmic_bytes_per_launch": alg,
+        },
+        "cpu_baseline": cpu,
+        "parity": parity,
+    }
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    if parity == "MISMATCH":
+        sys.exit(1)
+
+
+def _oracle_sample_check(layout, n, plen, off_host, byte_offset, got):
+    """Check the first 65536 packets of this rank's output against the C oracle."""
+    from aipstack_amd import synth
+    m = min(n, 65536)
+    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "libchksum_oracle.so"))
+    want = np.empty(m, dtype=np.uint16)
+    if layout == "strided":
+        host = np.empty(m * plen, dtype=np.uint8)
+        synth.fill_host(host, synth.SEED_DATA, byte_offset)
+        lib.oracle_batch_strided.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                                             ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32]
+        lib.oracle_batch_strided(host.ctypes.data, plen, plen, m, want.ctypes.data, 0)
+    else:
+        return None
+    return "bit-exact (first 65536 packets)" if np.array_equal(got[:m], want) else "MISMATCH"
+
+
+def _pmc_traffic(config):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, if one exists."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        v = d.get(config, {}).get("hbm_bytes_per_launch")
+        return None if v is None else int(v)
+    except (OSError, ValueError):
+        return None
+
+
+if __name__ == "__main__":
+    main()

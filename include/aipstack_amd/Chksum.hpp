@@ -1,0 +1,182 @@
+// aipstack_amd -- C++ host surface of the checksum engine.
+//
+// Mirrors the reference's checksum interface (ambrop72/aipstack src/aipstack/infra):
+//   IpChksumInverted            Chksum.h:77-99   (the extern "C" hook, in the .so)
+//   IpChksum(ptr, len)          Chksum.h:122-125
+//   IpChksumAccumulator         Chksum.h:148-316
+//   IpChksum(IpBufRef)          Chksum.h:332-336
+//   IpBufNode / IpBufRef        Buf.h:68-83, 118-251
+//   ipBufProcessBytes           BufUtils.h:129-178
+// in namespace AIpStackAmd, plus BatchChksum: a thin RAII-free C++ wrapper of the GPU
+// batch entry points of chksum.h.
+//
+// Drop-in use inside aipstack itself needs none of this: compile the stack with
+// -DAIPSTACK_EXTERNAL_CHKSUM and link libaipstack_chksum.so, whose extern "C"
+// IpChksumInverted the reference header then calls (Chksum.h:50-51). This header is for
+// code that wants the same calls without the reference headers, and for the batch API.
+#ifndef AIPSTACK_AMD_CHKSUM_HPP
+#define AIPSTACK_AMD_CHKSUM_HPP
+
+#include <cstddef>
+#include <cstdint>
+
+#include "aipstack_amd/chksum.h"
+
+namespace AIpStackAmd {
+
+// Chksum.h:122-125
+inline std::uint16_t IpChksum(char const *data, std::size_t len) {
+    return std::uint16_t(~IpChksumInverted(data, len));
+}
+
+// Buf.h:68-83
+struct IpBufNode {
+    char *ptr = nullptr;
+    std::size_t len = 0;
+    IpBufNode const *next = nullptr;
+};
+
+// Buf.h:118-251 (the subset the checksum path uses)
+struct IpBufRef {
+    IpBufNode const *node = nullptr;
+    std::size_t offset = 0;
+    std::size_t tot_len = 0;
+
+    char *getChunkPtr() const { return node->ptr + offset; }
+    std::size_t getChunkLength() const {
+        std::size_t rem = node->len - offset;
+        return tot_len < rem ? tot_len : rem;
+    }
+    IpBufRef hideHeader(std::size_t amount) const {
+        return IpBufRef{node, offset + amount, tot_len - amount};
+    }
+    IpBufRef revealHeader(std::size_t amount) const {
+        return IpBufRef{node, offset - amount, tot_len + amount};
+    }
+    IpBufRef subTo(std::size_t new_tot_len) const { return IpBufRef{node, offset, new_tot_len}; }
+};
+
+// BufUtils.h:129-178: visit each non-empty chunk of the first process_len bytes; moves
+// to the next node eagerly. `fn(char *ptr, size_t len)` returns how many it consumed.
+template <typename Fn>
+IpBufRef ipBufProcessBytes(IpBufRef buf, std::size_t process_len, Fn &&fn) {
+    std::size_t remain = buf.tot_len - process_len;
+    buf.tot_len = process_len;
+    for (;;) {
+        IpBufNode const node = *buf.node;
+        std::size_t node_rem = node.len - buf.offset;
+        bool consumed = buf.tot_len >= node_rem;
+        std::size_t chunk = consumed ? node_rem : buf.tot_len;
+        if (chunk > 0) {
+            std::size_t done = fn(node.ptr + buf.offset, chunk);
+            buf.tot_len -= done;
+            buf.offset += done;
+            if (done < chunk) {
+                remain += buf.tot_len;
+                buf.tot_len = 0;
+                break;
+            }
+        }
+        if (!consumed || node.next == nullptr) break;
+        buf.node = node.next;
+        buf.offset = 0;
+    }
+    buf.tot_len = remain;
+    return buf;
+}
+
+// Chksum.h:148-316. Same observable behaviour (State export/resume, header words added
+// without carry handling, chunk sums with end-around carry, getChksum = fold twice and
+// invert). Chunks are combined by their logical byte position: a chunk that starts at
+// an odd position contributes its sum byte-swapped, which is what the reference's
+// swap-after-odd-chunk rule amounts to (a byte swap is x*256 mod 0xFFFF, and swapping
+// twice is the identity).
+class IpChksumAccumulator {
+public:
+    enum class State : std::uint32_t {};
+
+    IpChksumAccumulator() : m_sum(0) {}
+    explicit IpChksumAccumulator(State state) : m_sum(std::uint32_t(state)) {}
+
+    State getState() const { return State(m_sum); }
+
+    void addWord16(std::uint16_t word) { m_sum += word; }
+    void addWordOctets(std::uint8_t hi, std::uint8_t lo) {
+        addWord16(std::uint16_t((std::uint16_t(hi) << 8) | lo));
+    }
+    void addWord32(std::uint32_t word) {
+        addWord16(std::uint16_t(word >> 16));
+        addWord16(std::uint16_t(word));
+    }
+    void addEvenBytes(char const *ptr, std::size_t num_bytes) {
+        unsigned char const *p = reinterpret_cast<unsigned char const *>(ptr);
+        for (std::size_t i = 0; i + 1 < num_bytes; i += 2)
+            addWord16(std::uint16_t((std::uint16_t(p[i]) << 8) | p[i + 1]));
+    }
+
+    std::uint16_t getChksum() {
+        fold();
+        return std::uint16_t(~m_sum);
+    }
+
+    std::uint16_t getChksum(IpBufRef buf) {
+        if (buf.tot_len > 0) addIpBuf(buf);
+        return getChksum();
+    }
+
+private:
+    void fold() {
+        m_sum = (m_sum & 0xFFFFu) + (m_sum >> 16);
+        m_sum = (m_sum & 0xFFFFu) + (m_sum >> 16);
+    }
+    static std::uint32_t swap16(std::uint32_t x) { return ((x & 0xFFu) << 8) | (x >> 8); }
+
+    void addIpBuf(IpBufRef buf) {
+        std::uint64_t sum = m_sum;
+        std::size_t pos = 0;  // logical position of the chunk inside the sequence
+        ipBufProcessBytes(buf, buf.tot_len, [&](char *p, std::size_t n) {
+            std::uint32_t b = IpChksumInverted(p, n);
+            sum += (pos & 1) ? swap16(b) : b;
+            pos += n;
+            return n;
+        });
+        // end-around-carry fold to 32 bits: nonzero stays nonzero, value mod 0xFFFF kept
+        sum = (sum & 0xFFFFFFFFu) + (sum >> 32);
+        sum = (sum & 0xFFFFFFFFu) + (sum >> 32);
+        m_sum = std::uint32_t(sum);
+    }
+
+    std::uint32_t m_sum;
+};
+
+// Chksum.h:332-336
+inline std::uint16_t IpChksum(IpBufRef buf) {
+    IpChksumAccumulator acc;
+    return acc.getChksum(buf);
+}
+
+// GPU batch entry points (device pointers, stream-ordered; see chksum.h).
+struct BatchChksum {
+    static int strided(void const *d_base, std::uint64_t stride, std::uint32_t len,
+                       std::uint64_t n, std::uint16_t *d_out, bool final_chksum = false,
+                       void *stream = nullptr) {
+        return aipstack_chksum_batch_strided(d_base, stride, len, n, d_out,
+                                             final_chksum ? AIPSTACK_CHKSUM_FINAL : 0u, stream);
+    }
+    static int csr(void const *d_base, std::uint64_t const *d_offsets, std::uint64_t n,
+                   std::uint16_t *d_out, bool final_chksum = false, void *stream = nullptr) {
+        return aipstack_chksum_batch_csr(d_base, d_offsets, n, d_out,
+                                         final_chksum ? AIPSTACK_CHKSUM_FINAL : 0u, stream);
+    }
+    static int seeded(void const *d_base, std::uint64_t const *d_offsets,
+                      IpChksumAccumulator::State const *d_states, std::uint64_t n,
+                      std::uint16_t *d_out, void *stream = nullptr) {
+        return aipstack_chksum_batch_seeded_csr(
+            d_base, d_offsets, reinterpret_cast<std::uint32_t const *>(d_states), n, d_out,
+            stream);
+    }
+};
+
+}  // namespace AIpStackAmd
+
+#endif

@@ -1,0 +1,109 @@
+/*
+ * aipstack_amd -- MI355X (gfx950) Internet-checksum engine: the C-ABI boundary.
+ *
+ * Plain C, plain pointers and sizes: callable from C, C++, cgo, ctypes, JNI.
+ * Implemented by libaipstack_chksum.so (aipstack_amd/lib/), which holds the host
+ * C++ code and the hand-written CDNA4 HIP kernels.
+ *
+ * Two kinds of entry point:
+ *
+ * 1. The per-packet link-time hook of the reference,
+ *      uint16_t IpChksumInverted(char const *data, size_t len);
+ *    which replaces the inline default in reference src/aipstack/infra/Chksum.h:77-99
+ *    when the consumer compiles with -DAIPSTACK_EXTERNAL_CHKSUM (declaration at
+ *    Chksum.h:50-51; contract at Chksum.h:54-76). This one runs on the HOST: a GPU
+ *    launch (microseconds) costs more than the whole scalar computation of one packet.
+ *
+ * 2. The batch entry points (aipstack_chksum_batch_*): the reference has no batch API
+ *    (every caller -- IpChksum(ptr,len) Chksum.h:122-125, IpChksumAccumulator::addIpBuf
+ *    Chksum.h:283-315 -- processes one packet at a time), so these are new. Each is the
+ *    batched equivalent of a reference call, evaluated for many packets at once on the
+ *    GPU. All pointers named d_* are DEVICE pointers (hipMalloc'd or HIP-registered);
+ *    the work is enqueued on `stream` (a hipStream_t; NULL = the legacy default stream)
+ *    and is complete when the stream is. Nothing here allocates or synchronises.
+ *    There is no CPU fallback: on a host without a usable gfx950 device these return
+ *    AIPSTACK_CHKSUM_EHIP / _ENODEV.
+ *
+ * Results are bit-exact with the reference for every packet whose length satisfies
+ * the reference precondition len <= 65535 (Chksum.h:73-74).
+ */
+#ifndef AIPSTACK_AMD_CHKSUM_H
+#define AIPSTACK_AMD_CHKSUM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes (0 = success, negative = failure) ---------------------------- */
+#define AIPSTACK_CHKSUM_OK      0
+#define AIPSTACK_CHKSUM_EINVAL (-1) /* bad argument: null pointer, len > 65535, n too big */
+#define AIPSTACK_CHKSUM_EHIP   (-2) /* HIP runtime error (see aipstack_chksum_last_hip_error) */
+#define AIPSTACK_CHKSUM_ENODEV (-3) /* no gfx950 device visible to this process */
+
+/* Largest packet length the reference admits (Chksum.h:73-74). */
+#define AIPSTACK_CHKSUM_MAX_LEN 65535u
+
+/* ---- flags for the batch entry points ------------------------------------------ */
+/* Write IpChksum (= ~IpChksumInverted, Chksum.h:122-125) instead of the inverted sum. */
+#define AIPSTACK_CHKSUM_FINAL 1u
+
+/* ---- 1. per-packet host hook ----------------------------------------------------- */
+
+/* Replaces reference Chksum.h:77-99 (declared at Chksum.h:51 under
+ * AIPSTACK_EXTERNAL_CHKSUM). Inverted checksum (ones'-complement sum of big-endian
+ * 16-bit words; odd tail byte padded with a zero low byte) of `len` bytes at `data`,
+ * any alignment. data must not be null; len <= 65535. Pure, reentrant, thread-safe. */
+uint16_t IpChksumInverted(const char *data, size_t len);
+
+/* ---- 2. batch entry points (device-resident, stream-ordered) -------------------- */
+
+/* Fixed-stride batch: packet i is the `len` bytes at d_base + i*stride, for i < n.
+ * d_out[i] = IpChksumInverted(packet i)   (or IpChksum(...) with AIPSTACK_CHKSUM_FINAL).
+ * Batched equivalent of n calls of reference IpChksumInverted (Chksum.h:77-99) /
+ * IpChksum (Chksum.h:122-125). d_base may have any byte alignment. */
+int aipstack_chksum_batch_strided(const void *d_base, uint64_t stride, uint32_t len,
+                                  uint64_t n, uint16_t *d_out, uint32_t flags,
+                                  void *stream);
+
+/* CSR batch: packet i is bytes [d_offsets[i], d_offsets[i+1]) of d_base (n+1 offsets,
+ * non-decreasing, each packet <= 65535 bytes; starts may be odd).
+ * d_out[i] as for the strided form. */
+int aipstack_chksum_batch_csr(const void *d_base, const uint64_t *d_offsets,
+                              uint64_t n, uint16_t *d_out, uint32_t flags,
+                              void *stream);
+
+/* Seeded CSR batch: d_out[i] = IpChksumAccumulator(State{d_states[i]})
+ *                                  .getChksum(IpBufRef{packet i})
+ * i.e. a per-packet saved accumulator state (pseudo-header / header words, exported by
+ * IpChksumAccumulator::getState, Chksum.h:171-184) resumed and completed over the
+ * packet bytes (Chksum.h:263-269, 283-315). Writes the FINAL checksum (as getChksum
+ * does). A state of 0 with no header words is the plain IpChksum(IpBufRef). */
+int aipstack_chksum_batch_seeded_csr(const void *d_base, const uint64_t *d_offsets,
+                                     const uint32_t *d_states, uint64_t n,
+                                     uint16_t *d_out, void *stream);
+
+/* ---- diagnostics ------------------------------------------------------------------ */
+
+/* Static description of a status code. Never NULL. */
+const char *aipstack_chksum_strerror(int status);
+
+/* hipError_t of the most recent failing HIP call made by this library on the calling
+ * thread (0 if none). */
+int aipstack_chksum_last_hip_error(void);
+
+/* AIPSTACK_CHKSUM_OK if `device` is a gfx950 device this library can launch on,
+ * else _ENODEV (or _EHIP if the HIP runtime itself fails). */
+int aipstack_chksum_device_check(int device);
+
+/* ABI version of this header: bumped on any incompatible change. */
+#define AIPSTACK_CHKSUM_ABI_VERSION 1
+int aipstack_chksum_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* AIPSTACK_AMD_CHKSUM_H */

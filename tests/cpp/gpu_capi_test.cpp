@@ -1,0 +1,135 @@
+// GPU parity test in plain C++ over the C-ABI (include/aipstack_amd/chksum.h): device
+// buffers from hipMalloc, work on a user hipStream_t, results checked against the C
+// oracle (oracle/chksum_oracle.c, linked in as the checker). Exercises exactly what a C++
+// consumer of libaipstack_chksum.so would do. Exit 0 = pass.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include "aipstack_amd/chksum.h"
+#include "aipstack_amd/synth.h"
+#include "chksum_oracle.h"
+
+#define HIP_OK(x)                                                                  \
+    do {                                                                           \
+        hipError_t e_ = (x);                                                       \
+        if (e_ != hipSuccess) {                                                    \
+            std::fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e_), \
+                         __FILE__, __LINE__);                                      \
+            std::exit(2);                                                          \
+        }                                                                          \
+    } while (0)
+
+static int failures = 0;
+#define EXPECT(cond, ...)                        \
+    do {                                         \
+        if (!(cond)) {                           \
+            std::fprintf(stderr, __VA_ARGS__);   \
+            std::fprintf(stderr, "\n");          \
+            if (++failures > 20) std::exit(1);   \
+        }                                        \
+    } while (0)
+
+int main() {
+    if (aipstack_chksum_device_check(0) != AIPSTACK_CHKSUM_OK) {
+        std::fprintf(stderr, "device 0 is not a usable gfx950 device\n");
+        return 3;
+    }
+    hipStream_t stream;
+    HIP_OK(hipStreamCreate(&stream));
+
+    // ---- strided, odd base pointers, lengths around segment boundaries
+    const uint64_t cap = 192ull << 20;
+    std::vector<unsigned char> h(cap + 64);
+    aipstack_synth_fill_host(h.data(), h.size(), 7, 0);
+    unsigned char *d = nullptr;
+    HIP_OK(hipMalloc(&d, h.size()));
+    HIP_OK(hipMemcpy(d, h.data(), h.size(), hipMemcpyHostToDevice));
+    uint16_t *dout = nullptr;
+    HIP_OK(hipMalloc(&dout, 200000 * sizeof(uint16_t)));
+    std::vector<uint16_t> got(200000), want(200000);
+    const uint32_t lens[] = {0, 1, 2, 15, 16, 17, 63, 64, 65, 1023, 1024, 1025, 1500, 2047, 9000, 65535};
+    const uint64_t bases[] = {0, 1, 2, 3, 7, 12, 15};
+    for (uint32_t len : lens) {
+        for (uint64_t b : bases) {
+            for (uint64_t stride : {uint64_t(len), uint64_t(len) + 3, uint64_t(1500)}) {
+                if (stride == 0) stride = 1;
+                uint64_t n = (cap - b - len) / stride;
+                if (n > 130) n = 130 + (len % 7);
+                for (uint32_t flags : {0u, 1u}) {
+                    int st = aipstack_chksum_batch_strided(d + b, stride, len, n, dout, flags, stream);
+                    EXPECT(st == 0, "strided launch failed %d", st);
+                    HIP_OK(hipMemcpyAsync(got.data(), dout, n * 2, hipMemcpyDeviceToHost, stream));
+                    HIP_OK(hipStreamSynchronize(stream));
+                    oracle_batch_strided(h.data() + b, stride, len, n, want.data(), flags);
+                    for (uint64_t i = 0; i < n; i++)
+                        EXPECT(got[i] == want[i], "strided len=%u base=%lu stride=%lu i=%lu got %04x want %04x",
+                               len, (unsigned long)b, (unsigned long)stride, (unsigned long)i, got[i], want[i]);
+                }
+            }
+        }
+    }
+
+    // ---- CSR with empty, odd, and maximum-length packets
+    std::mt19937_64 rng(99);
+    const uint64_t n = 100000;
+    std::vector<uint64_t> off(n + 1);
+    off[0] = 5;
+    for (uint64_t i = 0; i < n; i++) {
+        uint64_t r = rng() % 100;
+        uint64_t len = r < 3 ? 0 : r < 4 ? 65535 - (rng() % 2) : r < 20 ? rng() % 64 : rng() % 1600;
+        if (off[i] + len > cap) len = 0;
+        off[i + 1] = off[i] + len;
+    }
+    uint64_t *doff = nullptr;
+    HIP_OK(hipMalloc(&doff, (n + 1) * sizeof(uint64_t)));
+    HIP_OK(hipMemcpy(doff, off.data(), (n + 1) * 8, hipMemcpyHostToDevice));
+    for (uint32_t flags : {0u, 1u}) {
+        int st = aipstack_chksum_batch_csr(d, doff, n, dout, flags, stream);
+        EXPECT(st == 0, "csr launch failed %d", st);
+        HIP_OK(hipMemcpyAsync(got.data(), dout, n * 2, hipMemcpyDeviceToHost, stream));
+        HIP_OK(hipStreamSynchronize(stream));
+        oracle_batch_csr(h.data(), off.data(), n, want.data(), flags);
+        for (uint64_t i = 0; i < n; i++)
+            EXPECT(got[i] == want[i], "csr i=%lu len=%lu got %04x want %04x", (unsigned long)i,
+                   (unsigned long)(off[i + 1] - off[i]), got[i], want[i]);
+    }
+
+    // ---- seeded CSR (IpChksumAccumulator(State).getChksum(packet))
+    std::vector<uint32_t> states(n);
+    for (auto &s : states) s = (rng() % 4 == 0) ? 0xFFFFFFFFu - (uint32_t)(rng() % 3) : (uint32_t)rng();
+    uint32_t *dstates = nullptr;
+    HIP_OK(hipMalloc(&dstates, n * 4));
+    HIP_OK(hipMemcpy(dstates, states.data(), n * 4, hipMemcpyHostToDevice));
+    int st = aipstack_chksum_batch_seeded_csr(d, doff, dstates, n, dout, stream);
+    EXPECT(st == 0, "seeded launch failed %d", st);
+    HIP_OK(hipMemcpyAsync(got.data(), dout, n * 2, hipMemcpyDeviceToHost, stream));
+    HIP_OK(hipStreamSynchronize(stream));
+    oracle_batch_seeded_csr(h.data(), off.data(), states.data(), n, want.data());
+    for (uint64_t i = 0; i < n; i++)
+        EXPECT(got[i] == want[i], "seeded i=%lu got %04x want %04x", (unsigned long)i, got[i], want[i]);
+
+    // ---- argument errors are reported, not executed
+    EXPECT(aipstack_chksum_batch_strided(nullptr, 1, 1, 1, dout, 0, stream) == AIPSTACK_CHKSUM_EINVAL, "null base");
+    EXPECT(aipstack_chksum_batch_strided(d, 1, 65536, 1, dout, 0, stream) == AIPSTACK_CHKSUM_EINVAL, "len > 65535");
+    EXPECT(aipstack_chksum_batch_csr(d, nullptr, 1, dout, 0, stream) == AIPSTACK_CHKSUM_EINVAL, "null offsets");
+    EXPECT(aipstack_chksum_batch_strided(d, 1, 1, 0, nullptr, 0, stream) == AIPSTACK_CHKSUM_OK, "n = 0 is a no-op");
+
+    HIP_OK(hipStreamSynchronize(stream));
+    HIP_OK(hipFree(d));
+    HIP_OK(hipFree(dout));
+    HIP_OK(hipFree(doff));
+    HIP_OK(hipFree(dstates));
+    HIP_OK(hipStreamDestroy(stream));
+    if (failures) {
+        std::fprintf(stderr, "gpu_capi_test: %d failures\n", failures);
+        return 1;
+    }
+    std::printf("gpu_capi_test: OK\n");
+    return 0;
+}

@@ -1,0 +1,236 @@
+"""GPU parity: every batch entry point of libaipstack_chksum.so (through the C-ABI) against
+the oracle and the reference's golden vectors -- bit-exact, as required for integer work.
+
+Covers the BASELINE configs at full size (A: 1M x 1500 B, B: 256K x 9000 B, C: 2M mixed
+64-1500 B with odd lengths/starts and all-0x00 / all-0xFF / sum=0 mod 0xFFFF packets, D:
+a 1M shard of the 8-GPU batch) plus the edge cases the reference contract admits: empty
+batches and packets, ragged counts, odd base pointers, len 65535, FINAL flag, seeds.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import aipstack_amd as A
+from aipstack_amd import synth
+from conftest import ROOT
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    assert A.device_check(0) == A.AIPSTACK_CHKSUM_OK, "device 0 is not gfx950"
+
+
+def _d(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def _np(t):
+    return t.cpu().numpy()
+
+
+def test_native_library_loaded_in_process():
+    maps = open("/proc/self/maps").read()
+    assert os.path.join("aipstack_amd", "lib", "libaipstack_chksum.so") in maps
+
+
+def test_golden_flat_cases_strided_n1(golden):
+    """Each reference golden case (start, len) as a 1-packet strided launch."""
+    b = golden["blob"]
+    db = _d(b)
+    cases = golden["flat"]["flat"]
+    out = torch.empty(len(cases), dtype=torch.uint16, device=DEV)
+    fin = torch.empty(len(cases), dtype=torch.uint16, device=DEV)
+    for i, (o, l, _, _) in enumerate(cases):
+        A.chksum_batch_strided(db, max(l, 1), l, 1, out=out[i:], byte_offset=o)
+        A.chksum_batch_strided(db, max(l, 1), l, 1, out=fin[i:], byte_offset=o, final=True)
+    got, gotf = _np(out), _np(fin)
+    want = np.array([c[2] for c in cases], dtype=np.uint16)
+    wantf = np.array([c[3] for c in cases], dtype=np.uint16)
+    bad = np.nonzero((got != want) | (gotf != wantf))[0]
+    assert bad.size == 0, [cases[i] for i in bad[:10]]
+
+
+def test_golden_batch_fixtures_device_generated(golden):
+    bc = golden["batch"]
+    m = bc["mixed_csr"]
+    off = synth.mixed_offsets(m["n"], m["len_seed"])
+    buf = torch.empty(int(off[-1]), dtype=torch.uint8, device=DEV)
+    synth.fill_device(buf, m["data_seed"])
+    doff = _d(off)
+    synth.apply_classes_device(buf, doff, m["len_seed"])
+    assert _np(A.chksum_batch_csr(buf, doff)).tolist() == m["inverted"]
+    for name in ("strided_1500", "strided_9000"):
+        c = bc[name]
+        buf = torch.empty(c["stride"] * c["n"], dtype=torch.uint8, device=DEV)
+        synth.fill_device(buf, c["data_seed"])
+        got = _np(A.chksum_batch_strided(buf, c["stride"], c["len"], c["n"]))
+        assert got.tolist() == c["inverted"]
+
+
+def test_device_generator_matches_host():
+    buf = torch.empty(1 << 20, dtype=torch.uint8, device=DEV)
+    for off in (0, 3, 4096, 12345):
+        synth.fill_device(buf, 42, off)
+        assert np.array_equal(_np(buf), synth.random_bytes(42, 1 << 20, off))
+
+
+@pytest.mark.parametrize("cfg,n,plen", [("A", 1 << 20, 1500), ("B", 256 << 10, 9000)])
+def test_full_size_strided(oracle, cfg, n, plen):
+    buf = torch.empty(n * plen, dtype=torch.uint8, device=DEV)
+    synth.fill_device(buf, synth.SEED_DATA)
+    got = _np(A.chksum_batch_strided(buf, plen, plen, n))
+    host = _np(buf)
+    want = oracle.batch_strided(host, plen, plen, n)
+    assert np.array_equal(got, want), f"config {cfg}: {np.count_nonzero(got != want)} mismatches"
+    # idempotence: a second launch gives the same result
+    assert np.array_equal(_np(A.chksum_batch_strided(buf, plen, plen, n)), got)
+    # FINAL flag = bitwise NOT, packet for packet
+    fin = _np(A.chksum_batch_strided(buf, plen, plen, n, final=True))
+    assert np.array_equal(fin, ~got)
+
+
+def test_full_size_mixed_csr(oracle):
+    n = 2 << 20
+    off = synth.mixed_offsets(n)
+    buf = torch.empty(int(off[-1]), dtype=torch.uint8, device=DEV)
+    synth.fill_device(buf, synth.SEED_DATA)
+    doff = _d(off)
+    synth.apply_classes_device(buf, doff)
+    got = _np(A.chksum_batch_csr(buf, doff))
+    host = _np(buf)
+    want = oracle.batch_csr(host, off)
+    assert np.array_equal(got, want), f"{np.count_nonzero(got != want)} mismatches"
+    cls = synth.mixed_classes(n)
+    lens = np.diff(off)
+    assert np.all(got[cls == 1] == 0x0000)          # all-zero packets
+    assert np.all(got[cls == 2] == 0xFFFF)          # nonzero, sum = 0 mod 0xFFFF
+    ff = (cls == 0)
+    assert np.all(got[ff & (lens % 2 == 0)] == 0xFFFF)  # k * 0xFFFF
+    assert np.all(got[ff & (lens % 2 == 1)] == 0xFF00)  # k * 0xFFFF + 0xFF00 tail
+    assert np.any(off[:-1] % 2 == 1) and np.any(lens % 2 == 1)
+
+
+def test_config_d_shard_of_8(oracle):
+    """Rank 7's shard of the 8-GPU batch (packets [7M, 8M)) as bench.py builds it."""
+    n, plen, rank = 1 << 20, 1500, 7
+    buf = torch.empty(n * plen, dtype=torch.uint8, device=DEV)
+    synth.fill_device(buf, synth.SEED_DATA, rank * n * plen)
+    got = _np(A.chksum_batch_strided(buf, plen, plen, n))
+    want = oracle.batch_strided(_np(buf), plen, plen, n)
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 127, 129, 1000, 4097])
+@pytest.mark.parametrize("base", [0, 1, 2, 3, 5, 8, 13])
+def test_ragged_counts_and_odd_bases(oracle, n, base):
+    plen = 1500 if n % 2 else 1499
+    buf = torch.empty(n * plen + 64, dtype=torch.uint8, device=DEV)
+    synth.fill_device(buf, 9)
+    got = _np(A.chksum_batch_strided(buf, plen, plen, n, byte_offset=base))
+    want = oracle.batch_strided(_np(buf), plen, plen, n, base_off=base)
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("plen", [0, 1, 2, 3, 15, 16, 17, 31, 33, 1023, 1024, 1025, 2032,
+                                  2033, 4095, 8999, 9001, 16383, 65534, 65535])
+def test_lengths(oracle, plen):
+    n = 300
+    stride = max(plen, 1) + 7   # overlapping-free, misaligned starts
+    buf = torch.empty(n * stride + 64, dtype=torch.uint8, device=DEV)
+    synth.fill_device(buf, plen + 1)
+    got = _np(A.chksum_batch_strided(buf, stride, plen, n, byte_offset=3))
+    want = oracle.batch_strided(_np(buf), stride, plen, n, base_off=3)
+    assert np.array_equal(got, want)
+
+
+def test_overlapping_and_zero_stride(oracle):
+    buf = torch.empty(70000, dtype=torch.uint8, device=DEV)
+    synth.fill_device(buf, 77)
+    for stride, plen in ((1, 1500), (3, 65535), (0, 777), (2, 9000)):
+        n = 200
+        got = _np(A.chksum_batch_strided(buf, stride, plen, n))
+        want = oracle.batch_strided(_np(buf), stride, plen, n)
+        assert np.array_equal(got, want), (stride, plen)
+
+
+def test_all_zero_and_all_ff_batches():
+    for fill, want in ((0x00, 0x0000), (0xFF, 0xFFFF)):
+        buf = torch.full((1500 * 4096,), fill, dtype=torch.uint8, device=DEV)
+        got = _np(A.chksum_batch_strided(buf, 1500, 1500, 4096))
+        assert np.all(got == want)
+        got = _np(A.chksum_batch_strided(buf, 1500, 1499, 4096, byte_offset=1))
+        assert np.all(got == (0x0000 if fill == 0 else 0xFF00))  # odd: + 0xFF00 tail
+
+
+def test_csr_empty_and_long_packets(oracle):
+    rng = np.random.default_rng(3)
+    n = 50000
+    lens = rng.choice([0, 0, 1, 2, 3, 64, 1500, 9000, 65535], size=n,
+                      p=[.2, .05, .1, .1, .05, .2, .2, .08, .02])
+    off = np.zeros(n + 1, dtype=np.int64)
+    off[0] = 1
+    np.cumsum(lens, out=off[1:])
+    off[1:] += 1
+    buf = torch.empty(int(off[-1]) + 16, dtype=torch.uint8, device=DEV)
+    synth.fill_device(buf, 5)
+    got = _np(A.chksum_batch_csr(buf, _d(off)))
+    want = oracle.batch_csr(_np(buf), off)
+    assert np.array_equal(got, want)
+    assert np.all(got[lens == 0] == 0)
+    fin = _np(A.chksum_batch_csr(buf, _d(off), final=True))
+    assert np.array_equal(fin, ~want)
+
+
+def test_seeded_csr(oracle, golden):
+    n = 100000
+    off = synth.mixed_offsets(n, 11)
+    buf = torch.empty(int(off[-1]), dtype=torch.uint8, device=DEV)
+    synth.fill_device(buf, 12)
+    rng = np.random.default_rng(4)
+    states = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
+    states[::7] = 0xFFFFFFFF
+    states[1::7] = 0
+    got = _np(A.chksum_batch_seeded_csr(buf, _d(off), _d(states.view(np.int32))))
+    want = oracle.batch_seeded_csr(_np(buf), off, states)
+    assert np.array_equal(got, want)
+
+
+def test_seeded_against_reference_accumulate_golden(golden):
+    """IpChksumAccumulator header state (exported by the reference) + payload on the GPU."""
+    b = golden["blob"]
+    cases = golden["chain"]["accumulate"]
+    db = _d(b)
+    for c in cases:
+        po, pl = c["payload"]
+        off = _d(np.array([po, po + pl], dtype=np.int64))
+        st = _d(np.array([c["state"]], dtype=np.uint32).view(np.int32))
+        got = int(_np(A.chksum_batch_seeded_csr(db, off, st))[0])
+        assert got == c["chksum"], c
+
+
+def test_stream_ordering_user_stream(oracle):
+    s = torch.cuda.Stream()
+    n, plen = 20000, 1500
+    buf = torch.empty(n * plen, dtype=torch.uint8, device=DEV)
+    with torch.cuda.stream(s):
+        synth.fill_device(buf, 31, stream=s)
+        out = A.chksum_batch_strided(buf, plen, plen, n, stream=s)
+    s.synchronize()
+    assert np.array_equal(_np(out), oracle.batch_strided(_np(buf), plen, plen, n))
+
+
+def test_cpp_capi_program():
+    exe = os.path.join(ROOT, "tests", "cpp", "build", "gpu_capi_test")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "tests", "cpp"), "gpu"], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "OK" in r.stdout
