@@ -31,6 +31,7 @@ SIGNATURES = {
     "aipstack_chksum_last_hip_error": (_c_int, []),
     "aipstack_chksum_device_check": (_c_int, [_c_int]),
     "aipstack_chksum_abi_version": (_c_int, []),
+    "aipstack_chksum_tune": (_c_int, [ctypes.c_char_p, _c_int]),
     # synth.h
     "aipstack_synth_fill_host": (None, [_c_vp, _c_u64, _c_u64, _c_u64]),
     "aipstack_synth_mixed_offsets_host": (_c_u64, [_c_vp, _c_u64, _c_u64]),

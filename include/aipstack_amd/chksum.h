@@ -98,6 +98,12 @@ int aipstack_chksum_last_hip_error(void);
  * else _ENODEV (or _EHIP if the HIP runtime itself fails). */
 int aipstack_chksum_device_check(int device);
 
+/* Launch tunables, for benchmark sweeps (0 = automatic). Keys: "waves_per_cu",
+ * "chunks_per_wave", "unroll" (segments per lane issued up front, 1..4), "packets"
+ * (packets a wave keeps in flight: 1, 2, 4, 8), "nontemporal" (0/1). Process-wide;
+ * results never depend on them. Returns _OK or _EINVAL for an unknown key. */
+int aipstack_chksum_tune(const char *key, int value);
+
 /* ABI version of this header: bumped on any incompatible change. */
 #define AIPSTACK_CHKSUM_ABI_VERSION 1
 int aipstack_chksum_abi_version(void);

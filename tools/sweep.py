@@ -1,0 +1,136 @@
+#!/usr/bin/env python3
+"""Launch-parameter sweep of the batch checksum kernel, interleaved in ONE process.
+
+Each variant sets the library tunables (aipstack_chksum_tune), launches the batch, and is
+timed with HIP events on the launch stream; variants are interleaved round by round (so
+clock/thermal drift hits all of them alike) and every variant's output is checked equal
+to the first one's and, for a prefix, to the oracle. Prints one JSON object per variant
+(median/min kernel us, GB/s of algorithmic bytes, fraction of 8 TB/s) to stdout.
+
+    python tools/sweep.py --config A --rounds 8 [--variants "U,P,NT,WPC;..."]
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+DEFAULT_VARIANTS = {
+    "A": "0,0,1,0;2,1,1,0;2,2,1,0;2,4,1,0;2,8,1,0;2,4,0,0;2,8,0,0;2,4,1,32;2,4,1,128;"
+         "2,8,1,32;2,8,1,128;3,4,1,0;3,2,1,0",
+    "B": "0,0,1,0;3,1,1,0;3,2,1,0;3,4,1,0;3,2,0,0;4,1,1,0;4,2,1,0;2,4,1,0;2,2,1,0;3,2,1,32;"
+         "3,2,1,128;3,4,1,128",
+    "C": "0,0,1,0;2,1,1,0;2,2,1,0;2,4,1,0;1,1,1,0;1,2,1,0;1,4,1,0;2,1,0,0;2,1,1,128;"
+         "2,1,1,256;2,2,1,128;1,2,1,128",
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="A", choices=["A", "B", "C"])
+    ap.add_argument("--rounds", type=int, default=8)
+    ap.add_argument("--reps", type=int, default=5, help="launches per variant per round")
+    ap.add_argument("--variants", default=None, help='"U,P,NT,WPC;..." (0 = automatic)')
+    args = ap.parse_args()
+
+    import torch
+
+    import aipstack_amd as A
+    from aipstack_amd import _lib, synth
+    lib = _lib.load()
+
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream()
+    if args.config == "A":
+        n, plen, layout = 1 << 20, 1500, "strided"
+    elif args.config == "B":
+        n, plen, layout = 256 << 10, 9000, "strided"
+    else:
+        n, plen, layout = 2 << 20, None, "csr"
+    if layout == "strided":
+        total = n * plen
+        buf = torch.empty(total, dtype=torch.uint8, device=dev)
+        synth.fill_device(buf, synth.SEED_DATA)
+        alg = total + 2 * n
+    else:
+        off = synth.mixed_offsets(n)
+        total = int(off[-1])
+        buf = torch.empty(total, dtype=torch.uint8, device=dev)
+        synth.fill_device(buf, synth.SEED_DATA)
+        d_off = torch.from_numpy(off).to(dev)
+        synth.apply_classes_device(buf, d_off)
+        alg = total + 2 * n + 8 * (n + 1)
+    out = torch.empty(n, dtype=torch.uint16, device=dev)
+
+    def run():
+        if layout == "strided":
+            A.chksum_batch_strided(buf, plen, plen, n, out=out, stream=stream)
+        else:
+            A.chksum_batch_csr(buf, d_off, out=out, stream=stream)
+
+    variants = []
+    for v in (args.variants or DEFAULT_VARIANTS[args.config]).split(";"):
+        u, p, nt, wpc = (int(x) for x in v.split(","))
+        variants.append({"unroll": u, "packets": p, "nontemporal": nt, "waves_per_cu": wpc})
+
+    def apply(v):
+        for k, val in v.items():
+            assert lib.aipstack_chksum_tune(k.encode(), val) == 0
+        lib.aipstack_chksum_tune(b"chunks_per_wave", 0)
+
+    # reference output: oracle on a prefix
+    orc = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "libchksum_oracle.so"))
+    host = buf.cpu().numpy()
+    m = min(n, 65536)
+    want = np.empty(m, dtype=np.uint16)
+    if layout == "strided":
+        orc.oracle_batch_strided.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                                             ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32]
+        orc.oracle_batch_strided(host.ctypes.data, plen, plen, m, want.ctypes.data, 0)
+    else:
+        orc.oracle_batch_csr.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                         ctypes.c_void_p, ctypes.c_uint32]
+        o = off[:m + 1].astype(np.uint64)
+        orc.oracle_batch_csr(host.ctypes.data, o.ctypes.data, m, want.ctypes.data, 0)
+
+    first = None
+    times = [[] for _ in variants]
+    ok = [True] * len(variants)
+    for vi, v in enumerate(variants):  # warm-up + correctness per variant
+        apply(v)
+        run()
+        run()
+        torch.cuda.synchronize()
+        got = out.cpu().numpy()
+        if first is None:
+            first = got.copy()
+        ok[vi] = bool(np.array_equal(got, first) and np.array_equal(got[:m], want))
+    for _ in range(args.rounds):
+        for vi, v in enumerate(variants):
+            apply(v)
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                  for _ in range(args.reps)]
+            for s, e in ev:
+                s.record(stream)
+                run()
+                e.record(stream)
+            torch.cuda.synchronize()
+            times[vi].extend(s.elapsed_time(e) * 1e3 for s, e in ev)
+    for v, t, good in zip(variants, times, ok):
+        med = float(np.median(t))
+        print(json.dumps({"config": args.config, **v, "median_us": round(med, 2),
+                          "min_us": round(float(np.min(t)), 2),
+                          "GBps": round(alg / med / 1e3, 1),
+                          "frac_8TBps": round(alg / med / 1e3 / 8000.0, 4), "parity": good}),
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()
