@@ -16,6 +16,7 @@ from .chksum import (  # noqa: E402
     AIPSTACK_CHKSUM_FINAL,
     AIPSTACK_CHKSUM_MAX_LEN,
     AIPSTACK_CHKSUM_OK,
+    ChksumEngine,
     ChksumError,
     IpBufNode,
     IpBufRef,
@@ -33,7 +34,8 @@ LIB_PATH = _lib.LIB_PATH
 
 __all__ = [
     "AIPSTACK_CHKSUM_EHIP", "AIPSTACK_CHKSUM_EINVAL", "AIPSTACK_CHKSUM_ENODEV",
-    "AIPSTACK_CHKSUM_FINAL", "AIPSTACK_CHKSUM_MAX_LEN", "AIPSTACK_CHKSUM_OK", "ChksumError",
+    "AIPSTACK_CHKSUM_FINAL", "AIPSTACK_CHKSUM_MAX_LEN", "AIPSTACK_CHKSUM_OK", "ChksumEngine",
+    "ChksumError",
     "IpBufNode", "IpBufRef", "IpChksum", "IpChksumAccumulator", "IpChksumInverted",
     "chksum_batch_csr", "chksum_batch_seeded_csr", "chksum_batch_strided", "device_check",
     "ipBufProcessBytes", "LIB_PATH",

@@ -32,6 +32,12 @@ SIGNATURES = {
     "aipstack_chksum_device_check": (_c_int, [_c_int]),
     "aipstack_chksum_abi_version": (_c_int, []),
     "aipstack_chksum_tune": (_c_int, [ctypes.c_char_p, _c_int]),
+    "aipstack_chksum_engine_create": (_c_int, [_c_int, _c_u64, _c_int, ctypes.POINTER(_c_vp)]),
+    "aipstack_chksum_engine_destroy": (None, [_c_vp]),
+    "aipstack_chksum_engine_register": (_c_int, [_c_vp, _c_vp, _c_u64]),
+    "aipstack_chksum_engine_unregister": (_c_int, [_c_vp, _c_vp]),
+    "aipstack_chksum_engine_host_strided": (_c_int, [_c_vp, _c_vp, _c_u64, _c_u32, _c_u64, _c_vp, _c_u32]),
+    "aipstack_chksum_engine_host_csr": (_c_int, [_c_vp, _c_vp, _c_vp, _c_u64, _c_vp, _c_u32]),
     # synth.h
     "aipstack_synth_fill_host": (None, [_c_vp, _c_u64, _c_u64, _c_u64]),
     "aipstack_synth_mixed_offsets_host": (_c_u64, [_c_vp, _c_u64, _c_u64]),

@@ -22,6 +22,7 @@ device-memory / stream plumbing here; there is no CPU fallback for the batch cal
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Callable, Optional
 
 import numpy as np
@@ -322,6 +323,72 @@ def chksum_batch_seeded_csr(buf, offsets, states, *, out=None, stream=None):
         _stream_handle(stream))
     _check(st, "aipstack_chksum_batch_seeded_csr")
     return out
+
+
+class ChksumEngine:
+    """Host-memory streaming engine (C-ABI ``aipstack_chksum_engine_*``): checksums
+    batches held in HOST memory (numpy arrays) and returns results in host memory,
+    pipelining H2D / kernel / D2H over ``nstreams`` HIP streams."""
+
+    def __init__(self, device: int = 0, chunk_bytes: int = 0, nstreams: int = 2):
+        self._lib = _lib.load()
+        h = ctypes.c_void_p()
+        _check(self._lib.aipstack_chksum_engine_create(device, chunk_bytes, nstreams,
+                                                       ctypes.byref(h)),
+               "aipstack_chksum_engine_create")
+        self._h = h
+        self._registered = []
+
+    def close(self) -> None:
+        if self._h:
+            self._lib.aipstack_chksum_engine_destroy(self._h)
+            self._h = None
+            self._registered = []
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def register(self, arr: np.ndarray) -> None:
+        """Page-lock `arr` (kept alive by the engine) so batches in it are DMA'd directly."""
+        _check(self._lib.aipstack_chksum_engine_register(self._h, arr.ctypes.data, arr.nbytes),
+               "aipstack_chksum_engine_register")
+        self._registered.append(arr)
+
+    def unregister(self, arr: np.ndarray) -> None:
+        _check(self._lib.aipstack_chksum_engine_unregister(self._h, arr.ctypes.data),
+               "aipstack_chksum_engine_unregister")
+        self._registered = [a for a in self._registered if a is not arr]
+
+    def strided(self, buf: np.ndarray, stride: int, length: int, n: int, *, out=None,
+                final: bool = False) -> np.ndarray:
+        if n and (n - 1) * stride + length > buf.nbytes:
+            raise ValueError("batch exceeds buf")
+        out = np.empty(n, dtype=np.uint16) if out is None else out
+        _check(self._lib.aipstack_chksum_engine_host_strided(
+            self._h, buf.ctypes.data, stride, length, n, out.ctypes.data,
+            AIPSTACK_CHKSUM_FINAL if final else 0), "aipstack_chksum_engine_host_strided")
+        return out
+
+    def csr(self, buf: np.ndarray, offsets: np.ndarray, *, out=None,
+            final: bool = False) -> np.ndarray:
+        o = np.ascontiguousarray(offsets, dtype=np.uint64)
+        n = o.size - 1
+        if n > 0 and int(o[-1]) > buf.nbytes:
+            raise ValueError("offsets exceed buf")
+        out = np.empty(max(n, 0), dtype=np.uint16) if out is None else out
+        _check(self._lib.aipstack_chksum_engine_host_csr(
+            self._h, buf.ctypes.data, o.ctypes.data, n, out.ctypes.data,
+            AIPSTACK_CHKSUM_FINAL if final else 0), "aipstack_chksum_engine_host_csr")
+        return out
 
 
 def device_check(device: int = 0) -> int:

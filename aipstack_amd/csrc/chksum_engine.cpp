@@ -1,0 +1,262 @@
+// aipstack_amd -- host-memory streaming engine.
+//
+// The reference's packet path starts and ends in host memory: a TAP read() fills one host
+// buffer per frame (reference tap/linux/TapDeviceLinux.cpp:156-178) and write() sends one
+// (:122-127). This engine checksums batches that live in HOST memory and returns the
+// results to HOST memory, overlapping the PCIe transfers with the kernels:
+//
+//   chunk i (a run of whole packets, <= chunk_bytes) on stream i % nstreams:
+//     H2D (packet bytes [, offsets])  ->  batch kernel  ->  D2H (2 B per packet)
+//
+// Host buffers that were registered with aipstack_chksum_engine_register() (page-locked
+// via hipHostRegister, as a TAP/socket ring would be once at start-up) are copied by DMA
+// straight from the caller's memory; other host memory is first copied on the CPU into
+// pinned staging (the slower "pageable" path). Each call is synchronous for the caller.
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "aipstack_amd/chksum.h"
+#include "chksum_internal.h"
+
+using namespace aipstack_amd;
+
+namespace {
+
+struct Slot {
+    hipStream_t stream = nullptr;
+    void *d_bytes = nullptr;       // device staging for packet bytes
+    uint64_t *d_off = nullptr;     // device staging for CSR offsets
+    uint16_t *d_out = nullptr;     // device results
+    void *h_stage = nullptr;       // pinned host staging (pageable inputs)
+    uint64_t *h_off = nullptr;     // pinned host staging for rebased offsets
+    uint16_t *h_out = nullptr;     // pinned host results
+    hipEvent_t done = nullptr;
+    bool busy = false;
+    uint16_t *user_out = nullptr;  // where h_out goes once the slot completes
+    uint64_t count = 0;
+};
+
+struct Region {
+    const char *p;
+    uint64_t bytes;
+};
+
+}  // namespace
+
+struct aipstack_chksum_engine {
+    int device = 0;
+    uint64_t chunk_bytes = 0;
+    uint64_t chunk_packets = 0;
+    std::vector<Slot> slots;
+    std::vector<Region> registered;
+    std::mutex mu;  // one batch at a time per engine
+};
+
+namespace {
+
+bool is_registered(const aipstack_chksum_engine *e, const void *p, uint64_t bytes) {
+    const char *c = static_cast<const char *>(p);
+    for (const Region &r : e->registered)
+        if (c >= r.p && c + bytes <= r.p + r.bytes) return true;
+    return false;
+}
+
+void release(aipstack_chksum_engine *e) {
+    for (Slot &s : e->slots) {
+        if (s.stream) (void)hipStreamSynchronize(s.stream);
+        if (s.d_bytes) (void)hipFree(s.d_bytes);
+        if (s.d_off) (void)hipFree(s.d_off);
+        if (s.d_out) (void)hipFree(s.d_out);
+        if (s.h_stage) (void)hipHostFree(s.h_stage);
+        if (s.h_off) (void)hipHostFree(s.h_off);
+        if (s.h_out) (void)hipHostFree(s.h_out);
+        if (s.done) (void)hipEventDestroy(s.done);
+        if (s.stream) (void)hipStreamDestroy(s.stream);
+    }
+    for (const Region &r : e->registered) (void)hipHostUnregister(const_cast<char *>(r.p));
+}
+
+// Wait for slot s to finish and hand its results to the caller.
+int drain(Slot &s) {
+    if (!s.busy) return AIPSTACK_CHKSUM_OK;
+    int st = check_hip(hipEventSynchronize(s.done));
+    if (st == AIPSTACK_CHKSUM_OK) std::memcpy(s.user_out, s.h_out, s.count * sizeof(uint16_t));
+    s.busy = false;
+    return st;
+}
+
+// Pipeline over chunks. next(i0, &i1, &src, &bytes, &dst_base_shift) describes chunk
+// [i0, i1) of packets and its byte range in host memory.
+template <class Chunker, class Launch>
+int pipeline(aipstack_chksum_engine *e, uint64_t n, uint16_t *h_out, Chunker chunker,
+             Launch launch) {
+    std::lock_guard<std::mutex> lock(e->mu);
+    if (hipSetDevice(e->device) != hipSuccess) return AIPSTACK_CHKSUM_ENODEV;
+    int status = AIPSTACK_CHKSUM_OK;
+    uint64_t i0 = 0;
+    size_t k = 0;
+    while (i0 < n && status == AIPSTACK_CHKSUM_OK) {
+        Slot &s = e->slots[k % e->slots.size()];
+        ++k;
+        status = drain(s);
+        if (status != AIPSTACK_CHKSUM_OK) break;
+        uint64_t i1 = 0;
+        const char *src = nullptr;
+        uint64_t bytes = 0;
+        chunker(i0, &i1, &src, &bytes);
+        const uint64_t cnt = i1 - i0;
+        const void *h_src = src;
+        if (bytes && !is_registered(e, src, bytes)) {  // pageable: CPU copy into pinned
+            std::memcpy(s.h_stage, src, bytes);
+            h_src = s.h_stage;
+        }
+        if (bytes)
+            status = check_hip(hipMemcpyAsync(s.d_bytes, h_src, bytes, hipMemcpyHostToDevice,
+                                              s.stream));
+        if (status == AIPSTACK_CHKSUM_OK) status = launch(s, i0, i1);
+        if (status == AIPSTACK_CHKSUM_OK)
+            status = check_hip(hipMemcpyAsync(s.h_out, s.d_out, cnt * sizeof(uint16_t),
+                                              hipMemcpyDeviceToHost, s.stream));
+        if (status == AIPSTACK_CHKSUM_OK) status = check_hip(hipEventRecord(s.done, s.stream));
+        s.busy = status == AIPSTACK_CHKSUM_OK;
+        s.user_out = h_out + i0;
+        s.count = cnt;
+        i0 = i1;
+    }
+    for (Slot &s : e->slots) {
+        const int st = drain(s);
+        if (status == AIPSTACK_CHKSUM_OK) status = st;
+    }
+    return status;
+}
+
+}  // namespace
+
+extern "C" int aipstack_chksum_engine_create(int device, uint64_t chunk_bytes, int nstreams,
+                                             aipstack_chksum_engine **out) {
+    if (!out || nstreams < 1 || nstreams > 16) return AIPSTACK_CHKSUM_EINVAL;
+    *out = nullptr;
+    if (chunk_bytes == 0) chunk_bytes = 64ull << 20;
+    if (chunk_bytes < (1u << 17)) chunk_bytes = 1u << 17;  // >= 2 max-size packets
+    const int dc = aipstack_chksum_device_check(device);
+    if (dc != AIPSTACK_CHKSUM_OK) return dc;
+    if (hipSetDevice(device) != hipSuccess) return AIPSTACK_CHKSUM_ENODEV;
+    auto *e = new (std::nothrow) aipstack_chksum_engine;
+    if (!e) return AIPSTACK_CHKSUM_EINVAL;
+    e->device = device;
+    e->chunk_bytes = chunk_bytes;
+    // results/offsets staging sized for the smallest packets (64 B, the Ethernet minimum)
+    e->chunk_packets = chunk_bytes / 64 + 1;
+    e->slots.resize((size_t)nstreams);
+    int st = AIPSTACK_CHKSUM_OK;
+    for (Slot &s : e->slots) {
+        if (st == AIPSTACK_CHKSUM_OK) st = check_hip(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+        if (st == AIPSTACK_CHKSUM_OK) st = check_hip(hipMalloc(&s.d_bytes, chunk_bytes));
+        if (st == AIPSTACK_CHKSUM_OK) st = check_hip(hipMalloc(reinterpret_cast<void **>(&s.d_off), (e->chunk_packets + 1) * 8));
+        if (st == AIPSTACK_CHKSUM_OK) st = check_hip(hipMalloc(reinterpret_cast<void **>(&s.d_out), e->chunk_packets * 2));
+        if (st == AIPSTACK_CHKSUM_OK) st = check_hip(hipHostMalloc(&s.h_stage, chunk_bytes, hipHostMallocDefault));
+        if (st == AIPSTACK_CHKSUM_OK) st = check_hip(hipHostMalloc(reinterpret_cast<void **>(&s.h_off), (e->chunk_packets + 1) * 8, hipHostMallocDefault));
+        if (st == AIPSTACK_CHKSUM_OK) st = check_hip(hipHostMalloc(reinterpret_cast<void **>(&s.h_out), e->chunk_packets * 2, hipHostMallocDefault));
+        if (st == AIPSTACK_CHKSUM_OK) st = check_hip(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+    }
+    if (st != AIPSTACK_CHKSUM_OK) {
+        release(e);
+        delete e;
+        return st;
+    }
+    *out = e;
+    return AIPSTACK_CHKSUM_OK;
+}
+
+extern "C" void aipstack_chksum_engine_destroy(aipstack_chksum_engine *e) {
+    if (!e) return;
+    (void)hipSetDevice(e->device);
+    release(e);
+    delete e;
+}
+
+extern "C" int aipstack_chksum_engine_register(aipstack_chksum_engine *e, void *host_ptr,
+                                               uint64_t bytes) {
+    if (!e || !host_ptr || bytes == 0) return AIPSTACK_CHKSUM_EINVAL;
+    std::lock_guard<std::mutex> lock(e->mu);
+    if (hipSetDevice(e->device) != hipSuccess) return AIPSTACK_CHKSUM_ENODEV;
+    const int st = check_hip(hipHostRegister(host_ptr, bytes, hipHostRegisterDefault));
+    if (st == AIPSTACK_CHKSUM_OK) e->registered.push_back(Region{static_cast<char *>(host_ptr), bytes});
+    return st;
+}
+
+extern "C" int aipstack_chksum_engine_unregister(aipstack_chksum_engine *e, void *host_ptr) {
+    if (!e || !host_ptr) return AIPSTACK_CHKSUM_EINVAL;
+    std::lock_guard<std::mutex> lock(e->mu);
+    for (size_t i = 0; i < e->registered.size(); ++i) {
+        if (e->registered[i].p == host_ptr) {
+            (void)hipSetDevice(e->device);
+            const int st = check_hip(hipHostUnregister(host_ptr));
+            e->registered.erase(e->registered.begin() + (long)i);
+            return st;
+        }
+    }
+    return AIPSTACK_CHKSUM_EINVAL;
+}
+
+extern "C" int aipstack_chksum_engine_host_strided(aipstack_chksum_engine *e, const void *h_base,
+                                                   uint64_t stride, uint32_t len, uint64_t n,
+                                                   uint16_t *h_out, uint32_t flags) {
+    if (!e || !h_base || !h_out || len > AIPSTACK_CHKSUM_MAX_LEN) return AIPSTACK_CHKSUM_EINVAL;
+    if (n == 0) return AIPSTACK_CHKSUM_OK;
+    // packets per chunk: the chunk's byte span (i1-i0-1)*stride + len must fit
+    uint64_t per = stride ? (e->chunk_bytes - len) / stride + 1 : e->chunk_packets;
+    per = std::min<uint64_t>(std::max<uint64_t>(per, 1), e->chunk_packets);
+    if ((per - 1) * stride + len > e->chunk_bytes) return AIPSTACK_CHKSUM_EINVAL;
+    const char *base = static_cast<const char *>(h_base);
+    auto chunker = [&](uint64_t i0, uint64_t *i1, const char **src, uint64_t *bytes) {
+        *i1 = std::min(n, i0 + per);
+        *src = base + i0 * stride;
+        *bytes = (*i1 - i0 - 1) * stride + len;
+    };
+    auto launch = [&](Slot &s, uint64_t i0, uint64_t i1) {
+        return aipstack_chksum_batch_strided(s.d_bytes, stride, len, i1 - i0, s.d_out, flags,
+                                             s.stream);
+    };
+    return pipeline(e, n, h_out, chunker, launch);
+}
+
+extern "C" int aipstack_chksum_engine_host_csr(aipstack_chksum_engine *e, const void *h_base,
+                                               const uint64_t *h_offsets, uint64_t n,
+                                               uint16_t *h_out, uint32_t flags) {
+    if (!e || !h_base || !h_offsets || !h_out) return AIPSTACK_CHKSUM_EINVAL;
+    if (n == 0) return AIPSTACK_CHKSUM_OK;
+    for (uint64_t i = 0; i < n; ++i)  // contract check: non-decreasing, each <= 65535
+        if (h_offsets[i + 1] < h_offsets[i] || h_offsets[i + 1] - h_offsets[i] > AIPSTACK_CHKSUM_MAX_LEN)
+            return AIPSTACK_CHKSUM_EINVAL;
+    const char *base = static_cast<const char *>(h_base);
+    auto chunker = [&](uint64_t i0, uint64_t *i1, const char **src, uint64_t *bytes) {
+        // whole packets while they fit the chunk (binary search on the offsets)
+        const uint64_t limit = h_offsets[i0] + e->chunk_bytes;
+        const uint64_t *hi = std::upper_bound(h_offsets + i0 + 1,
+                                              h_offsets + std::min(n, i0 + e->chunk_packets) + 1,
+                                              limit);
+        uint64_t j = (uint64_t)(hi - h_offsets) - 1;  // last offset <= limit
+        if (j <= i0) j = i0 + 1;
+        *i1 = j;
+        *src = base + h_offsets[i0];
+        *bytes = h_offsets[j] - h_offsets[i0];
+    };
+    auto launch = [&](Slot &s, uint64_t i0, uint64_t i1) {
+        const uint64_t cnt = i1 - i0;
+        const uint64_t b0 = h_offsets[i0];
+        for (uint64_t i = 0; i <= cnt; ++i) s.h_off[i] = h_offsets[i0 + i] - b0;  // rebased
+        int st = check_hip(hipMemcpyAsync(s.d_off, s.h_off, (cnt + 1) * 8, hipMemcpyHostToDevice,
+                                          s.stream));
+        if (st != AIPSTACK_CHKSUM_OK) return st;
+        return aipstack_chksum_batch_csr(s.d_bytes, s.d_off, cnt, s.d_out, flags, s.stream);
+    };
+    return pipeline(e, n, h_out, chunker, launch);
+}

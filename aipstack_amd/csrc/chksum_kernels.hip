@@ -64,6 +64,7 @@ __device__ __forceinline__ uint32_t settle(uint32_t x) {
 }
 
 struct StridedDesc {
+    static constexpr bool kCsr = false;
     uint64_t base;    // absolute address of packet 0
     uint64_t stride;  // bytes between packet starts
     uint32_t len;     // bytes per packet
@@ -86,6 +87,7 @@ struct StridedDesc {
 };
 
 struct CsrDesc {
+    static constexpr bool kCsr = true;
     uint64_t base;            // absolute address offsets are relative to
     const uint64_t *offsets;  // n+1 byte offsets
 
@@ -426,11 +428,14 @@ int pick_unroll(uint32_t max_len) {
     return 4;
 }
 
-// P: packets in flight per wave; keep P*U*4 data VGPRs <= 32 (8 waves/SIMD).
-int pick_packets(int u) {
+// P: packets whose loads a wave keeps in flight. Measured (tools/sweep.py, MI355X):
+// 1500 B strided best at P = 4..8, 9000 B at P = 1 (U = 3 already has 3 KiB in flight
+// per wave), mixed CSR at P = 2.
+int pick_packets(int u, bool csr) {
     const int t = tuning().packets.load(std::memory_order_relaxed);
     if (t == 1 || t == 2 || t == 4 || t == 8) return t;
-    return u <= 2 ? 4 : 2;
+    if (csr) return 2;
+    return u <= 2 ? 4 : 1;
 }
 
 template <class Desc, int U, int P, bool NT, bool SEEDED>
@@ -442,7 +447,7 @@ int launch_k(const Desc &desc, uint64_t n, uint16_t *d_out, uint32_t flags,
     uint64_t cpw = (uint64_t)tuning().chunks_per_wave.load(std::memory_order_relaxed);
     if (cpw == 0) {
         int wpc = tuning().waves_per_cu.load(std::memory_order_relaxed);
-        if (wpc <= 0) wpc = kDefaultWavesPerCu;
+        if (wpc <= 0) wpc = Desc::kCsr ? 2 * kDefaultWavesPerCu : kDefaultWavesPerCu;
         const uint64_t target_waves = (uint64_t)cus * (uint64_t)wpc;
         cpw = (nchunks + target_waves - 1) / target_waves;
         if (cpw == 0) cpw = 1;
@@ -459,7 +464,7 @@ template <class Desc, int U, bool SEEDED>
 int launch_u(const Desc &desc, uint64_t n, uint16_t *d_out, uint32_t flags,
              hipStream_t stream) {
     const bool nt = tuning().nontemporal.load(std::memory_order_relaxed) != 0;
-    const int p = pick_packets(U);
+    const int p = pick_packets(U, Desc::kCsr);
 #define AIPSTACK_LAUNCH_P(PP)                                                               \
     case PP:                                                                                \
         return nt ? launch_k<Desc, U, PP, true, SEEDED>(desc, n, d_out, flags, stream)      \

@@ -61,6 +61,13 @@ def parse():
     p.add_argument("--cpu-reps", type=int, default=15,
                    help="timed single-thread passes of the CPU baseline sample")
     p.add_argument("--no-parity", action="store_true")
+    p.add_argument("--e2e", action="store_true",
+                   help="end-to-end mode: batch in HOST memory, results to HOST memory "
+                        "(host-memory streaming engine; PCIe-inclusive). Prints its own line.")
+    p.add_argument("--e2e-pageable", action="store_true",
+                   help="with --e2e: do not page-lock the host batch (CPU copy to staging)")
+    p.add_argument("--e2e-streams", type=int, default=4)
+    p.add_argument("--e2e-chunk-mib", type=int, default=64)
     return p.parse_args()
 
 
@@ -177,6 +184,8 @@ def main():
 
     layout, n, plen = CONFIGS[args.config]
     stream = torch.cuda.current_stream()
+    if args.e2e:
+        return e2e(args, rank, world, local_rank, layout, n, plen)
 
     # ---- this rank's shard, generated in place (global packets [rank*n, (rank+1)*n))
     off_host = None
@@ -208,23 +217,24 @@ def main():
         step()
     torch.cuda.synchronize()
 
-    # ---- timed region: barrier + synchronize on both sides, per-launch HIP events
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    # ---- timed region: barrier + synchronize on both sides; one HIP event pair on the
+    # launch stream brackets the K launches, so the per-launch average includes the
+    # kernel-to-kernel gaps (conservative for roofline.achieved)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        starts[i].record(stream)
+    ev0.record(stream)
+    for _ in range(args.steps):
         step()
-        ends[i].record(stream)
+    ev1.record(stream)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-    kernel_ms = [s.elapsed_time(e) for s, e in zip(starts, ends)]
-    avg_kernel_s = float(np.mean(kernel_ms)) / 1e3
+    avg_kernel_s = ev0.elapsed_time(ev1) / 1e3 / args.steps
 
     t = torch.tensor([elapsed], dtype=torch.float64)
     if world > 1:
@@ -293,6 +303,84 @@ def main():
         sys.exit(1)
 
 
+def e2e(args, rank, world, local_rank, layout, n, plen):
+    """Host memory in, host memory out, through aipstack_chksum_engine (PCIe-inclusive)."""
+    import torch.distributed as dist
+    import aipstack_amd as A
+    from aipstack_amd import synth
+    if layout == "strided":
+        total = n * plen
+        byte_offset = rank * total
+        host = np.empty(total, dtype=np.uint8)
+        synth.fill_host(host, synth.SEED_DATA, byte_offset)
+        off = None
+    else:
+        off_all = synth.mixed_offsets(n * world)
+        off = off_all[rank * n:(rank + 1) * n + 1] - off_all[rank * n]
+        byte_offset = int(off_all[rank * n])
+        total = int(off[-1])
+        host = np.empty(total, dtype=np.uint8)
+        synth.fill_host(host, synth.SEED_DATA, byte_offset)
+        synth.apply_classes_host(host, off, first_packet=rank * n)
+    out = np.empty(n, dtype=np.uint16)
+    eng = A.ChksumEngine(local_rank, chunk_bytes=args.e2e_chunk_mib << 20,
+                         nstreams=args.e2e_streams)
+    if not args.e2e_pageable:
+        eng.register(host)
+
+    def step():
+        if layout == "strided":
+            eng.strided(host, plen, plen, n, out=out)
+        else:
+            eng.csr(host, off, out=out)
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    import torch
+    t = torch.tensor([elapsed], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    max_elapsed = float(t.item())
+    parity = None
+    if rank == 0 and not args.no_parity:
+        lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "libchksum_oracle.so"))
+        want = np.empty(n, dtype=np.uint16)
+        if layout == "strided":
+            lib.oracle_batch_strided.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                                                 ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32]
+            lib.oracle_batch_strided(host.ctypes.data, plen, plen, n, want.ctypes.data, 0)
+        else:
+            lib.oracle_batch_csr.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                             ctypes.c_void_p, ctypes.c_uint32]
+            o = off.astype(np.uint64)
+            lib.oracle_batch_csr(host.ctypes.data, o.ctypes.data, n, want.ctypes.data, 0)
+        parity = "bit-exact" if np.array_equal(out, want) else "MISMATCH"
+    value = total * world * args.steps / max_elapsed / 2**30
+    if rank == 0:
+        print(json.dumps({
+            "metric": "GiB/s checksummed end-to-end (host memory in, host results out)",
+            "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(max_elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u16",
+            "data": "synthetic (splitmix64 bytes, seed 42; host memory)",
+            "config": {"workload": WORKLOAD_NAMES[args.config], "config": args.config,
+                       "host_memory": "pageable (CPU copy into pinned staging)"
+                       if args.e2e_pageable else "registered (hipHostRegister, DMA direct)",
+                       "streams": args.e2e_streams, "chunk_MiB": args.e2e_chunk_mib},
+            "parity": parity}), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def _oracle_sample_check(layout, n, plen, off_host, byte_offset, got):
     """Check the first 65536 packets of this rank's output against the C oracle."""
     from aipstack_amd import synth
@@ -311,7 +399,9 @@ def _oracle_sample_check(layout, n, plen, off_host, byte_offset, got):
 
 
 def _pmc_traffic(config):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary, if one exists."""
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), measured
+    by tools/pmc_run.sh on the same command: (2 x FETCH_SIZE + WRITE_SIZE) KiB, the x2
+    being the gfx950 correction of MI355X_MICROARCH.md (HBM section)."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:

@@ -85,6 +85,36 @@ int aipstack_chksum_batch_seeded_csr(const void *d_base, const uint64_t *d_offse
                                      const uint32_t *d_states, uint64_t n,
                                      uint16_t *d_out, void *stream);
 
+/* ---- 3. host-memory streaming engine ----------------------------------------------- */
+
+/* The reference's packet path starts and ends in host memory (TAP read()/write(),
+ * reference tap/linux/TapDeviceLinux.cpp:122-178). An engine checksums batches held in
+ * HOST memory and writes the results to HOST memory, pipelining H2D copies, kernels and
+ * D2H copies over `nstreams` HIP streams in chunks of at most `chunk_bytes` (0 = 64 MiB)
+ * of whole packets. Host buffers registered with aipstack_chksum_engine_register()
+ * (page-locked once, e.g. a receive ring) are DMA'd directly; other host memory is first
+ * copied into the engine's pinned staging. Calls are synchronous; one batch at a time
+ * per engine (calls on one engine from several threads are serialised). */
+typedef struct aipstack_chksum_engine aipstack_chksum_engine;
+
+int aipstack_chksum_engine_create(int device, uint64_t chunk_bytes, int nstreams,
+                                  aipstack_chksum_engine **out);
+void aipstack_chksum_engine_destroy(aipstack_chksum_engine *engine);
+int aipstack_chksum_engine_register(aipstack_chksum_engine *engine, void *host_ptr,
+                                    uint64_t bytes);
+int aipstack_chksum_engine_unregister(aipstack_chksum_engine *engine, void *host_ptr);
+
+/* h_out[i] for packet i = h_base[i*stride .. +len) (host memory), as the strided batch. */
+int aipstack_chksum_engine_host_strided(aipstack_chksum_engine *engine, const void *h_base,
+                                        uint64_t stride, uint32_t len, uint64_t n,
+                                        uint16_t *h_out, uint32_t flags);
+
+/* h_out[i] for packet i = h_base[h_offsets[i] .. h_offsets[i+1]) (host memory; offsets
+ * non-decreasing, each packet <= 65535 bytes, else _EINVAL before any work). */
+int aipstack_chksum_engine_host_csr(aipstack_chksum_engine *engine, const void *h_base,
+                                    const uint64_t *h_offsets, uint64_t n, uint16_t *h_out,
+                                    uint32_t flags);
+
 /* ---- diagnostics ------------------------------------------------------------------ */
 
 /* Static description of a status code. Never NULL. */

@@ -234,3 +234,40 @@ def test_cpp_capi_program():
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "OK" in r.stdout
+
+
+# ---- host-memory streaming engine ------------------------------------
+
+@pytest.mark.parametrize("register", [False, True])
+def test_engine_host_strided(oracle, register):
+    n, plen = 300000, 1500
+    host = synth.random_bytes(21, n * plen + 3)
+    with A.ChksumEngine(0, chunk_bytes=16 << 20, nstreams=3) as eng:
+        if register:
+            eng.register(host)
+        got = eng.strided(host[3:], plen, plen, n) if not register else \
+            eng.strided(host, plen, plen, n)
+        want = oracle.batch_strided(host, plen, plen, n, base_off=0 if register else 3)
+        assert np.array_equal(got, want)
+        fin = eng.strided(host, 1501, 1499, 1000, final=True)
+        assert np.array_equal(fin, oracle.batch_strided(host, 1501, 1499, 1000, final=True))
+
+
+@pytest.mark.parametrize("register", [False, True])
+def test_engine_host_csr(oracle, register):
+    buf, off = synth.mixed_batch(400000)
+    with A.ChksumEngine(0, chunk_bytes=8 << 20, nstreams=2) as eng:
+        if register:
+            eng.register(buf)
+        got = eng.csr(buf, off)
+        assert np.array_equal(got, oracle.batch_csr(buf, off))
+
+
+def test_engine_rejects_bad_offsets():
+    buf = np.zeros(1 << 20, dtype=np.uint8)
+    with A.ChksumEngine(0) as eng:
+        with pytest.raises(A.ChksumError):
+            eng.csr(buf, np.array([0, 100, 50], dtype=np.uint64))
+        with pytest.raises(A.ChksumError):
+            eng.csr(buf, np.array([0, 70000], dtype=np.uint64))
+        assert eng.csr(buf, np.array([0], dtype=np.uint64)).size == 0

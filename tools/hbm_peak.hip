@@ -1,0 +1,76 @@
+// Streaming-read ceiling of this MI355X: read a large buffer once with 16-byte loads,
+// fold it into one word per wave (so nothing is dead-code-eliminated), in the same
+// style and grid shapes as the checksum kernel. Reports GB/s per variant (median of
+// reps, HIP events). Not part of the product; it calibrates roofline.frac.
+//   hipcc --offload-arch=gfx950 -O3 -o tools/build/hbm_peak tools/hbm_peak.hip
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cstdio>
+#include <cstdint>
+#include <vector>
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <int UNROLL, bool NT>
+__global__ __launch_bounds__(256) void read_kernel(const u32x4 *__restrict__ p, uint64_t n16,
+                                                   uint64_t per_wave, uint32_t *out) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t wave = (uint64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint64_t i = wave * per_wave;
+    const uint64_t end = min(i + per_wave, n16);
+    uint32_t acc = 0;
+    __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)(p + i), (short)0,
+                                                                 (int)((end - i) * 16), 0x00020000);
+    for (uint32_t off = 0; i + off < end; off += 64 * UNROLL) {
+        u32x4 v[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u)
+            v[u] = __builtin_amdgcn_raw_buffer_load_b128(r, (lane + u * 64) * 16, off * 16, NT ? 2 : 0);
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) acc ^= v[u][0] + v[u][1] + v[u][2] + v[u][3];
+    }
+    if (acc == 0x12345678u) out[wave] = acc;  // practically never: keeps loads live
+}
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e), __LINE__); return 1; } } while (0)
+
+template <int U, bool NT>
+float run(const u32x4 *d, uint64_t n16, uint64_t per_wave, uint32_t *out, int reps) {
+    uint64_t waves = (n16 + per_wave - 1) / per_wave;
+    dim3 grid((unsigned)((waves + 3) / 4));
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a); (void)hipEventCreate(&b);
+    std::vector<float> t;
+    for (int r = 0; r < reps + 2; ++r) {
+        (void)hipEventRecord(a);
+        hipLaunchKernelGGL((read_kernel<U, NT>), grid, dim3(256), 0, 0, d, n16, per_wave, out);
+        (void)hipEventRecord(b);
+        (void)hipEventSynchronize(b);
+        float ms; (void)hipEventElapsedTime(&ms, a, b);
+        if (r >= 2) t.push_back(ms);
+    }
+    std::sort(t.begin(), t.end());
+    return t[t.size() / 2];
+}
+
+int main() {
+    const uint64_t bytes = 2359296000ull;  // config B's payload (2.36 GB, > 256 MiB MALL)
+    const uint64_t n16 = bytes / 16;
+    u32x4 *d; uint32_t *out;
+    CK(hipMalloc(&d, bytes));
+    CK(hipMalloc(&out, 1 << 24));
+    CK(hipMemset(d, 1, bytes));
+    CK(hipDeviceSynchronize());
+    const uint64_t pw[] = {2048, 4096, 8192, 16384, 32768};
+    for (uint64_t per_wave : pw) {
+        float t1 = run<1, true>(d, n16, per_wave, out, 10);
+        float t2 = run<2, true>(d, n16, per_wave, out, 10);
+        float t4 = run<4, true>(d, n16, per_wave, out, 10);
+        float t4d = run<4, false>(d, n16, per_wave, out, 10);
+        float t8 = run<8, true>(d, n16, per_wave, out, 10);
+        printf("{\"segments_per_wave\": %lu, \"GBps\": {\"u1_nt\": %.1f, \"u2_nt\": %.1f, \"u4_nt\": %.1f, \"u4_default\": %.1f, \"u8_nt\": %.1f}}\n",
+               (unsigned long)per_wave, bytes / t1 / 1e6, bytes / t2 / 1e6, bytes / t4 / 1e6,
+               bytes / t4d / 1e6, bytes / t8 / 1e6);
+    }
+    return 0;
+}
