@@ -71,6 +71,40 @@ def parse():
     return p.parse_args()
 
 
+def shard_spec(config, rank, world, n=None):
+    """This rank's shard of the global batch: packets [rank*n, (rank+1)*n).
+
+    Returns dict(layout, n, plen, byte_offset, offsets (local, CSR only), first_packet,
+    total). The global batch is the same for every world size: strided shards are
+    consecutive byte ranges of one splitmix64 stream; CSR shards are slices of one global
+    offsets array, rebased to 0, whose bytes start at the global offset of their first
+    packet (so classes and data come from global indices)."""
+    from aipstack_amd import synth
+    layout, n_default, plen = CONFIGS[config]
+    n = n_default if n is None else n
+    spec = {"layout": layout, "n": n, "plen": plen, "first_packet": rank * n}
+    if layout == "strided":
+        spec["total"] = n * plen
+        spec["byte_offset"] = rank * n * plen
+        spec["offsets"] = None
+    else:
+        off_all = synth.mixed_offsets(n * world)
+        spec["offsets"] = off_all[rank * n:(rank + 1) * n + 1] - off_all[rank * n]
+        spec["byte_offset"] = int(off_all[rank * n])
+        spec["total"] = int(spec["offsets"][-1])
+    return spec
+
+
+def host_shard(spec):
+    """The shard's bytes in host memory (numpy), exactly as the device generators make them."""
+    from aipstack_amd import synth
+    host = np.empty(spec["total"], dtype=np.uint8)
+    synth.fill_host(host, synth.SEED_DATA, spec["byte_offset"])
+    if spec["layout"] == "csr":
+        synth.apply_classes_host(host, spec["offsets"], first_packet=spec["first_packet"])
+    return host
+
+
 def algorithmic_bytes(layout, n, total_payload):
     """L bytes read + 2 bytes written per packet (+8 B offset for CSR)."""
     b = total_payload + 2 * n
@@ -79,14 +113,11 @@ def algorithmic_bytes(layout, n, total_payload):
     return b
 
 
-def cpu_baseline(layout, n, plen, off_host, data_seed, byte_offset, first_packet):
-    """Reference scalar path on the host, bounded sample = this rank's whole batch."""
-    from aipstack_amd import synth
-    total = int(off_host[-1]) if layout == "csr" else n * plen
-    host = np.empty(total, dtype=np.uint8)
-    synth.fill_host(host, data_seed, byte_offset)
-    if layout == "csr":
-        synth.apply_classes_host(host, off_host, first_packet=first_packet)
+def cpu_baseline(spec):
+    """Reference scalar path on the host; bounded sample = this rank's whole batch."""
+    layout, n, plen, off_host = spec["layout"], spec["n"], spec["plen"], spec["offsets"]
+    total = spec["total"]
+    host = host_shard(spec)
     out = np.empty(n, dtype=np.uint16)
     ref_path = os.path.join(ROOT, "oracle", "_ref", "libref_chksum.so")
     cores_all = min(16, os.cpu_count() or 1)
@@ -188,22 +219,15 @@ def main():
         return e2e(args, rank, world, local_rank, layout, n, plen)
 
     # ---- this rank's shard, generated in place (global packets [rank*n, (rank+1)*n))
-    off_host = None
-    if layout == "strided":
-        total = n * plen
-        byte_offset = rank * total
-        buf = torch.empty(total, dtype=torch.uint8, device=dev)
-        synth.fill_device(buf, synth.SEED_DATA, byte_offset)
-    else:
-        # mixed lengths of the GLOBAL batch, this rank's slice, rebased to 0
-        off_all = synth.mixed_offsets(n * world)
-        off_host = off_all[rank * n:(rank + 1) * n + 1] - off_all[rank * n]
-        byte_offset = int(off_all[rank * n])
-        total = int(off_host[-1])
-        buf = torch.empty(total, dtype=torch.uint8, device=dev)
-        synth.fill_device(buf, synth.SEED_DATA, byte_offset)
+    spec = shard_spec(args.config, rank, world)
+    off_host = spec["offsets"]
+    byte_offset = spec["byte_offset"]
+    total = spec["total"]
+    buf = torch.empty(total, dtype=torch.uint8, device=dev)
+    synth.fill_device(buf, synth.SEED_DATA, byte_offset)
+    if layout == "csr":
         d_off = torch.from_numpy(off_host).to(dev)
-        synth.apply_classes_device(buf, d_off, first_packet=rank * n)
+        synth.apply_classes_device(buf, d_off, first_packet=spec["first_packet"])
     out = torch.empty(n, dtype=torch.uint16, device=dev)
     torch.cuda.synchronize()
 
@@ -250,12 +274,11 @@ def main():
     if rank == 0:
         host_out = out.cpu().numpy()
         if not args.no_cpu_baseline and world == 1:
-            cpu, want = cpu_baseline(layout, n, plen, off_host, synth.SEED_DATA, byte_offset,
-                                     rank * n)
+            cpu, want = cpu_baseline(spec)
             if not args.no_parity:
                 parity = "bit-exact" if np.array_equal(host_out, want) else "MISMATCH"
         elif not args.no_parity:
-            parity = _oracle_sample_check(layout, n, plen, off_host, byte_offset, host_out)
+            parity = oracle_check(spec, host_out)
 
     bytes_all = payload * world  # weak scaling: every rank holds the same-size shard
     value = bytes_all * args.steps / max_elapsed / 2**30
@@ -308,20 +331,9 @@ def e2e(args, rank, world, local_rank, layout, n, plen):
     import torch.distributed as dist
     import aipstack_amd as A
     from aipstack_amd import synth
-    if layout == "strided":
-        total = n * plen
-        byte_offset = rank * total
-        host = np.empty(total, dtype=np.uint8)
-        synth.fill_host(host, synth.SEED_DATA, byte_offset)
-        off = None
-    else:
-        off_all = synth.mixed_offsets(n * world)
-        off = off_all[rank * n:(rank + 1) * n + 1] - off_all[rank * n]
-        byte_offset = int(off_all[rank * n])
-        total = int(off[-1])
-        host = np.empty(total, dtype=np.uint8)
-        synth.fill_host(host, synth.SEED_DATA, byte_offset)
-        synth.apply_classes_host(host, off, first_packet=rank * n)
+    spec = shard_spec(args.config, rank, world)
+    off, total = spec["offsets"], spec["total"]
+    host = host_shard(spec)
     out = np.empty(n, dtype=np.uint16)
     eng = A.ChksumEngine(local_rank, chunk_bytes=args.e2e_chunk_mib << 20,
                          nstreams=args.e2e_streams)
@@ -381,21 +393,23 @@ def e2e(args, rank, world, local_rank, layout, n, plen):
         dist.destroy_process_group()
 
 
-def _oracle_sample_check(layout, n, plen, off_host, byte_offset, got):
-    """Check the first 65536 packets of this rank's output against the C oracle."""
-    from aipstack_amd import synth
-    m = min(n, 65536)
+def oracle_check(spec, got):
+    """Check this rank's whole output against the C oracle on the same bytes."""
+    host = host_shard(spec)
     lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "libchksum_oracle.so"))
-    want = np.empty(m, dtype=np.uint16)
-    if layout == "strided":
-        host = np.empty(m * plen, dtype=np.uint8)
-        synth.fill_host(host, synth.SEED_DATA, byte_offset)
+    n = spec["n"]
+    want = np.empty(n, dtype=np.uint16)
+    if spec["layout"] == "strided":
         lib.oracle_batch_strided.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
                                              ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32]
-        lib.oracle_batch_strided(host.ctypes.data, plen, plen, m, want.ctypes.data, 0)
+        lib.oracle_batch_strided(host.ctypes.data, spec["plen"], spec["plen"], n,
+                                 want.ctypes.data, 0)
     else:
-        return None
-    return "bit-exact (first 65536 packets)" if np.array_equal(got[:m], want) else "MISMATCH"
+        lib.oracle_batch_csr.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                         ctypes.c_void_p, ctypes.c_uint32]
+        o = spec["offsets"].astype(np.uint64)
+        lib.oracle_batch_csr(host.ctypes.data, o.ctypes.data, n, want.ctypes.data, 0)
+    return "bit-exact (whole batch vs oracle)" if np.array_equal(got, want) else "MISMATCH"
 
 
 def _pmc_traffic(config):
