@@ -23,10 +23,12 @@ from .chksum import (  # noqa: E402
     IpChksum,
     IpChksumAccumulator,
     IpChksumInverted,
+    chksum_batch_chain,
     chksum_batch_csr,
     chksum_batch_seeded_csr,
     chksum_batch_strided,
     device_check,
+    flatten_chains,
     ipBufProcessBytes,
 )
 
@@ -37,6 +39,6 @@ __all__ = [
     "AIPSTACK_CHKSUM_FINAL", "AIPSTACK_CHKSUM_MAX_LEN", "AIPSTACK_CHKSUM_OK", "ChksumEngine",
     "ChksumError",
     "IpBufNode", "IpBufRef", "IpChksum", "IpChksumAccumulator", "IpChksumInverted",
-    "chksum_batch_csr", "chksum_batch_seeded_csr", "chksum_batch_strided", "device_check",
+    "chksum_batch_chain", "chksum_batch_csr", "chksum_batch_seeded_csr", "flatten_chains", "chksum_batch_strided", "device_check",
     "ipBufProcessBytes", "LIB_PATH",
 ]

@@ -391,6 +391,59 @@ class ChksumEngine:
         return out
 
 
+def chksum_batch_chain(chunk_addr, chunk_len, chunk_index, states=None, *, out=None,
+                       final: bool = False, stream=None):
+    """Chained (scatter-gather) batch on the GPU: chain i = chunks
+    ``[chunk_index[i], chunk_index[i+1])``, chunk k = ``chunk_len[k]`` bytes at DEVICE
+    address ``chunk_addr[k]``. ``final=True`` gives
+    ``IpChksumAccumulator(State(states[i])).getChksum(chain i)``; ``final=False`` its NOT.
+    Tensors: int64 addresses, int32 lengths, int64 index (n+1), int32 states (or None)."""
+    for t, name in ((chunk_addr, "chunk_addr"), (chunk_len, "chunk_len"),
+                    (chunk_index, "chunk_index")):
+        _require_device(t, name)
+    if chunk_addr.element_size() != 8 or chunk_len.element_size() != 4 \
+            or chunk_index.element_size() != 8:
+        raise ValueError("chunk_addr/chunk_index must be 64-bit, chunk_len 32-bit")
+    n = chunk_index.numel() - 1
+    if n < 0:
+        raise ValueError("chunk_index must hold n+1 entries")
+    sp = 0
+    if states is not None:
+        _require_device(states, "states")
+        if states.numel() < n or states.element_size() != 4:
+            raise ValueError("states must hold n 32-bit entries")
+        sp = states.data_ptr()
+    out = _out_tensor(out, n, chunk_index)
+    st = _lib.load().aipstack_chksum_batch_chain(
+        chunk_addr.data_ptr(), chunk_len.data_ptr(), chunk_index.data_ptr(), sp or None, n,
+        out.data_ptr(), AIPSTACK_CHKSUM_FINAL if final else 0, _stream_handle(stream))
+    _check(st, "aipstack_chksum_batch_chain")
+    return out
+
+
+def flatten_chains(refs, host_base: np.ndarray, device_base: int):
+    """Flatten IpBufRef chains whose nodes point into `host_base` (a numpy byte array
+    mirrored on the device at `device_base`) into the chunk table of
+    :func:`chksum_batch_chain`: the non-empty chunks ipBufProcessBytes visits
+    (BufUtils.h:129-178), translated to device addresses. Returns numpy
+    (addr uint64, len uint32, index uint64)."""
+    base_ptr = host_base.ctypes.data
+    addrs, lens, index = [], [], [0]
+    for ref in refs:
+        if ref.tot_len > 0:
+            def visit(mv, n):
+                ptr = np.frombuffer(mv, dtype=np.uint8).ctypes.data
+                if not base_ptr <= ptr < base_ptr + host_base.nbytes:
+                    raise ValueError("chain node outside host_base")
+                addrs.append(device_base + (ptr - base_ptr))
+                lens.append(n)
+                return n
+            ipBufProcessBytes(ref, ref.tot_len, visit)
+        index.append(len(addrs))
+    return (np.array(addrs, dtype=np.uint64), np.array(lens, dtype=np.uint32),
+            np.array(index, dtype=np.uint64))
+
+
 def device_check(device: int = 0) -> int:
     """AIPSTACK_CHKSUM_OK if `device` is a gfx950 device the library can launch on."""
     return int(_lib.load().aipstack_chksum_device_check(device))

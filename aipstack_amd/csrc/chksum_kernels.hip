@@ -384,6 +384,70 @@ __global__ __launch_bounds__(kBlock) void chksum_batch_kernel(Desc desc, uint64_
 }
 
 // ---------------------------------------------------------------------------------
+// Chained batch: IpChksumAccumulator(State{states[i]})
+// .getChksum(IpBufRef{chain i}) (Chksum.h:171-174, 263-315) for n chains. Chain i is the
+// chunks [index[i], index[i+1]) of a chunk table (absolute address, length), in order:
+// the IpBufRef's nodes as ipBufProcessBytes visits them (BufUtils.h:129-178).
+//
+// The reference adds each chunk's IpChksumInverted with end-around carry and byte-swaps
+// the running sum after every odd-length chunk, once more at the end if the count of
+// swaps is odd (Chksum.h:294-314). A swap is x*256 mod 0xFFFF, so chunk k contributes
+// its big-endian sum times 256^(parity of its logical position q_k), and the state is
+// swapped an even number of times. With the kernel's little-endian sum of the chunk at
+// address a_k, that is: byte-swap the folded chunk sum iff parity(a_k) == parity(q_k).
+// ---------------------------------------------------------------------------------
+template <int U, bool NT>
+__global__ __launch_bounds__(kBlock) void chksum_chain_kernel(
+    const uint64_t *__restrict__ chunk_addr, const uint32_t *__restrict__ chunk_len,
+    const uint64_t *__restrict__ index, const uint32_t *__restrict__ states, uint64_t n,
+    uint32_t chunks_per_wave, uint16_t *__restrict__ out, uint32_t flags) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint32_t wave_in_block = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerBlock + wave_in_block;
+    const uint64_t nchunks = (n + kWave - 1) / kWave;
+    uint64_t c = wave * chunks_per_wave;
+    const uint64_t c_end = min(c + chunks_per_wave, nchunks);
+    const bool final_flag = (flags & AIPSTACK_CHKSUM_FINAL) != 0;
+    const uint32_t voff = (uint32_t)lane * 16u;
+    const uint32_t not_lane0 = lane == 0 ? 0u : ~0u;
+    CsrDesc idx_desc{0, index};  // reuse the CSR offset walk for the chunk index
+
+    for (; c < c_end; ++c) {
+        const uint64_t p0 = c * kWave;
+        const auto chunk = idx_desc.begin_chunk(p0, n, lane);
+        const int cnt = (int)min((uint64_t)kWave, n - p0);
+        uint32_t state = 0;
+        if (states != nullptr && p0 + lane < n)
+            state = states[p0 + lane];
+        uint32_t sums = 0;  // lane j: sum of chain j's orientation-corrected chunk sums
+        for (int j = 0; j < cnt; ++j) {
+            uint64_t k0, k1;
+            idx_desc.bounds(chunk, j, k0, k1);
+            uint32_t acc = 0;   // <= nchunks * 0xFFFF
+            uint32_t pos = 0;   // parity of the logical position
+            for (uint64_t k = k0; k < k1; ++k) {
+                const uint64_t a = chunk_addr[k];
+                const uint32_t l = chunk_len[k];
+                PacketLoad<U, NT> pk;
+                pk.issue(a, a + l, voff);
+                uint32_t r = fold16(pk.finish(lane, voff, not_lane0));
+                if ((uint32_t)(a & 1) == pos)
+                    r = bswap16(r);
+                acc += r;
+                pos ^= l & 1;
+            }
+            sums = (lane == j) ? acc : sums;
+        }
+        // m_sum = state (+) chain sum with end-around carry; getChksum folds and inverts.
+        const uint64_t t = (uint64_t)state + fold16(sums);
+        uint32_t r = fold16((uint32_t)t + (uint32_t)(t >> 32));
+        r = final_flag ? (~r & 0xFFFFu) : r;
+        if (lane < cnt)
+            out[p0 + lane] = (uint16_t)r;
+    }
+}
+
+// ---------------------------------------------------------------------------------
 // Launch configuration
 // ---------------------------------------------------------------------------------
 
@@ -492,6 +556,24 @@ int launch(const Desc &desc, uint64_t n, uint32_t max_len, uint16_t *d_out, uint
     return AIPSTACK_CHKSUM_EINVAL;
 }
 
+template <int U, bool NT>
+int launch_chain(const uint64_t *d_addr, const uint32_t *d_len, const uint64_t *d_index,
+                 const uint32_t *d_states, uint64_t n, uint16_t *d_out, uint32_t flags,
+                 hipStream_t stream) {
+    const uint64_t nchunks = (n + kWave - 1) / kWave;
+    const int cus = device_cu_count();
+    if (cus <= 0) return AIPSTACK_CHKSUM_EHIP;
+    const uint64_t target_waves = (uint64_t)cus * 2 * kDefaultWavesPerCu;
+    uint64_t cpw = (nchunks + target_waves - 1) / target_waves;
+    if (cpw == 0) cpw = 1;
+    const uint64_t waves = (nchunks + cpw - 1) / cpw;
+    const uint64_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
+    if (blocks > 0x7FFFFFFFull || cpw > 0xFFFFFFFFull) return AIPSTACK_CHKSUM_EINVAL;
+    hipLaunchKernelGGL((chksum_chain_kernel<U, NT>), dim3((unsigned)blocks), dim3(kBlock), 0,
+                       stream, d_addr, d_len, d_index, d_states, n, (uint32_t)cpw, d_out, flags);
+    return check_hip(hipGetLastError());
+}
+
 }  // namespace
 }  // namespace aipstack_amd
 
@@ -542,4 +624,20 @@ extern "C" int aipstack_chksum_tune(const char *key, int value) {
     else if (!std::strcmp(key, "nontemporal")) t.nontemporal = value;
     else return AIPSTACK_CHKSUM_EINVAL;
     return AIPSTACK_CHKSUM_OK;
+}
+
+extern "C" int aipstack_chksum_batch_chain(const uint64_t *d_chunk_addr,
+                                           const uint32_t *d_chunk_len,
+                                           const uint64_t *d_chunk_index,
+                                           const uint32_t *d_states, uint64_t n,
+                                           uint16_t *d_out, uint32_t flags, void *stream) {
+    if (n == 0) return AIPSTACK_CHKSUM_OK;
+    if (!d_chunk_addr || !d_chunk_len || !d_chunk_index || !d_out) return AIPSTACK_CHKSUM_EINVAL;
+    if (n > (1ull << 40)) return AIPSTACK_CHKSUM_EINVAL;
+    // Chains are mostly short pieces (headers, ring-buffer halves): U = 2 covers 2 KiB.
+    return tuning().nontemporal.load(std::memory_order_relaxed)
+               ? launch_chain<2, true>(d_chunk_addr, d_chunk_len, d_chunk_index, d_states, n,
+                                       d_out, flags, (hipStream_t)stream)
+               : launch_chain<2, false>(d_chunk_addr, d_chunk_len, d_chunk_index, d_states, n,
+                                        d_out, flags, (hipStream_t)stream);
 }

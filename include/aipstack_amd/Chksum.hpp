@@ -155,6 +155,24 @@ inline std::uint16_t IpChksum(IpBufRef buf) {
     return acc.getChksum(buf);
 }
 
+// Flatten an IpBufRef chain into the chunk table of aipstack_chksum_batch_chain: appends
+// the non-empty chunks ipBufProcessBytes visits (BufUtils.h:129-178) as (device address,
+// length) and closes the chain's index entry. `to_device(char *host_ptr)` maps a node's
+// host pointer to the device address of the same byte (e.g. base_dev + (p - base_host)).
+template <typename ToDevice, typename AddrVec, typename LenVec, typename IndexVec>
+void appendChain(IpBufRef buf, ToDevice &&to_device, AddrVec &addr, LenVec &len,
+                 IndexVec &index) {
+    if (index.empty()) index.push_back(0);
+    if (buf.tot_len > 0) {
+        ipBufProcessBytes(buf, buf.tot_len, [&](char *p, std::size_t n) {
+            addr.push_back(std::uint64_t(to_device(p)));
+            len.push_back(std::uint32_t(n));
+            return n;
+        });
+    }
+    index.push_back(std::uint64_t(addr.size()));
+}
+
 // GPU batch entry points (device pointers, stream-ordered; see chksum.h).
 struct BatchChksum {
     static int strided(void const *d_base, std::uint64_t stride, std::uint32_t len,
@@ -174,6 +192,15 @@ struct BatchChksum {
         return aipstack_chksum_batch_seeded_csr(
             d_base, d_offsets, reinterpret_cast<std::uint32_t const *>(d_states), n, d_out,
             stream);
+    }
+    static int chain(std::uint64_t const *d_chunk_addr, std::uint32_t const *d_chunk_len,
+                     std::uint64_t const *d_chunk_index,
+                     IpChksumAccumulator::State const *d_states, std::uint64_t n,
+                     std::uint16_t *d_out, bool final_chksum = true, void *stream = nullptr) {
+        return aipstack_chksum_batch_chain(
+            d_chunk_addr, d_chunk_len, d_chunk_index,
+            reinterpret_cast<std::uint32_t const *>(d_states), n, d_out,
+            final_chksum ? AIPSTACK_CHKSUM_FINAL : 0u, stream);
     }
 };
 

@@ -85,6 +85,18 @@ int aipstack_chksum_batch_seeded_csr(const void *d_base, const uint64_t *d_offse
                                      const uint32_t *d_states, uint64_t n,
                                      uint16_t *d_out, void *stream);
 
+/* Chained (scatter-gather) batch: chain i is the chunks [d_chunk_index[i],
+ * d_chunk_index[i+1]) of the chunk table, taken in order as one logical byte sequence:
+ * chunk k is the d_chunk_len[k] bytes at DEVICE address d_chunk_addr[k] (any alignment,
+ * each <= 65535 bytes). This is an IpBufRef chain (reference Buf.h:68-251) flattened into
+ * the non-empty chunks ipBufProcessBytes visits (BufUtils.h:129-178). With
+ * AIPSTACK_CHKSUM_FINAL, d_out[i] = IpChksumAccumulator(State{s_i}).getChksum(chain i)
+ * (Chksum.h:171-174, 263-315), s_i = d_states[i] or 0 when d_states is NULL; without
+ * the flag, the bitwise NOT of that (the inverted sum). n+1 index entries. */
+int aipstack_chksum_batch_chain(const uint64_t *d_chunk_addr, const uint32_t *d_chunk_len,
+                                const uint64_t *d_chunk_index, const uint32_t *d_states,
+                                uint64_t n, uint16_t *d_out, uint32_t flags, void *stream);
+
 /* ---- 3. host-memory streaming engine ----------------------------------------------- */
 
 /* The reference's packet path starts and ends in host memory (TAP read()/write(),

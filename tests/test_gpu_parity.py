@@ -271,3 +271,96 @@ def test_engine_rejects_bad_offsets():
         with pytest.raises(A.ChksumError):
             eng.csr(buf, np.array([0, 70000], dtype=np.uint64))
         assert eng.csr(buf, np.array([0], dtype=np.uint64)).size == 0
+
+
+# ---- chained scatter-gather batches ---------------------------------
+
+def _chain_tables(golden, db):
+    from conftest import chain_to_chunks
+    addrs, lens, index, states, want = [], [], [0], [], []
+    base = db.data_ptr()
+    for c in golden["chain"]["chains"]:
+        for o, l in chain_to_chunks(c):
+            addrs.append(base + o)
+            lens.append(l)
+        index.append(len(addrs))
+        states.append(c["state"])
+        want.append(c["chksum"])
+    return (np.array(addrs, dtype=np.uint64), np.array(lens, dtype=np.uint32),
+            np.array(index, dtype=np.uint64), np.array(states, dtype=np.uint32),
+            np.array(want, dtype=np.uint16))
+
+
+def test_chain_golden_reference_cases(golden):
+    """All 3,609 reference chain cases (the 512-node 0x00FF KAT, the chain==flat splits,
+    scatter chains with states/offsets/tot_len) in ONE GPU batch."""
+    db = _d(golden["blob"])
+    addr, ln, idx, st, want = _chain_tables(golden, db)
+    got = _np(A.chksum_batch_chain(_d(addr.view(np.int64)), _d(ln.view(np.int32)),
+                                   _d(idx.view(np.int64)), _d(st.view(np.int32)), final=True))
+    assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
+    inv = _np(A.chksum_batch_chain(_d(addr.view(np.int64)), _d(ln.view(np.int32)),
+                                   _d(idx.view(np.int64)), _d(st.view(np.int32))))
+    assert np.array_equal(inv, ~want)
+
+
+def test_chain_flatten_and_null_states(oracle):
+    """Python IpBufRef chains -> flatten_chains -> GPU, vs the host accumulator mirror."""
+    rng = np.random.default_rng(8)
+    host = rng.integers(0, 256, size=1 << 20, dtype=np.uint8)
+    db = _d(host)
+    refs, want = [], []
+    for _ in range(5000):
+        nodes = None
+        for _ in range(int(rng.integers(1, 6))):
+            o = int(rng.integers(0, host.size - 2000))
+            l = int(rng.choice([0, 1, 2, 3, int(rng.integers(0, 1600))]))
+            nodes = A.IpBufNode(host[o:o + l], l, nodes)
+        total, nd = 0, nodes
+        while nd is not None:
+            total += nd.len
+            nd = nd.next
+        off = int(rng.integers(0, nodes.len + 1))
+        ref = A.IpBufRef(nodes, off, total - off)
+        refs.append(ref)
+        want.append(A.IpChksumAccumulator().getChksum(ref))
+    addr, ln, idx = A.flatten_chains(refs, host, db.data_ptr())
+    got = _np(A.chksum_batch_chain(_d(addr.view(np.int64)), _d(ln.view(np.int32)),
+                                   _d(idx.view(np.int64)), None, final=True))
+    assert np.array_equal(got, np.array(want, dtype=np.uint16))
+
+
+def test_chain_tcp_tx_shape(oracle):
+    """TCP Tx shape (tcp/IpTcpProto_output.h:1251-1277): pseudo-header state + header node
+    + up to 2 send-ring chunks (utils/TcpRingBufferUtils.h:51), 100k segments."""
+    rng = np.random.default_rng(9)
+    ring = rng.integers(0, 256, size=1 << 22, dtype=np.uint8)
+    hdrs = rng.integers(0, 256, size=100000 * 60, dtype=np.uint8)
+    dring, dh = _d(ring), _d(hdrs)
+    addrs, lens, idx, states, want = [], [], [0], [], []
+    for i in range(100000):
+        hl = 20 + 4 * int(rng.integers(0, 11))
+        chunks = [(dh.data_ptr() + 60 * i, hl, hdrs[60 * i:60 * i + hl])]
+        seg = int(rng.integers(0, 1461))
+        start = int(rng.integers(0, ring.size))
+        first = min(seg, ring.size - start)
+        chunks.append((dring.data_ptr() + start, first, ring[start:start + first]))
+        if seg > first:
+            chunks.append((dring.data_ptr(), seg - first, ring[:seg - first]))
+        st = int(rng.integers(0, 2**20))
+        acc = A.IpChksumAccumulator(st)
+        nodes = None
+        for _, l, h in reversed(chunks):
+            nodes = A.IpBufNode(h, l, nodes)
+        want.append(acc.getChksum(A.IpBufRef(nodes, 0, sum(c[1] for c in chunks))))
+        for a, l, _ in chunks:
+            if l:
+                addrs.append(a)
+                lens.append(l)
+        idx.append(len(addrs))
+        states.append(st)
+    got = _np(A.chksum_batch_chain(_d(np.array(addrs, dtype=np.int64)),
+                                   _d(np.array(lens, dtype=np.int32)),
+                                   _d(np.array(idx, dtype=np.int64)),
+                                   _d(np.array(states, dtype=np.int32)), final=True))
+    assert np.array_equal(got, np.array(want, dtype=np.uint16))
