@@ -30,6 +30,9 @@ from .chksum import (  # noqa: E402
     device_check,
     flatten_chains,
     ipBufProcessBytes,
+    RX_VERDICTS,
+    rx_verify,
+    tx_fill,
 )
 
 LIB_PATH = _lib.LIB_PATH
@@ -40,5 +43,5 @@ __all__ = [
     "ChksumError",
     "IpBufNode", "IpBufRef", "IpChksum", "IpChksumAccumulator", "IpChksumInverted",
     "chksum_batch_chain", "chksum_batch_csr", "chksum_batch_seeded_csr", "flatten_chains", "chksum_batch_strided", "device_check",
-    "ipBufProcessBytes", "LIB_PATH",
+    "ipBufProcessBytes", "LIB_PATH", "RX_VERDICTS", "rx_verify", "tx_fill",
 ]

@@ -28,6 +28,8 @@ SIGNATURES = {
     "aipstack_chksum_batch_csr": (_c_int, [_c_vp, _c_vp, _c_u64, _c_vp, _c_u32, _c_vp]),
     "aipstack_chksum_batch_seeded_csr": (_c_int, [_c_vp, _c_vp, _c_vp, _c_u64, _c_vp, _c_vp]),
     "aipstack_chksum_batch_chain": (_c_int, [_c_vp, _c_vp, _c_vp, _c_vp, _c_u64, _c_vp, _c_u32, _c_vp]),
+    "aipstack_chksum_rx_verify": (_c_int, [_c_vp, _c_vp, _c_u64, _c_vp, _c_vp]),
+    "aipstack_chksum_tx_fill": (_c_int, [_c_vp, _c_vp, _c_u64, _c_vp, _c_vp]),
     "aipstack_chksum_strerror": (ctypes.c_char_p, [_c_int]),
     "aipstack_chksum_last_hip_error": (_c_int, []),
     "aipstack_chksum_device_check": (_c_int, [_c_int]),
@@ -45,6 +47,7 @@ SIGNATURES = {
     "aipstack_synth_apply_classes_host": (None, [_c_vp, _c_vp, _c_u64, _c_u64, _c_u64]),
     "aipstack_synth_fill_device": (_c_int, [_c_vp, _c_u64, _c_u64, _c_u64, _c_vp]),
     "aipstack_synth_apply_classes_device": (_c_int, [_c_vp, _c_vp, _c_u64, _c_u64, _c_u64, _c_vp]),
+    "aipstack_synth_frames_host": (_c_u64, [_c_vp, _c_vp, _c_u64, _c_u64, _c_u32]),
 }
 
 ABI_VERSION = 1

@@ -421,6 +421,47 @@ def chksum_batch_chain(chunk_addr, chunk_len, chunk_index, states=None, *, out=N
     return out
 
 
+def _u8_out(out, n, like):
+    torch = _torch()
+    if out is None:
+        return torch.empty(n, dtype=torch.uint8, device=like.device)
+    _require_device(out, "out")
+    if out.element_size() != 1 or out.numel() < n:
+        raise ValueError("out must be a uint8 device tensor with >= n elements")
+    return out
+
+
+def rx_verify(frames, offsets, *, out=None, stream=None):
+    """Rx verify on the GPU: frame i = ``frames[offsets[i]:offsets[i+1]]`` (raw Ethernet);
+    returns one AIPSTACK_RX_* verdict per frame (uint8 device tensor). Read-only."""
+    _require_device(frames, "frames")
+    _require_device(offsets, "offsets")
+    n = offsets.numel() - 1
+    out = _u8_out(out, max(n, 0), frames)
+    _check(_lib.load().aipstack_chksum_rx_verify(frames.data_ptr(), offsets.data_ptr(), n,
+                                                 out.data_ptr(), _stream_handle(stream)),
+           "aipstack_chksum_rx_verify")
+    return out
+
+
+def tx_fill(frames, offsets, *, out=None, stream=None):
+    """Tx fill on the GPU, IN PLACE: writes the IPv4 header checksum and the TCP / UDP /
+    ICMP checksum of every frame; returns one status per frame (AIPSTACK_RX_* codes)."""
+    _require_device(frames, "frames")
+    _require_device(offsets, "offsets")
+    n = offsets.numel() - 1
+    out = _u8_out(out, max(n, 0), frames)
+    _check(_lib.load().aipstack_chksum_tx_fill(frames.data_ptr(), offsets.data_ptr(), n,
+                                               out.data_ptr(), _stream_handle(stream)),
+           "aipstack_chksum_tx_fill")
+    return out
+
+
+RX_VERDICTS = {0: "NOT_IP4", 1: "DROP_IP_MALFORMED", 2: "DROP_IP_CHKSUM", 3: "FRAGMENT",
+               4: "DROP_L4_MALFORMED", 5: "DROP_L4_CHKSUM", 6: "ACCEPT",
+               7: "ACCEPT_NO_CHKSUM", 8: "ACCEPT_OTHER"}
+
+
 def flatten_chains(refs, host_base: np.ndarray, device_base: int):
     """Flatten IpBufRef chains whose nodes point into `host_base` (a numpy byte array
     mirrored on the device at `device_base`) into the chunk table of

@@ -38,291 +38,10 @@
 #include "aipstack_amd/chksum.h"
 #include "chksum_internal.h"
 
+#include "chksum_device.h"
+
 namespace aipstack_amd {
 namespace {
-
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-constexpr int kWave = 64;
-constexpr int kWavesPerBlock = 4;
-constexpr int kBlock = kWave * kWavesPerBlock;
-
-// ---------------------------------------------------------------------------------
-// Packet descriptors. A wave walks 64-packet chunks; per chunk the descriptor may fetch
-// per-lane data (lane j <-> packet j of the chunk), then gives
-//   bounds(j)      the wave-uniform absolute byte range [S, E) of packet j (SGPRs), and
-//   lane_start()   the start address of this lane's packet (VGPR, for the finalisation).
-// ---------------------------------------------------------------------------------
-
-// A copy of x in a fresh VGPR. The compiler waits for the load that produced x here,
-// once per chunk, instead of before every later v_readlane of it (where, inside the
-// packet loop, the wait would also drain the packet loads already in flight).
-__device__ __forceinline__ uint32_t settle(uint32_t x) {
-    uint32_t y;
-    asm volatile("v_mov_b32 %0, %1" : "=v"(y) : "v"(x));
-    return y;
-}
-
-struct StridedDesc {
-    static constexpr bool kCsr = false;
-    uint64_t base;    // absolute address of packet 0
-    uint64_t stride;  // bytes between packet starts
-    uint32_t len;     // bytes per packet
-
-    struct Chunk {
-        uint64_t s0;  // start of the chunk's first packet
-    };
-    __device__ __forceinline__ Chunk begin_chunk(uint64_t p0, uint64_t, int) const {
-        return Chunk{base + p0 * stride};
-    }
-    __device__ __forceinline__ void bounds(const Chunk &c, int j, uint64_t &S,
-                                           uint64_t &E) const {
-        S = c.s0 + (uint64_t)j * stride;
-        E = S + len;
-    }
-    __device__ __forceinline__ uint64_t lane_start(const Chunk &c, int lane) const {
-        return c.s0 + (uint64_t)lane * stride;
-    }
-    __device__ __forceinline__ uint32_t lane_seed(const Chunk &) const { return 0; }
-};
-
-struct CsrDesc {
-    static constexpr bool kCsr = true;
-    uint64_t base;            // absolute address offsets are relative to
-    const uint64_t *offsets;  // n+1 byte offsets
-
-    struct Chunk {
-        uint32_t off_lo, off_hi;  // lane j: offsets[c0 + j] (settled)
-        uint64_t end_off;         // offsets[min(c0 + 64, n)] (scalar load)
-    };
-    // Lane j fetches offsets[c0 + j]: one coalesced 512-B load per chunk.
-    __device__ __forceinline__ Chunk begin_chunk(uint64_t c0, uint64_t n, int lane) const {
-        Chunk c;
-        const uint64_t i = c0 + (uint64_t)lane;
-        const uint64_t o = offsets[i <= n ? i : n];
-        c.off_lo = settle((uint32_t)o);
-        c.off_hi = settle((uint32_t)(o >> 32));
-        const uint64_t last = c0 + kWave < n ? c0 + kWave : n;
-        c.end_off = offsets[last];
-        return c;
-    }
-    __device__ __forceinline__ uint64_t offset_of(const Chunk &c, int j) const {
-        const uint32_t lo = __builtin_amdgcn_readlane(c.off_lo, j);
-        const uint32_t hi = __builtin_amdgcn_readlane(c.off_hi, j);
-        return ((uint64_t)hi << 32) | lo;
-    }
-    __device__ __forceinline__ void bounds(const Chunk &c, int j, uint64_t &S,
-                                           uint64_t &E) const {
-        S = base + offset_of(c, j);
-        E = base + ((j + 1 < kWave) ? offset_of(c, j + 1) : c.end_off);
-    }
-    __device__ __forceinline__ uint64_t lane_start(const Chunk &c, int) const {
-        return base + (((uint64_t)c.off_hi << 32) | c.off_lo);
-    }
-    __device__ __forceinline__ uint32_t lane_seed(const Chunk &) const { return 0; }
-};
-
-struct SeededCsrDesc : CsrDesc {
-    const uint32_t *states;  // n accumulator states (IpChksumAccumulator::State)
-
-    struct Chunk : CsrDesc::Chunk {
-        uint32_t state;  // lane j: states[c0 + j]
-    };
-    __device__ __forceinline__ Chunk begin_chunk(uint64_t c0, uint64_t n, int lane) const {
-        Chunk c;
-        static_cast<CsrDesc::Chunk &>(c) = CsrDesc::begin_chunk(c0, n, lane);
-        const uint64_t i = c0 + (uint64_t)lane;
-        c.state = i < n ? states[i] : 0u;
-        return c;
-    }
-    __device__ __forceinline__ uint32_t lane_seed(const Chunk &c) const { return c.state; }
-};
-
-// ---------------------------------------------------------------------------------
-// Per-lane pieces
-// ---------------------------------------------------------------------------------
-
-// Ones'-complement (end-around-carry) accumulator over 32-bit words: the add-with-carry
-// chain compiles to one v_addc_co_u32 per word; the carry out of each add is folded into
-// the next one, and finish() adds the last carry (twice at most). 2^32 = 1 (mod 0xFFFF),
-// so the 32-bit ones'-complement sum is congruent to the sum of the 16-bit halves, and it
-// is 0 only if every word was 0.
-struct Eac {
-    uint32_t s = 0, c = 0;
-    __device__ __forceinline__ void add(uint32_t x) { s = __builtin_addc(s, x, c, &c); }
-    __device__ __forceinline__ uint32_t finish() {
-        uint32_t c2;
-        uint32_t r = __builtin_addc(s, c, 0u, &c2);
-        return r + c2;
-    }
-};
-
-// Byte masks of a 16-byte segment as four dwords, in constant memory so that a wave
-// fetches them with one s_load_dwordx4 each (scalar cache) instead of computing them:
-//   kMaskFrom[f] keeps bytes [f, 16)  (head segment, f = S & 15)
-//   kMaskTo[t]   keeps bytes [0, t)   (tail segment, t in 1..16)
-constexpr uint32_t byte_range_dword(int lo, int hi, int d) {
-    uint32_t m = 0;
-    for (int b = 0; b < 4; ++b)
-        if (4 * d + b >= lo && 4 * d + b < hi) m |= 0xFFu << (8 * b);
-    return m;
-}
-#define AIPSTACK_MASK_FROM(f) \
-    {byte_range_dword(f, 16, 0), byte_range_dword(f, 16, 1), byte_range_dword(f, 16, 2), \
-     byte_range_dword(f, 16, 3)}
-#define AIPSTACK_MASK_TO(t) \
-    {byte_range_dword(0, t, 0), byte_range_dword(0, t, 1), byte_range_dword(0, t, 2), \
-     byte_range_dword(0, t, 3)}
-__constant__ uint32_t kMaskFrom[16][4] = {
-    AIPSTACK_MASK_FROM(0),  AIPSTACK_MASK_FROM(1),  AIPSTACK_MASK_FROM(2),  AIPSTACK_MASK_FROM(3),
-    AIPSTACK_MASK_FROM(4),  AIPSTACK_MASK_FROM(5),  AIPSTACK_MASK_FROM(6),  AIPSTACK_MASK_FROM(7),
-    AIPSTACK_MASK_FROM(8),  AIPSTACK_MASK_FROM(9),  AIPSTACK_MASK_FROM(10), AIPSTACK_MASK_FROM(11),
-    AIPSTACK_MASK_FROM(12), AIPSTACK_MASK_FROM(13), AIPSTACK_MASK_FROM(14), AIPSTACK_MASK_FROM(15)};
-__constant__ uint32_t kMaskTo[17][4] = {
-    AIPSTACK_MASK_TO(0),  AIPSTACK_MASK_TO(1),  AIPSTACK_MASK_TO(2),  AIPSTACK_MASK_TO(3),
-    AIPSTACK_MASK_TO(4),  AIPSTACK_MASK_TO(5),  AIPSTACK_MASK_TO(6),  AIPSTACK_MASK_TO(7),
-    AIPSTACK_MASK_TO(8),  AIPSTACK_MASK_TO(9),  AIPSTACK_MASK_TO(10), AIPSTACK_MASK_TO(11),
-    AIPSTACK_MASK_TO(12), AIPSTACK_MASK_TO(13), AIPSTACK_MASK_TO(14), AIPSTACK_MASK_TO(15),
-    AIPSTACK_MASK_TO(16)};
-#undef AIPSTACK_MASK_FROM
-#undef AIPSTACK_MASK_TO
-
-__device__ __forceinline__ u32x4 load_mask(const uint32_t (&m)[4]) {
-    return u32x4{m[0], m[1], m[2], m[3]};
-}
-
-// v & (m | sel): sel = ~0 keeps v (lanes the mask does not apply to), sel = 0 masks it.
-// One v_bitop3_b32 per dword.
-__device__ __forceinline__ void apply_mask(u32x4 &v, const u32x4 &m, uint32_t sel) {
-#pragma unroll
-    for (int d = 0; d < 4; ++d) v[d] &= (m[d] | sel);
-}
-
-// Buffer-load cache policy (aux): 2 = nt (streaming), 0 = default.
-template <bool NT>
-__device__ __forceinline__ u32x4 load_segment(__amdgpu_buffer_rsrc_t rsrc, uint32_t voff,
-                                              uint32_t soff) {
-    return __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, soff, NT ? 2 : 0);
-}
-
-// Sum over the 64 lanes (defined below).
-__device__ __forceinline__ uint32_t wave_sum(uint32_t v);
-
-// One packet's aligned-segment loads, split into issue() and finish() so that a wave
-// can keep several packets' loads in flight before it reduces the first of them.
-//
-// The packet [S, E) is read as the 16-byte-aligned segments A0 = S & ~15, A0 + 16, ...
-// through a buffer descriptor whose base is A0 and whose size is 16 * nseg: lane k reads
-// segment k (voffset = 16 * lane, soffset = 1 KiB per slot), and the hardware range check
-// returns zeros for segments past the end, with no exec masking. Bytes of the head
-// segment before S and of the tail segment from E on are masked off. Each lane keeps a
-// ones'-complement sum of its dwords; finish() folds it to 18 bits and adds the 64 lanes
-// exactly (< 2^24), returning a wave-uniform value that is 0 iff every byte is 0 and is
-// congruent (mod 0xFFFF) to the sum of the little-endian 16-bit halves.
-// U = segments per lane issued up front (group 0 = the first 64*U segments); longer
-// packets loop over further groups inside finish().
-template <int U, bool NT>
-struct PacketLoad {
-    uint64_t A0;
-    int rel_s;  // S - A0 (0..15)
-    int rel_e;  // E - A0
-    int nseg;   // aligned segments covering [S, E); 0 for an empty packet
-    __amdgpu_buffer_rsrc_t rsrc;
-    u32x4 v[U];
-
-    u32x4 hm, tm;  // head / tail byte masks
-
-    __device__ __forceinline__ void issue(uint64_t S, uint64_t E, uint32_t voff) {
-        A0 = S & ~(uint64_t)15;
-        rel_s = (int)(S - A0);
-        // Lengths of 2 GiB or more, and E < S, are outside every contract: empty packet.
-        const uint64_t len = E - S;
-        const bool empty = len == 0 || len >= (1ull << 31);
-        rel_e = empty ? rel_s : rel_s + (int)len;
-        nseg = empty ? 0 : (rel_e + 15) >> 4;
-        hm = load_mask(kMaskFrom[rel_s]);
-        tm = load_mask(kMaskTo[empty ? 16 : rel_e - 16 * (nseg - 1)]);
-        rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(A0), (short)0,
-                                                 nseg * 16, 0x00020000);
-        // Unconditional: slots past the packet fail the descriptor's range check and
-        // return zeros without touching memory. Keeping the loads straight-line lets the
-        // compiler count them, so finishing packet q waits only for q's loads
-        // (s_waitcnt vmcnt(N)), not for every packet in flight (a branch -> vmcnt(0)).
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            v[u] = load_segment<NT>(rsrc, voff, (uint32_t)(u * kWave * 16));
-    }
-
-    // Mask the tail segment `last` (lane lt of slot (last - g) >> 6) if it is in group g.
-    __device__ __forceinline__ void mask_tail(int g, int last, const u32x4 &tm,
-                                              uint32_t not_lt) {
-        if (last >= g && last < g + kWave * U) {
-            const int ut = (last - g) >> 6;
-            // Branch-free slot choice: an `if (u == ut)` chain gets merged by LLVM into one
-            // dynamically indexed v[ut], which lives in scratch.
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                apply_mask(v[u], tm, u == ut ? not_lt : ~0u);
-        }
-    }
-
-    // Two interleaved carry chains (even / odd dwords): independent v_addc_co_u32 fill
-    // each other's carry-hazard wait states.
-    __device__ __forceinline__ void accumulate(Eac &a0, Eac &a1) const {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            a0.add(v[u][0]);
-            a1.add(v[u][1]);
-            a0.add(v[u][2]);
-            a1.add(v[u][3]);
-        }
-    }
-
-    // not_lane0 = ~0 on every lane but lane 0 (where it is 0).
-    __device__ __forceinline__ uint32_t finish(int lane, uint32_t voff, uint32_t not_lane0) {
-        if (nseg == 0)
-            return 0;
-        const int last = nseg - 1;
-        const uint32_t not_lt = (lane == (last & (kWave - 1))) ? 0u : ~0u;
-        apply_mask(v[0], hm, not_lane0);  // head: segment 0 = slot 0, lane 0
-        mask_tail(0, last, tm, not_lt);
-        Eac acc0, acc1;
-        accumulate(acc0, acc1);
-        for (int g = kWave * U; g < nseg; g += kWave * U) {  // packets > 64*U segments
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                v[u] = load_segment<NT>(rsrc, voff, (uint32_t)((g + u * kWave) * 16));
-            mask_tail(g, last, tm, not_lt);
-            accumulate(acc0, acc1);
-        }
-        // fold each chain to 17 bits (nonzero stays nonzero): 2 x 64 lanes x 0x1FFFE < 2^24
-        const uint32_t s0 = acc0.finish(), s1 = acc1.finish();
-        return wave_sum((s0 & 0xFFFFu) + (s0 >> 16) + (s1 & 0xFFFFu) + (s1 >> 16));
-    }
-};
-
-// Sum over the 64 lanes (DPP row scan + row broadcasts); result valid in lane 63,
-// returned wave-uniform via readlane.
-__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
-    // dpp_ctrl: row_shr:n = 0x110 + n; row_bcast:15 = 0x142; row_bcast:31 = 0x143.
-    v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xF, 0xF, false);
-    v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xF, 0xF, false);
-    v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xF, 0xF, false);
-    v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xF, 0xF, false);
-    v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xA, 0xF, false);
-    v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xC, 0xF, false);
-    return __builtin_amdgcn_readlane(v, 63);
-}
-
-__device__ __forceinline__ uint32_t fold16(uint32_t s) {
-    s = (s & 0xFFFFu) + (s >> 16);
-    s = (s & 0xFFFFu) + (s >> 16);
-    return s;
-}
-
-__device__ __forceinline__ uint32_t bswap16(uint32_t x) {
-    return ((x & 0xFFu) << 8) | ((x >> 8) & 0xFFu);
-}
 
 // ---------------------------------------------------------------------------------
 // The kernel: wave w handles 64-packet chunks [w*cpw, (w+1)*cpw).

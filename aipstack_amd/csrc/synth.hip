@@ -122,3 +122,91 @@ extern "C" int aipstack_synth_apply_classes_device(void *d_buf, const uint64_t *
                        first_packet);
     return aipstack_amd::check_hip(hipGetLastError());
 }
+
+namespace {
+
+struct FrameShape {
+    uint32_t kind;     // 0 TCP, 1 UDP, 2 ICMP, 3 other proto, 4 ARP, 5 fragment (TCP/UDP)
+    uint32_t ihl;      // IPv4 header words
+    uint32_t l4hdr;    // L4 header bytes
+    uint32_t payload;  // bytes after the L4 header
+    uint32_t frame;    // total frame bytes (>= 60)
+};
+
+FrameShape frame_shape(uint64_t seed, uint64_t i, uint32_t max_payload) {
+    const uint64_t s = seed ^ AIPSTACK_SYNTH_FRAME_SALT;
+    const uint64_t r0 = aipstack_synth_word(s, 8 * i + 0);
+    const uint64_t r1 = aipstack_synth_word(s, 8 * i + 1);
+    const uint64_t r2 = aipstack_synth_word(s, 8 * i + 2);
+    const uint64_t r3 = aipstack_synth_word(s, 8 * i + 3);
+    FrameShape f;
+    const uint32_t k = (uint32_t)(r0 % 100);
+    f.kind = k < 50 ? 0 : k < 78 ? 1 : k < 88 ? 2 : k < 93 ? 3 : k < 97 ? 4 : 5;
+    f.ihl = (r1 % 100) < 85 ? 5u : 6u + (uint32_t)((r1 >> 8) % 10);
+    f.payload = (uint32_t)(r2 % ((uint64_t)max_payload + 1));
+    const uint32_t proto_kind = f.kind == 5 ? (uint32_t)((r3 >> 20) & 1) : f.kind;
+    f.l4hdr = proto_kind == 0 ? 20u + 4u * ((r3 % 100) < 70 ? 0u : (uint32_t)((r3 >> 8) % 11))
+            : proto_kind == 1 ? 8u : proto_kind == 2 ? 8u : 0u;
+    if (f.kind == 4) {  // ARP: 28-byte body
+        f.ihl = 0; f.l4hdr = 0; f.payload = 28;
+    }
+    uint32_t len = 14 + 4 * f.ihl + f.l4hdr + f.payload;
+    f.frame = len < 60 ? 60 : len;
+    return f;
+}
+
+inline void put16(uint8_t *p, uint32_t v) { p[0] = (uint8_t)(v >> 8); p[1] = (uint8_t)v; }
+
+}  // namespace
+
+extern "C" uint64_t aipstack_synth_frames_host(void *buf, uint64_t *offsets, uint64_t n,
+                                               uint64_t seed, uint32_t max_payload) {
+    uint64_t o = 0;
+    offsets[0] = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        o += frame_shape(seed, i, max_payload).frame;
+        offsets[i + 1] = o;
+    }
+    if (!buf) return o;
+    uint8_t *b = static_cast<uint8_t *>(buf);
+    aipstack_synth_fill_host(b, o, seed, 0);  // random bytes everywhere, then the headers
+    const uint64_t s = seed ^ AIPSTACK_SYNTH_FRAME_SALT;
+    for (uint64_t i = 0; i < n; ++i) {
+        const FrameShape f = frame_shape(seed, i, max_payload);
+        uint8_t *fr = b + offsets[i];
+        const uint64_t r3 = aipstack_synth_word(s, 8 * i + 3);
+        const uint64_t r4 = aipstack_synth_word(s, 8 * i + 4);
+        if (f.kind == 4) {
+            put16(fr + 12, 0x0806);
+            for (uint32_t j = 14 + 28; j < f.frame; ++j) fr[j] = 0;
+            continue;
+        }
+        put16(fr + 12, 0x0800);
+        uint8_t *ip = fr + 14;
+        const uint32_t hl = 4 * f.ihl;
+        const uint32_t total = hl + f.l4hdr + f.payload;
+        ip[0] = (uint8_t)(0x40 | f.ihl);
+        put16(ip + 2, total);
+        uint32_t flags_off = (r4 & 1) ? 0x4000u : 0u;  // DF sometimes
+        if (f.kind == 5)
+            flags_off = (r4 & 2) ? (0x2000u | (uint32_t)((r4 >> 8) % 0x2000)) : (uint32_t)(1 + (r4 >> 8) % 0x1FFF);
+        put16(ip + 6, flags_off);
+        ip[8] = 64;
+        const uint32_t proto_kind = f.kind == 5 ? (uint32_t)((r3 >> 20) & 1) : f.kind;
+        ip[9] = proto_kind == 0 ? 6 : proto_kind == 1 ? 17 : proto_kind == 2 ? 1 : 47;
+        put16(ip + 10, 0);
+        uint8_t *l4 = ip + hl;
+        if (proto_kind == 0) {
+            l4[12] = (uint8_t)(((f.l4hdr / 4) << 4) | (l4[12] & 0x0F));
+            put16(l4 + 16, 0);
+        } else if (proto_kind == 1) {
+            put16(l4 + 4, 8 + f.payload);
+            put16(l4 + 6, 0);
+        } else if (proto_kind == 2) {
+            l4[0] = (uint8_t)((r4 >> 16) % 3 == 0 ? 0 : (r4 >> 16) % 3 == 1 ? 8 : 3);
+            put16(l4 + 2, 0);
+        }
+        for (uint32_t j = 14 + total; j < f.frame; ++j) fr[j] = 0;  // Ethernet padding
+    }
+    return o;
+}

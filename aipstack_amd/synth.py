@@ -111,3 +111,14 @@ def apply_classes_device(tensor, d_offsets, len_seed: int = SEED_LENGTHS, first_
         int(s.cuda_stream))
     if st != 0:
         raise RuntimeError(f"aipstack_synth_apply_classes_device failed ({st})")
+
+
+def frames_host(n: int, seed: int = SEED_DATA, max_payload: int = 1400):
+    """(buf uint8, offsets int64) of n raw Ethernet frames with zero checksum fields
+    (aipstack_synth_frames_host; see include/aipstack_amd/synth.h for the mix)."""
+    lib = _lib.load()
+    off = np.zeros(n + 1, dtype=np.uint64)
+    total = lib.aipstack_synth_frames_host(None, off.ctypes.data, n, seed, max_payload)
+    buf = np.empty(max(total, 1), dtype=np.uint8)
+    lib.aipstack_synth_frames_host(buf.ctypes.data, off.ctypes.data, n, seed, max_payload)
+    return buf[:total], off.astype(np.int64)

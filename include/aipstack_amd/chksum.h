@@ -97,6 +97,37 @@ int aipstack_chksum_batch_chain(const uint64_t *d_chunk_addr, const uint32_t *d_
                                 const uint64_t *d_chunk_index, const uint32_t *d_states,
                                 uint64_t n, uint16_t *d_out, uint32_t flags, void *stream);
 
+/* ---- frame-level batches: Rx verify / Tx fill on raw Ethernet frames ------------------ */
+
+/* Per-frame verdicts of aipstack_chksum_rx_verify (and statuses of _tx_fill), restating the
+ * reference's receive-path decisions that involve checksums or the lengths they cover:
+ * eth/EthIpIface.h:367-390, ip/IpStack.h:936-1018 and :1093-1130 (ICMP),
+ * tcp/IpTcpProto_input.h:68-100, udp/IpUdpProto.h:470-490 and :631-652. Checks that need
+ * stack state (interface addresses, listeners, reassembly) stay with the host. */
+#define AIPSTACK_RX_NOT_IP4            0 /* < 14 bytes or EtherType != 0x0800 (e.g. ARP) */
+#define AIPSTACK_RX_DROP_IP_MALFORMED  1 /* IPv4 header/length checks fail (IpStack.h:938-990) */
+#define AIPSTACK_RX_DROP_IP_CHKSUM     2 /* IPv4 header checksum bad (IpStack.h:1016) */
+#define AIPSTACK_RX_FRAGMENT           3 /* header OK, MF or offset set: host reassembles */
+#define AIPSTACK_RX_DROP_L4_MALFORMED  4 /* TCP < 20 B, UDP length bad, ICMP < 8 B */
+#define AIPSTACK_RX_DROP_L4_CHKSUM     5 /* TCP/UDP/ICMP checksum bad */
+#define AIPSTACK_RX_ACCEPT             6 /* every checksum present verified */
+#define AIPSTACK_RX_ACCEPT_NO_CHKSUM   7 /* UDP with checksum field 0 = none (IpUdpProto.h:637) */
+#define AIPSTACK_RX_ACCEPT_OTHER       8 /* IPv4 header OK; protocol other than TCP/UDP/ICMP */
+
+/* Rx verify: frame i = bytes [d_offsets[i], d_offsets[i+1]) of d_base (an Ethernet frame,
+ * as the TAP driver delivers it); d_verdict[i] = one of AIPSTACK_RX_*. Read-only. */
+int aipstack_chksum_rx_verify(const void *d_base, const uint64_t *d_offsets, uint64_t n,
+                              uint8_t *d_verdict, void *stream);
+
+/* Tx fill, IN PLACE: for each IPv4 frame, write the IPv4 header checksum (field taken as 0,
+ * ip/IpStack.h:425-453) and, unless it is a fragment, the TCP / UDP (0 -> 0xFFFF) / ICMP
+ * checksum (tcp/IpTcpProto_output.h:1251-1277, udp/IpUdpProto.h:164-179,
+ * ip/IpStack.h:1164-1190). d_status[i]: AIPSTACK_RX_ACCEPT (filled), _ACCEPT_OTHER (IPv4
+ * header only), _FRAGMENT (IPv4 header only), _NOT_IP4 / _DROP_*_MALFORMED (untouched,
+ * or IPv4 header only for L4-malformed). Frames must not overlap. */
+int aipstack_chksum_tx_fill(void *d_base, const uint64_t *d_offsets, uint64_t n,
+                            uint8_t *d_status, void *stream);
+
 /* ---- 3. host-memory streaming engine ----------------------------------------------- */
 
 /* The reference's packet path starts and ends in host memory (TAP read()/write(),

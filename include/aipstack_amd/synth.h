@@ -50,6 +50,18 @@ int aipstack_synth_apply_classes_device(void *d_buf, const uint64_t *d_offsets, 
                                         uint64_t len_seed, uint64_t first_packet,
                                         void *stream);
 
+/* Host: n raw Ethernet frames with every checksum field zero (fill them with a Tx-fill
+ * pass). Writes offsets[0..n] (frames back to back, first at 0) and, if buf != NULL, the
+ * bytes; returns the total size. Per frame i, from word(seed ^ AIPSTACK_SYNTH_FRAME_SALT,
+ * 8i + k): 50 % TCP (20-60 B header), 28 % UDP, 10 % ICMP, 5 % other IP protocol (47),
+ * 4 % ARP (EtherType 0x0806), 3 % IPv4 fragments (MF / offset set); IHL 5 (85 %) or 6-15
+ * with option bytes; payload 0..max_payload bytes; frames shorter than 60 B are padded
+ * with zeros past the IPv4 total length (Ethernet minimum). Header fields other than
+ * lengths / protocol / checksums and all payload bytes are byte(seed, .) of the stream. */
+#define AIPSTACK_SYNTH_FRAME_SALT 0xF4A3E5ull
+uint64_t aipstack_synth_frames_host(void *buf, uint64_t *offsets, uint64_t n, uint64_t seed,
+                                    uint32_t max_payload);
+
 #ifdef __cplusplus
 }
 #endif

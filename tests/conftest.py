@@ -44,7 +44,26 @@ class Oracle:
         lib.oracle_batch_strided.argtypes = [vp, u64, u32, u64, vp, u32]
         lib.oracle_batch_csr.argtypes = [vp, vp, u64, vp, u32]
         lib.oracle_batch_seeded_csr.argtypes = [vp, vp, vp, u64, vp]
+        lib.oracle_rx_verify.restype = ctypes.c_int
+        lib.oracle_rx_verify.argtypes = [vp, sz]
+        lib.oracle_tx_fill.restype = ctypes.c_int
+        lib.oracle_tx_fill.argtypes = [vp, sz]
+        lib.oracle_rx_verify_batch.argtypes = [vp, vp, u64, vp]
+        lib.oracle_tx_fill_batch.argtypes = [vp, vp, u64, vp]
         self.lib = lib
+
+    def rx_verify_batch(self, buf, offsets):
+        o = np.ascontiguousarray(offsets, dtype=np.uint64)
+        out = np.empty(o.size - 1, dtype=np.uint8)
+        self.lib.oracle_rx_verify_batch(buf.ctypes.data, o.ctypes.data, o.size - 1, out.ctypes.data)
+        return out
+
+    def tx_fill_batch(self, buf, offsets):
+        """In place on the numpy buffer; returns statuses."""
+        o = np.ascontiguousarray(offsets, dtype=np.uint64)
+        out = np.empty(o.size - 1, dtype=np.uint8)
+        self.lib.oracle_tx_fill_batch(buf.ctypes.data, o.ctypes.data, o.size - 1, out.ctypes.data)
+        return out
 
     def inverted(self, arr: np.ndarray, off: int, length: int) -> int:
         return int(self.lib.oracle_chksum_inverted(arr.ctypes.data + off, length))

@@ -364,3 +364,55 @@ def test_chain_tcp_tx_shape(oracle):
                                    _d(np.array(idx, dtype=np.int64)),
                                    _d(np.array(states, dtype=np.int32)), final=True))
     assert np.array_equal(got, np.array(want, dtype=np.uint16))
+
+
+# ---- frame-level batches: Tx fill / Rx verify ----------------------
+
+def _corrupt(buf, off, frac, seed):
+    """Flip one random byte in a fraction of frames (header or payload)."""
+    rng = np.random.default_rng(seed)
+    n = off.size - 1
+    for i in np.nonzero(rng.random(n) < frac)[0]:
+        s, e = int(off[i]), int(off[i + 1])
+        j = s + int(rng.integers(12, e - s))
+        buf[j] ^= np.uint8(1 << int(rng.integers(0, 8)))
+
+
+@pytest.mark.parametrize("n,maxp", [(200000, 1460), (20000, 9000)])
+def test_tx_fill_matches_oracle(oracle, n, maxp):
+    buf, off = synth.frames_host(n, seed=11, max_payload=maxp)
+    dbuf, doff = _d(buf), _d(off)
+    st = _np(A.tx_fill(dbuf, doff))
+    want_buf = buf.copy()
+    want_st = oracle.tx_fill_batch(want_buf, off)
+    assert np.array_equal(st, want_st)
+    got_buf = _np(dbuf)
+    bad = np.nonzero(got_buf != want_buf)[0]
+    assert bad.size == 0, bad[:10]
+
+
+@pytest.mark.parametrize("n,maxp", [(200000, 1460), (20000, 9000)])
+def test_rx_verify_matches_oracle(oracle, n, maxp):
+    buf, off = synth.frames_host(n, seed=12, max_payload=maxp)
+    oracle.tx_fill_batch(buf, off)                 # valid frames ...
+    rng = np.random.default_rng(1)
+    for i in np.nonzero(rng.random(n) < 0.05)[0]:  # ... some UDP without checksum ...
+        s = int(off[i])
+        if buf[s + 12] == 8 and buf[s + 13] == 0 and buf[s + 23] == 17:
+            hl = int(buf[s + 14] & 15) * 4
+            buf[s + 14 + hl + 6: s + 14 + hl + 8] = 0
+    _corrupt(buf, off, 0.15, 2)                    # ... and 15 % with one flipped bit
+    got = _np(A.rx_verify(_d(buf), _d(off)))
+    want = oracle.rx_verify_batch(buf, off)
+    assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
+    kinds = set(np.unique(want).tolist())
+    assert {0, 2, 3, 5, 6, 7, 8} <= kinds          # the verdicts this mix must reach
+
+
+def test_fill_then_verify_on_gpu():
+    buf, off = synth.frames_host(100000, seed=13)
+    dbuf, doff = _d(buf), _d(off)
+    st = _np(A.tx_fill(dbuf, doff))
+    v = _np(A.rx_verify(dbuf, doff))
+    assert np.array_equal(st, v)
+    assert set(np.unique(v).tolist()) <= {0, 3, 6, 8}
