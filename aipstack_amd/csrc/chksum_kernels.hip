@@ -177,6 +177,7 @@ struct Tuning {
     std::atomic<int> chunks_per_wave{0};  // 64-packet chunks per wave (overrides the above)
     std::atomic<int> unroll{0};           // U: segments per lane issued up front (1..4)
     std::atomic<int> packets{0};          // P: packets whose loads a wave keeps in flight
+    std::atomic<int> frames{0};           // frames in flight per wave (frame kernels)
     std::atomic<int> nontemporal{1};      // 1 = nontemporal (streaming) loads: every byte is
                                           // read once; measured faster on configs A and B
 
@@ -189,6 +190,7 @@ struct Tuning {
         env("AIPSTACK_CHKSUM_UNROLL", unroll);
         env("AIPSTACK_CHKSUM_PACKETS", packets);
         env("AIPSTACK_CHKSUM_NT", nontemporal);
+        env("AIPSTACK_CHKSUM_FRAMES", frames);
     }
 };
 
@@ -294,6 +296,12 @@ int launch_chain(const uint64_t *d_addr, const uint32_t *d_len, const uint64_t *
 }
 
 }  // namespace
+
+int tuning_frames_in_flight() {
+    const int f = tuning().frames.load(std::memory_order_relaxed);
+    return (f == 1 || f == 2 || f == 4) ? f : 2;
+}
+
 }  // namespace aipstack_amd
 
 using namespace aipstack_amd;
@@ -341,6 +349,7 @@ extern "C" int aipstack_chksum_tune(const char *key, int value) {
     else if (!std::strcmp(key, "unroll")) t.unroll = value;
     else if (!std::strcmp(key, "packets")) t.packets = value;
     else if (!std::strcmp(key, "nontemporal")) t.nontemporal = value;
+    else if (!std::strcmp(key, "frames")) t.frames = value;
     else return AIPSTACK_CHKSUM_EINVAL;
     return AIPSTACK_CHKSUM_OK;
 }

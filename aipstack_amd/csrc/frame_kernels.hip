@@ -54,22 +54,14 @@ __device__ __forceinline__ uint32_t stage4(const uint32_t *st, int x) {
     const uint32_t r = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(x & 3));
     return __builtin_amdgcn_readfirstlane(r);
 }
-__device__ __forceinline__ uint32_t be16_at(const uint32_t *st, int x) {
-    const uint32_t w = stage4(st, x);
-    return ((w & 0xFFu) << 8) | ((w >> 8) & 0xFFu);
-}
-__device__ __forceinline__ uint32_t be32_at(const uint32_t *st, int x) {
-    return bswap32(stage4(st, x));
-}
-
-// Masked sum of the frame bytes [r0, r1) relative to A0, except the two bytes at fx
-// (fx < 0: none), over the segments the wave has loaded (group 0 in fl.v, further groups
-// loaded here). Returns the wave-uniform sum of the lanes' 17-bit folded ones'-complement
-// sums (< 2^24): congruent mod 0xFFFF to the little-endian 16-bit halves of those bytes,
-// 0 iff they are all 0.
+// This lane's share of the masked sum of the frame bytes [r0, r1) relative to A0, except
+// the two bytes at fx (fx < 0: none), over the segments the wave has loaded (group 0 in
+// fl.v, further groups loaded here): the lane's 18-bit folded ones'-complement sum. Summed
+// over the wave (< 2^24) it is congruent mod 0xFFFF to the little-endian 16-bit halves of
+// those bytes and 0 iff they are all 0.
 template <int U, bool NT>
-__device__ __forceinline__ uint32_t range_sum(PacketLoad<U, NT> &fl, int r0, int r1, int fx,
-                                              int lane, uint32_t voff) {
+__device__ __forceinline__ uint32_t range_lane(PacketLoad<U, NT> &fl, int r0, int r1, int fx,
+                                               int lane, uint32_t voff) {
     if (r1 <= r0)
         return 0;
     const int k0 = r0 >> 4, k1 = (r1 - 1) >> 4;
@@ -81,8 +73,7 @@ __device__ __forceinline__ uint32_t range_sum(PacketLoad<U, NT> &fl, int r0, int
     const u32x4 xm2 = load_mask(kMaskFrom[1]);      // byte 0 of segment kx+1 (bx == 15)
     const int kx2 = (fx >= 0 && bx == 15) ? kx + 1 : -2;
     Eac a0, a1;
-    const int last_seg = k1;
-    for (int g = 0; g <= last_seg; g += kWave * U) {
+    for (int g = 0; g <= k1; g += kWave * U) {
         if (g > 0) {
 #pragma unroll
             for (int u = 0; u < U; ++u)
@@ -95,8 +86,10 @@ __device__ __forceinline__ uint32_t range_sum(PacketLoad<U, NT> &fl, int r0, int
             u32x4 x = fl.v[u];
             apply_mask(x, hm, k == k0 ? 0u : ~0u);
             apply_mask(x, tm, k == k1 ? 0u : ~0u);
-            apply_mask(x, xm, k == kx ? 0u : ~0u);
-            apply_mask(x, xm2, k == kx2 ? 0u : ~0u);
+            if (fx >= 0) {  // wave-uniform: Tx only
+                apply_mask(x, xm, k == kx ? 0u : ~0u);
+                apply_mask(x, xm2, k == kx2 ? 0u : ~0u);
+            }
             a0.add(x[0] & in);
             a1.add(x[1] & in);
             a0.add(x[2] & in);
@@ -104,7 +97,24 @@ __device__ __forceinline__ uint32_t range_sum(PacketLoad<U, NT> &fl, int r0, int
         }
     }
     const uint32_t s0 = a0.finish(), s1 = a1.finish();
-    return wave_sum((s0 & 0xFFFFu) + (s0 >> 16) + (s1 & 0xFFFFu) + (s1 >> 16));
+    return (s0 & 0xFFFFu) + (s0 >> 16) + (s1 & 0xFFFFu) + (s1 >> 16);
+}
+
+// Two wave sums at once: the two DPP chains interleave, so neither waits on its own
+// data-hazard slots. Results wave-uniform.
+__device__ __forceinline__ void wave_sum2(uint32_t &a, uint32_t &b) {
+#define AIPSTACK_DPP2(ctrl, rowmask)                                                     \
+    a += __builtin_amdgcn_update_dpp(0u, a, ctrl, rowmask, 0xF, false);                  \
+    b += __builtin_amdgcn_update_dpp(0u, b, ctrl, rowmask, 0xF, false);
+    AIPSTACK_DPP2(0x111, 0xF)
+    AIPSTACK_DPP2(0x112, 0xF)
+    AIPSTACK_DPP2(0x114, 0xF)
+    AIPSTACK_DPP2(0x118, 0xF)
+    AIPSTACK_DPP2(0x142, 0xA)
+    AIPSTACK_DPP2(0x143, 0xC)
+#undef AIPSTACK_DPP2
+    a = __builtin_amdgcn_readlane(a, 63);
+    b = __builtin_amdgcn_readlane(b, 63);
 }
 
 // IpChksumAccumulator(words).getChksum() over a little-endian range sum `t` of bytes that
@@ -124,14 +134,119 @@ __device__ __forceinline__ void store_be16(uint64_t addr, uint32_t v) {
     p[1] = (uint8_t)v;
 }
 
+// One frame, its segment loads already issued into fl: stage the header, parse, sum,
+// decide (and for Tx, write the checksums). Returns the AIPSTACK_RX_* verdict / status.
 template <bool TX, int U, bool NT>
+__device__ __forceinline__ int process_frame(PacketLoad<U, NT> &fl, uint64_t S, int len,
+                                             uint32_t *st, int lane, uint32_t voff) {
+    const int rs = fl.rel_s;
+    // stage frame bytes [0, 112) (segments 0..7) in this wave's LDS slot
+    if (lane < kStageBytes / 16) {
+        st[4 * lane + 0] = fl.v[0][0];
+        st[4 * lane + 1] = fl.v[0][1];
+        st[4 * lane + 2] = fl.v[0][2];
+        st[4 * lane + 3] = fl.v[0][3];
+    }
+    __builtin_amdgcn_wave_barrier();
+    // all fixed-offset header dwords in one batch of LDS reads
+    const uint32_t w12 = stage4(st, rs + 12);  // EtherType | version/IHL | TOS
+    const uint32_t w16 = stage4(st, rs + 16);  // total length | ident
+    const uint32_t w20 = stage4(st, rs + 20);  // flags/offset | TTL | protocol
+    const uint32_t w28 = stage4(st, rs + 28);
+    const uint32_t w24 = stage4(st, rs + 24);
+    const uint32_t w32 = stage4(st, rs + 32);
+    const uint32_t ethertype = ((w12 & 0xFFu) << 8) | ((w12 >> 8) & 0xFFu);
+    // ---- Ethernet (EthIpIface.h:370-384)
+    if (len < 14 || ethertype != 0x0800)
+        return AIPSTACK_RX_NOT_IP4;
+    // ---- IPv4 header checks (IpStack.h:938-990)
+    const int plen = len - 14;
+    if (plen < 20)
+        return AIPSTACK_RX_DROP_IP_MALFORMED;
+    const uint32_t vihl = (w12 >> 16) & 0xFFu;
+    int hl = 20;
+    if (vihl != 0x45) {
+        hl = (int)(vihl & 0xFu) * 4;
+        if ((vihl >> 4) != 4 || hl < 20 || hl > plen)
+            return AIPSTACK_RX_DROP_IP_MALFORMED;
+    }
+    const int total_len = (int)(((w16 & 0xFFu) << 8) | ((w16 >> 8) & 0xFFu));
+    if (total_len < hl || total_len > plen)
+        return AIPSTACK_RX_DROP_IP_MALFORMED;
+    const uint32_t flags_off = ((w20 & 0xFFu) << 8) | ((w20 >> 8) & 0xFFu);
+    const bool fragment = (flags_off & 0x3FFFu) != 0;                  // IpStack.h:1020
+    const uint32_t proto = w20 >> 24;
+    const uint32_t src = bswap32((w24 >> 16) | (w28 << 16));
+    const uint32_t dst = bswap32((w28 >> 16) | (w32 << 16));
+    // ---- L4: which bytes the checksum covers, or a verdict without one
+    const int dg = 14 + hl;
+    const int dlen = total_len - hl;
+    const uint32_t pseudo_sa = (src >> 16) + (src & 0xFFFFu) + (dst >> 16) + (dst & 0xFFFFu);
+    int l4len = -1, fld = 0, l4verdict = AIPSTACK_RX_ACCEPT_OTHER;
+    uint32_t words = 0;
+    bool udp = false;
+    if (!fragment) {
+        if (proto == 6) {                                              // TCP
+            if (dlen < 20) l4verdict = AIPSTACK_RX_DROP_L4_MALFORMED;
+            else { l4len = dlen; fld = dg + 16; words = pseudo_sa + 6 + (uint32_t)dlen; }
+        } else if (proto == 17) {                                      // UDP
+            if (dlen < 8) {
+                l4verdict = AIPSTACK_RX_DROP_L4_MALFORMED;
+            } else {
+                const uint32_t w = stage4(st, rs + dg + 4);
+                const int ulen = (int)(((w & 0xFFu) << 8) | ((w >> 8) & 0xFFu));
+                const uint32_t ucs = ((w >> 8) & 0xFF00u) | (w >> 24);
+                if (ulen < 8 || ulen > dlen) {
+                    l4verdict = AIPSTACK_RX_DROP_L4_MALFORMED;
+                } else if (!TX && ucs == 0) {
+                    l4verdict = AIPSTACK_RX_ACCEPT_NO_CHKSUM;          // IpUdpProto.h:637
+                } else {
+                    l4len = ulen; fld = dg + 6; words = pseudo_sa + 17 + (uint32_t)ulen;
+                    udp = true;
+                }
+            }
+        } else if (proto == 1) {                                       // ICMP
+            if (dlen < 8) l4verdict = AIPSTACK_RX_DROP_L4_MALFORMED;
+            else { l4len = dlen; fld = dg + 2; }
+        }
+    }
+    // ---- both sums, one interleaved reduction: header word `lane` (LDS), L4 bytes (regs)
+    uint32_t hw = 0;
+    if (2 * lane < hl && !(TX && lane == 5)) {
+        const uint8_t *sb = reinterpret_cast<const uint8_t *>(st);
+        const int o = rs + 14 + 2 * lane;
+        hw = ((uint32_t)sb[o] << 8) | sb[o + 1];
+    }
+    const int r0 = rs + dg;
+    uint32_t lw = l4len >= 0 ? range_lane<U, NT>(fl, r0, r0 + l4len, TX ? rs + fld : -1, lane, voff)
+                             : 0u;
+    wave_sum2(hw, lw);
+    const uint32_t hchk = (~fold16(hw)) & 0xFFFFu;                     // IpStack.h:1016
+    if (TX) {
+        if (lane == 0) store_be16(S + 24, hchk);
+    } else if (hchk != 0) {
+        return AIPSTACK_RX_DROP_IP_CHKSUM;
+    }
+    if (fragment)
+        return AIPSTACK_RX_FRAGMENT;
+    if (l4len < 0)
+        return l4verdict;
+    uint32_t chk = finish_chksum(words, lw, S + (uint64_t)dg);
+    if (TX) {
+        if (udp && chk == 0) chk = 0xFFFFu;                            // IpUdpProto.h:176-178
+        if (lane == 0) store_be16(S + (uint64_t)fld, chk);
+        return AIPSTACK_RX_ACCEPT;
+    }
+    return chk == 0 ? AIPSTACK_RX_ACCEPT : AIPSTACK_RX_DROP_L4_CHKSUM;
+}
+
+template <bool TX, int U, int P, bool NT>
 __global__ __launch_bounds__(kBlock) void frame_kernel(CsrDesc desc, uint64_t n,
                                                        uint32_t chunks_per_wave,
                                                        uint8_t *__restrict__ status) {
-    __shared__ uint32_t stage_all[kWavesPerBlock][kStageBytes / 4 + 1];
+    __shared__ uint32_t stage_all[kWavesPerBlock][P][kStageBytes / 4 + 1];
     const int lane = threadIdx.x & (kWave - 1);
     const uint32_t wave_in_block = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    uint32_t *st = stage_all[wave_in_block];
     const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerBlock + wave_in_block;
     const uint64_t nchunks = (n + kWave - 1) / kWave;
     uint64_t c = wave * chunks_per_wave;
@@ -143,120 +258,28 @@ __global__ __launch_bounds__(kBlock) void frame_kernel(CsrDesc desc, uint64_t n,
         const auto chunk = desc.begin_chunk(p0, n, lane);
         const int cnt = (int)min((uint64_t)kWave, n - p0);
         uint32_t verdicts = 0;
-        for (int j = 0; j < cnt; ++j) {
-            uint64_t S, E;
-            desc.bounds(chunk, j, S, E);
-            const uint64_t len64 = E - S;
-            const int len = len64 >= (1ull << 31) ? 0 : (int)len64;  // out of contract: empty
-            PacketLoad<U, NT> fl;
-            fl.issue(S, S + (uint64_t)len, voff);
-            const int rs = fl.rel_s;
-            // stage frame bytes [0, 112) (segments 0..7) for the header parse
-            if (lane < kStageBytes / 16) {
-                st[4 * lane + 0] = fl.v[0][0];
-                st[4 * lane + 1] = fl.v[0][1];
-                st[4 * lane + 2] = fl.v[0][2];
-                st[4 * lane + 3] = fl.v[0][3];
+        for (int j0 = 0; j0 < cnt; j0 += P) {
+            PacketLoad<U, NT> fl[P];
+            uint64_t S[P];
+            int len[P];
+#pragma unroll
+            for (int q = 0; q < P; ++q) {  // P frames' loads in flight
+                uint64_t s = 0, e = 0;
+                if (j0 + q < cnt)
+                    desc.bounds(chunk, j0 + q, s, e);
+                const uint64_t l64 = e - s;
+                len[q] = l64 >= (1ull << 31) ? 0 : (int)l64;  // out of contract: empty
+                S[q] = s;
+                fl[q].issue(s, s + (uint64_t)len[q], voff);
             }
-            if (lane == 0) st[kStageBytes / 4] = 0;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-
-            int verdict;
-            // ---- Ethernet (EthIpIface.h:370-384)
-            const uint32_t w12 = stage4(st, rs + 12);  // EtherType, version/IHL, TOS
-            const uint32_t ethertype = ((w12 & 0xFFu) << 8) | ((w12 >> 8) & 0xFFu);
-            if (len < 14 || ethertype != 0x0800) {
-                verdict = AIPSTACK_RX_NOT_IP4;
-            } else {
-                // ---- IPv4 header checks (IpStack.h:938-990)
-                const int plen = len - 14;
-                const uint32_t vihl = (w12 >> 16) & 0xFFu;
-                int hl = 20;
-                verdict = -1;
-                if (plen < 20) {
-                    verdict = AIPSTACK_RX_DROP_IP_MALFORMED;
-                } else if (vihl != 0x45) {
-                    hl = (int)(vihl & 0xFu) * 4;
-                    if ((vihl >> 4) != 4 || hl < 20 || hl > plen)
-                        verdict = AIPSTACK_RX_DROP_IP_MALFORMED;
-                }
-                const int total_len = (int)be16_at(st, rs + 16);
-                if (verdict < 0 && (total_len < hl || total_len > plen))
-                    verdict = AIPSTACK_RX_DROP_IP_MALFORMED;
-                if (verdict < 0) {
-                    // ---- IPv4 header checksum: lane l adds header word l (LDS)
-                    uint32_t wsum = 0;
-                    if (2 * lane < hl && !(TX && lane == 5)) {
-                        const uint8_t *sb = reinterpret_cast<const uint8_t *>(st);
-                        const int o = rs + 14 + 2 * lane;
-                        wsum = ((uint32_t)sb[o] << 8) | sb[o + 1];
-                    }
-                    const uint32_t hsum = wave_sum(wsum);
-                    const uint32_t hchk = (~fold16(hsum)) & 0xFFFFu;
-                    if (TX) {
-                        if (lane == 0) store_be16(S + 24, hchk);
-                    } else if (hchk != 0) {
-                        verdict = AIPSTACK_RX_DROP_IP_CHKSUM;       // IpStack.h:1016
-                    }
-                    const uint32_t flags_off = be16_at(st, rs + 20);
-                    if (verdict < 0 && (flags_off & 0x3FFFu) != 0)
-                        verdict = AIPSTACK_RX_FRAGMENT;             // IpStack.h:1020
-                }
-                if (verdict < 0) {
-                    const uint32_t proto = (stage4(st, rs + 20) >> 24) & 0xFFu;
-                    const uint32_t src = be32_at(st, rs + 26);
-                    const uint32_t dst = be32_at(st, rs + 30);
-                    const int dg = 14 + hl;                     // datagram offset in frame
-                    const int dlen = total_len - hl;
-                    const uint32_t pseudo_sa =
-                        (src >> 16) + (src & 0xFFFFu) + (dst >> 16) + (dst & 0xFFFFu);
-                    int l4len = -1, fld = -1;
-                    uint32_t words = 0;
-                    bool udp_zero_ok = false;
-                    if (proto == 6) {                           // TCP
-                        if (dlen < 20) verdict = AIPSTACK_RX_DROP_L4_MALFORMED;
-                        else { l4len = dlen; fld = dg + 16; words = pseudo_sa + 6 + (uint32_t)dlen; }
-                    } else if (proto == 17) {                   // UDP
-                        if (dlen < 8) {
-                            verdict = AIPSTACK_RX_DROP_L4_MALFORMED;
-                        } else {
-                            const uint32_t w = stage4(st, rs + dg + 4);
-                            const int ulen = (int)(((w & 0xFFu) << 8) | ((w >> 8) & 0xFFu));
-                            const uint32_t ucs = ((w >> 8) & 0xFF00u) | (w >> 24);
-                            if (ulen < 8 || ulen > dlen) {
-                                verdict = AIPSTACK_RX_DROP_L4_MALFORMED;
-                            } else if (!TX && ucs == 0) {
-                                verdict = AIPSTACK_RX_ACCEPT_NO_CHKSUM;  // IpUdpProto.h:637
-                            } else {
-                                l4len = ulen; fld = dg + 6; words = pseudo_sa + 17 + (uint32_t)ulen;
-                                udp_zero_ok = true;
-                            }
-                        }
-                    } else if (proto == 1) {                    // ICMP
-                        if (dlen < 8) verdict = AIPSTACK_RX_DROP_L4_MALFORMED;
-                        else { l4len = dlen; fld = dg + 2; words = 0; }
-                    } else {
-                        verdict = AIPSTACK_RX_ACCEPT_OTHER;
-                    }
-                    if (l4len >= 0) {
-                        const int r0 = rs + dg;
-                        const uint32_t t = range_sum<U, NT>(fl, r0, r0 + l4len,
-                                                            TX ? rs + fld : -1, lane, voff);
-                        uint32_t chk = finish_chksum(words, t, S + (uint64_t)dg);
-                        if (TX) {
-                            if (udp_zero_ok && chk == 0) chk = 0xFFFFu;  // IpUdpProto.h:176-178
-                            if (lane == 0) store_be16(S + (uint64_t)fld, chk);
-                            verdict = AIPSTACK_RX_ACCEPT;
-                        } else {
-                            verdict = chk == 0 ? AIPSTACK_RX_ACCEPT : AIPSTACK_RX_DROP_L4_CHKSUM;
-                        }
-                    }
-                }
+#pragma unroll
+            for (int q = 0; q < P; ++q) {
+                const int v = process_frame<TX, U, NT>(fl[q], S[q], len[q],
+                                                       stage_all[wave_in_block][q], lane, voff);
+                verdicts = (lane == j0 + q) ? (uint32_t)v : verdicts;
             }
-            // the stage is reused by the next frame: order its reads before those writes
+            // the stage slots are rewritten by the next frames: reads before writes
             __builtin_amdgcn_wave_barrier();
-            verdicts = (lane == j) ? (uint32_t)verdict : verdicts;
         }
         if (lane < cnt)
             status[p0 + lane] = (uint8_t)verdicts;
@@ -276,8 +299,19 @@ int launch_frames(const void *d_base, const uint64_t *d_offsets, uint64_t n, uin
     const uint64_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
     if (blocks > 0x7FFFFFFFull || cpw > 0xFFFFFFFFull) return AIPSTACK_CHKSUM_EINVAL;
     CsrDesc desc{(uint64_t)(uintptr_t)d_base, d_offsets};
-    hipLaunchKernelGGL((frame_kernel<TX, 2, true>), dim3((unsigned)blocks), dim3(kBlock), 0,
-                       stream, desc, n, (uint32_t)cpw, d_status);
+    switch (tuning_frames_in_flight()) {
+        case 1:
+            hipLaunchKernelGGL((frame_kernel<TX, 2, 1, true>), dim3((unsigned)blocks), dim3(kBlock),
+                               0, stream, desc, n, (uint32_t)cpw, d_status);
+            break;
+        case 4:
+            hipLaunchKernelGGL((frame_kernel<TX, 2, 4, true>), dim3((unsigned)blocks), dim3(kBlock),
+                               0, stream, desc, n, (uint32_t)cpw, d_status);
+            break;
+        default:
+            hipLaunchKernelGGL((frame_kernel<TX, 2, 2, true>), dim3((unsigned)blocks), dim3(kBlock),
+                               0, stream, desc, n, (uint32_t)cpw, d_status);
+    }
     return check_hip(hipGetLastError());
 }
 

@@ -39,11 +39,18 @@ CONFIGS = {
     "A": ("strided", 1 << 20, 1500),
     "B": ("strided", 256 << 10, 9000),
     "C": ("csr", 2 << 20, None),
+    # SURVEY 8(f) rows 2-3 (not BASELINE metric lines): raw Ethernet frames
+    "RX": ("rx", 1 << 20, None),
+    "TX": ("tx", 1 << 20, None),
 }
 WORKLOAD_NAMES = {
     "A": "1M x 1500B Ethernet-MTU packets per GPU, IP checksum (BASELINE configs[1]; x8 = configs[4])",
     "B": "256K x 9000B jumbo packets per GPU, IP checksum (BASELINE configs[2])",
     "C": "2M mixed 64-1500B packets per GPU incl. odd lengths/starts, CSR (BASELINE configs[3])",
+    "RX": "1M raw Ethernet frames per GPU (TCP/UDP/ICMP/other/ARP/fragments, 0-1460B payload), "
+          "Rx verify: IPv4 header + L4 checksum verdicts",
+    "TX": "1M raw Ethernet frames per GPU (same mix), Tx fill: IPv4 header + L4 checksums "
+          "written in place",
 }
 
 
@@ -87,6 +94,12 @@ def shard_spec(config, rank, world, n=None):
         spec["total"] = n * plen
         spec["byte_offset"] = rank * n * plen
         spec["offsets"] = None
+    elif layout in ("rx", "tx"):
+        # each rank synthesises its own frames (seed per rank): frames are independent
+        spec["seed"] = synth.SEED_DATA + 1000 * rank
+        spec["byte_offset"] = 0
+        spec["offsets"] = None  # known after synthesis
+        spec["total"] = None
     else:
         off_all = synth.mixed_offsets(n * world)
         spec["offsets"] = off_all[rank * n:(rank + 1) * n + 1] - off_all[rank * n]
@@ -98,6 +111,17 @@ def shard_spec(config, rank, world, n=None):
 def host_shard(spec):
     """The shard's bytes in host memory (numpy), exactly as the device generators make them."""
     from aipstack_amd import synth
+    if spec["layout"] in ("rx", "tx"):
+        buf, off = synth.frames_host(spec["n"], seed=spec["seed"], max_payload=1460)
+        spec["offsets"], spec["total"] = off, int(off[-1])
+        if spec["layout"] == "rx":  # valid frames: fill with the oracle (test infrastructure)
+            lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "libchksum_oracle.so"))
+            lib.oracle_tx_fill_batch.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_uint64,
+                                                                         ctypes.c_void_p]
+            st = np.empty(spec["n"], dtype=np.uint8)
+            o = off.astype(np.uint64)
+            lib.oracle_tx_fill_batch(buf.ctypes.data, o.ctypes.data, spec["n"], st.ctypes.data)
+        return buf
     host = np.empty(spec["total"], dtype=np.uint8)
     synth.fill_host(host, synth.SEED_DATA, spec["byte_offset"])
     if spec["layout"] == "csr":
@@ -106,7 +130,10 @@ def host_shard(spec):
 
 
 def algorithmic_bytes(layout, n, total_payload):
-    """L bytes read + 2 bytes written per packet (+8 B offset for CSR)."""
+    """L bytes read + 2 bytes written per packet (+8 B offset for CSR).
+    Frames: L read + 8 B offset + 1 B verdict/status (+ 4 B of checksums written, Tx)."""
+    if layout in ("rx", "tx"):
+        return total_payload + 9 * n + 8 + (4 * n if layout == "tx" else 0)
     b = total_payload + 2 * n
     if layout == "csr":
         b += 8 * (n + 1)
@@ -220,11 +247,17 @@ def main():
 
     # ---- this rank's shard, generated in place (global packets [rank*n, (rank+1)*n))
     spec = shard_spec(args.config, rank, world)
+    if layout in ("rx", "tx"):
+        frames_host = host_shard(spec)          # frames are synthesised on the host
+        buf = torch.from_numpy(frames_host).to(dev)
+        d_off = torch.from_numpy(spec["offsets"]).to(dev)
+        status = torch.empty(n, dtype=torch.uint8, device=dev)
     off_host = spec["offsets"]
     byte_offset = spec["byte_offset"]
     total = spec["total"]
-    buf = torch.empty(total, dtype=torch.uint8, device=dev)
-    synth.fill_device(buf, synth.SEED_DATA, byte_offset)
+    if layout in ("strided", "csr"):
+        buf = torch.empty(total, dtype=torch.uint8, device=dev)
+        synth.fill_device(buf, synth.SEED_DATA, byte_offset)
     if layout == "csr":
         d_off = torch.from_numpy(off_host).to(dev)
         synth.apply_classes_device(buf, d_off, first_packet=spec["first_packet"])
@@ -234,8 +267,12 @@ def main():
     def step():
         if layout == "strided":
             A.chksum_batch_strided(buf, plen, plen, n, out=out, stream=stream)
-        else:
+        elif layout == "csr":
             A.chksum_batch_csr(buf, d_off, out=out, stream=stream)
+        elif layout == "rx":
+            A.rx_verify(buf, d_off, out=status, stream=stream)
+        else:  # tx: idempotent (the filled fields are excluded from their own sums)
+            A.tx_fill(buf, d_off, out=status, stream=stream)
 
     for _ in range(args.warmup):
         step()
@@ -271,7 +308,10 @@ def main():
     # ---- parity of this run's output against the oracle / reference (rank 0 sample)
     parity = None
     cpu = None
-    if rank == 0:
+    if rank == 0 and layout in ("rx", "tx"):
+        if not args.no_parity:
+            parity = frames_check(spec, frames_host, buf.cpu().numpy(), status.cpu().numpy())
+    elif rank == 0:
         host_out = out.cpu().numpy()
         if not args.no_cpu_baseline and world == 1:
             cpu, want = cpu_baseline(spec)
@@ -300,7 +340,8 @@ def main():
             "workload": WORKLOAD_NAMES[args.config],
             "config": args.config,
             "packets_per_gpu": n,
-            "packet_bytes": plen if plen else "64-1500 (mixed)",
+            "packet_bytes": plen if plen else ("64-1500 (mixed)" if layout == "csr"
+                                                else "60-1514 (frames)"),
             "payload_bytes_per_gpu": payload,
             "layout": layout,
             "parallelism": f"disjoint packet shards x{world}, no collective",
@@ -391,6 +432,20 @@ def e2e(args, rank, world, local_rank, layout, n, plen):
     eng.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def frames_check(spec, frames_before, frames_after, status):
+    """Frames: statuses (and, for Tx, the filled frames) vs the oracle on the host."""
+    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "libchksum_oracle.so"))
+    o = spec["offsets"].astype(np.uint64)
+    n = spec["n"]
+    want = np.empty(n, dtype=np.uint8)
+    fn = lib.oracle_rx_verify_batch if spec["layout"] == "rx" else lib.oracle_tx_fill_batch
+    fn.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_uint64, ctypes.c_void_p]
+    ref = frames_before.copy()
+    fn(ref.ctypes.data, o.ctypes.data, n, want.ctypes.data)
+    ok = np.array_equal(status, want) and np.array_equal(frames_after, ref)
+    return "bit-exact (verdicts/frames vs oracle)" if ok else "MISMATCH"
 
 
 def oracle_check(spec, got):
