@@ -56,6 +56,12 @@ struct StridedDesc {
     __device__ __forceinline__ uint64_t lane_start(const Chunk &c, int lane) const {
         return c.s0 + (uint64_t)lane * stride;
     }
+    // This lane's packet (chunk packet `lane`) as [S, E) in VGPRs.
+    __device__ __forceinline__ void lane_bounds(const Chunk &c, int lane, uint64_t &S,
+                                                uint64_t &E) const {
+        S = c.s0 + (uint64_t)lane * stride;
+        E = S + len;
+    }
     __device__ __forceinline__ uint32_t lane_seed(const Chunk &) const { return 0; }
 };
 
@@ -91,6 +97,15 @@ struct CsrDesc {
     }
     __device__ __forceinline__ uint64_t lane_start(const Chunk &c, int) const {
         return base + (((uint64_t)c.off_hi << 32) | c.off_lo);
+    }
+    // This lane's packet as [S, E): its offset and the next lane's (lane 63: end_off).
+    __device__ __forceinline__ void lane_bounds(const Chunk &c, int lane, uint64_t &S,
+                                                uint64_t &E) const {
+        const uint32_t nlo = (uint32_t)__shfl_down((int)c.off_lo, 1);
+        const uint32_t nhi = (uint32_t)__shfl_down((int)c.off_hi, 1);
+        const uint64_t next = lane == kWave - 1 ? c.end_off : (((uint64_t)nhi << 32) | nlo);
+        S = base + (((uint64_t)c.off_hi << 32) | c.off_lo);
+        E = base + next;
     }
     __device__ __forceinline__ uint32_t lane_seed(const Chunk &) const { return 0; }
 };
@@ -181,6 +196,25 @@ __device__ __forceinline__ u32x4 load_segment(__amdgpu_buffer_rsrc_t rsrc, uint3
 // Sum over the 64 lanes (defined below).
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v);
 
+// Per-packet load parameters, computed for 64 packets at once (lane j <-> packet j, VALU)
+// and fetched per packet with three v_readlane: the aligned base A0 = S & ~15 and a
+// packed word {rel_s = S & 15 : 4 | tail bytes t (1..16) : 5 | nseg : 23}. Lengths of
+// 2^26 bytes or more, and E < S, are outside every contract and packed as empty.
+struct LaneMeta {
+    uint32_t a0_lo, a0_hi, packed;
+};
+
+__device__ __forceinline__ LaneMeta lane_meta(uint64_t S, uint64_t E) {
+    const uint64_t len = E - S;
+    const bool empty = ((len - 1) >> 26) != 0;
+    const uint32_t rs = (uint32_t)S & 15u;
+    const uint32_t re = rs + (empty ? 0u : (uint32_t)len);
+    const uint32_t nseg = empty ? 0u : (re + 15u) >> 4;
+    const uint32_t t = empty ? 16u : ((re - 1u) & 15u) + 1u;
+    const uint64_t a0 = S & ~(uint64_t)15;
+    return LaneMeta{(uint32_t)a0, (uint32_t)(a0 >> 32), rs | (t << 4) | (nseg << 9)};
+}
+
 // One packet's aligned-segment loads, split into issue() and finish() so that a wave
 // can keep several packets' loads in flight before it reduces the first of them.
 //
@@ -207,20 +241,38 @@ struct PacketLoad {
 
     __device__ __forceinline__ void issue(uint64_t S, uint64_t E, uint32_t voff) {
         A0 = S & ~(uint64_t)15;
-        rel_s = (int)(S - A0);
+        rel_s = (int)(S & 15);
         // Lengths of 2 GiB or more, and E < S, are outside every contract: empty packet.
+        // ((len - 1) >> 31) != 0  <=>  len == 0 || len >= 2^31, in SALU-only 64-bit ops
+        // (gfx950 SALU has no unsigned 64-bit ordered compare).
         const uint64_t len = E - S;
-        const bool empty = len == 0 || len >= (1ull << 31);
-        rel_e = empty ? rel_s : rel_s + (int)len;
+        const bool empty = ((len - 1) >> 31) != 0;
+        rel_e = rel_s + (empty ? 0 : (int)(uint32_t)len);
         nseg = empty ? 0 : (rel_e + 15) >> 4;
         hm = load_mask(kMaskFrom[rel_s]);
-        tm = load_mask(kMaskTo[empty ? 16 : rel_e - 16 * (nseg - 1)]);
+        tm = load_mask(kMaskTo[empty ? 16 : ((rel_e - 1) & 15) + 1]);  // tail bytes, 1..16
         rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(A0), (short)0,
                                                  nseg * 16, 0x00020000);
         // Unconditional: slots past the packet fail the descriptor's range check and
         // return zeros without touching memory. Keeping the loads straight-line lets the
         // compiler count them, so finishing packet q waits only for q's loads
         // (s_waitcnt vmcnt(N)), not for every packet in flight (a branch -> vmcnt(0)).
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            v[u] = load_segment<NT>(rsrc, voff, (uint32_t)(u * kWave * 16));
+    }
+
+    // issue() from a packed LaneMeta (wave-uniform values read back with v_readlane).
+    __device__ __forceinline__ void issue_meta(uint64_t a0, uint32_t packed, uint32_t voff) {
+        A0 = a0;
+        rel_s = (int)(packed & 15u);
+        const int t = (int)((packed >> 4) & 31u);
+        nseg = (int)(packed >> 9);
+        rel_e = nseg > 0 ? 16 * (nseg - 1) + t : rel_s;
+        hm = load_mask(kMaskFrom[rel_s]);
+        tm = load_mask(kMaskTo[t]);
+        rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(A0), (short)0,
+                                                 nseg * 16, 0x00020000);
 #pragma unroll
         for (int u = 0; u < U; ++u)
             v[u] = load_segment<NT>(rsrc, voff, (uint32_t)(u * kWave * 16));

@@ -67,16 +67,23 @@ __global__ __launch_bounds__(kBlock) void chksum_batch_kernel(Desc desc, uint64_
         const uint64_t p0 = c * kWave;
         const auto chunk = desc.begin_chunk(p0, n, lane);
         const int cnt = (int)min((uint64_t)kWave, n - p0);
+        // every packet's load parameters at once: lane j <-> packet j (VALU, vectorised)
+        uint64_t lS, lE;
+        desc.lane_bounds(chunk, lane, lS, lE);
+        if (lane >= cnt) lE = lS;  // past the batch: empty
+        const LaneMeta meta = lane_meta(lS, lE);
         uint32_t sums = 0;  // lane j: exact halves-sum of packet j (< 2^24)
         // P packets at a time: all their first-group loads in flight, then reduce each.
         for (int j0 = 0; j0 < cnt; j0 += P) {
             PacketLoad<U, NT> pk[P];
 #pragma unroll
             for (int q = 0; q < P; ++q) {
-                uint64_t s = 0, e = 0;
-                if (j0 + q < cnt)
-                    desc.bounds(chunk, j0 + q, s, e);
-                pk[q].issue(s, e, voff);
+                const int j = min(j0 + q, kWave - 1);  // j0 + q >= cnt: an empty lane
+                const uint64_t a0 = ((uint64_t)__builtin_amdgcn_readlane(meta.a0_hi, j) << 32) |
+                                    (uint32_t)__builtin_amdgcn_readlane(meta.a0_lo, j);
+                const uint32_t packed =
+                    j0 + q < cnt ? (uint32_t)__builtin_amdgcn_readlane(meta.packed, j) : 16u << 4;
+                pk[q].issue_meta(a0, packed, voff);
             }
 #pragma unroll
             for (int q = 0; q < P; ++q) {
@@ -86,7 +93,7 @@ __global__ __launch_bounds__(kBlock) void chksum_batch_kernel(Desc desc, uint64_
         }
         // Finalise the chunk's 64 results together (VALU, one packet per lane).
         uint32_t r = fold16(sums);
-        if ((desc.lane_start(chunk, lane) & 1) == 0)
+        if ((meta.packed & 1u) == 0)  // S even (A0 is 16-aligned, so S & 1 = rel_s & 1)
             r = bswap16(r);  // little-endian pairing -> the reference's big-endian words
         if constexpr (SEEDED) {
             // IpChksumAccumulator(State): m_sum = state; m_sum += r with end-around
@@ -213,14 +220,14 @@ int pick_unroll(uint32_t max_len) {
     return 4;
 }
 
-// P: packets whose loads a wave keeps in flight. Measured (tools/sweep.py, MI355X):
-// 1500 B strided best at P = 4..8, 9000 B at P = 1 (U = 3 already has 3 KiB in flight
-// per wave), mixed CSR at P = 2.
+// P: packets whose loads a wave keeps in flight. Measured (tools/sweep.py, MI355X,
+// profiles/r01/sweep_*.jsonl): 1500 B strided best at P = 8, 9000 B at P = 1 (U = 3
+// already has 3 KiB in flight per wave), mixed 64-1500 B CSR at P = 4.
 int pick_packets(int u, bool csr) {
     const int t = tuning().packets.load(std::memory_order_relaxed);
     if (t == 1 || t == 2 || t == 4 || t == 8) return t;
-    if (csr) return 2;
-    return u <= 2 ? 4 : 1;
+    if (csr) return 4;
+    return u <= 2 ? 8 : 1;
 }
 
 template <class Desc, int U, int P, bool NT, bool SEEDED>

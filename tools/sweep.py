@@ -23,12 +23,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 DEFAULT_VARIANTS = {
-    "A": "0,0,1,0;2,1,1,0;2,2,1,0;2,4,1,0;2,8,1,0;2,4,0,0;2,8,0,0;2,4,1,32;2,4,1,128;"
-         "2,8,1,32;2,8,1,128;3,4,1,0;3,2,1,0",
+    "A": "0,0,1,0;2,1,1,0;2,2,1,0;2,4,1,0;2,8,1,0;2,8,0,0;2,8,1,32;2,8,1,128;2,8,1,256;"
+         "3,4,1,0;3,8,1,0",
     "B": "0,0,1,0;3,1,1,0;3,2,1,0;3,4,1,0;3,2,0,0;4,1,1,0;4,2,1,0;2,4,1,0;2,2,1,0;3,2,1,32;"
          "3,2,1,128;3,4,1,128",
-    "C": "0,0,1,0;2,1,1,0;2,2,1,0;2,4,1,0;1,1,1,0;1,2,1,0;1,4,1,0;2,1,0,0;2,1,1,128;"
-         "2,1,1,256;2,2,1,128;1,2,1,128",
+    "C": "0,0,1,0;2,2,1,0;2,4,1,0;2,8,1,0;1,4,1,0;1,8,1,0;2,4,0,0;2,4,1,64;2,4,1,256;"
+         "2,8,1,64;2,8,1,256;1,8,1,64",
 }
 
 
