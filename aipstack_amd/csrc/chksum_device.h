@@ -24,7 +24,7 @@ constexpr int kBlock = kWave * kWavesPerBlock;
 // Packet descriptors. A wave walks 64-packet chunks; per chunk the descriptor may fetch
 // per-lane data (lane j <-> packet j of the chunk), then gives
 //   bounds(j)      the wave-uniform absolute byte range [S, E) of packet j (SGPRs), and
-//   lane_start()   the start address of this lane's packet (VGPR, for the finalisation).
+//   lane_bounds()  [S, E) of this lane's packet (VGPRs; vectorised per-chunk metadata).
 // ---------------------------------------------------------------------------------
 
 // A copy of x in a fresh VGPR. The compiler waits for the load that produced x here,
@@ -52,9 +52,6 @@ struct StridedDesc {
                                            uint64_t &E) const {
         S = c.s0 + (uint64_t)j * stride;
         E = S + len;
-    }
-    __device__ __forceinline__ uint64_t lane_start(const Chunk &c, int lane) const {
-        return c.s0 + (uint64_t)lane * stride;
     }
     // This lane's packet (chunk packet `lane`) as [S, E) in VGPRs.
     __device__ __forceinline__ void lane_bounds(const Chunk &c, int lane, uint64_t &S,
@@ -94,9 +91,6 @@ struct CsrDesc {
                                            uint64_t &E) const {
         S = base + offset_of(c, j);
         E = base + ((j + 1 < kWave) ? offset_of(c, j + 1) : c.end_off);
-    }
-    __device__ __forceinline__ uint64_t lane_start(const Chunk &c, int) const {
-        return base + (((uint64_t)c.off_hi << 32) | c.off_lo);
     }
     // This lane's packet as [S, E): its offset and the next lane's (lane 63: end_off).
     __device__ __forceinline__ void lane_bounds(const Chunk &c, int lane, uint64_t &S,

@@ -6,27 +6,26 @@
 //   IpChksum = ~that (Chksum.h:122-125). IpChksumAccumulator(State s).getChksum(buf)
 //   (Chksum.h:171-174, 263-315) = the same sum seeded with the 32-bit state s.
 //
-// How (MI355X-first; see DESIGN.md "Kernel arithmetic"):
-//   * One packet per 64-lane wavefront at a time. A wave owns a contiguous run of
-//     64-packet chunks; lane j of the wave keeps packet j's result and the chunk ends
-//     in ONE coalesced 128-byte store of 64 uint16 results.
-//   * A packet [S, E) (absolute byte addresses) is read as the 16-byte-aligned
-//     segments A0 = S & ~15, A0+16, ... covering it: lane k loads segment k with a
-//     global_load_dwordx4 (a wave instruction reads 1 KiB contiguous). Every segment
-//     loaded contains at least one byte of the packet, so no load leaves the pages
-//     of the caller's buffer (a 16-byte block never straddles a page).
-//   * Segments are summed unmasked: each dword as its two little-endian 16-bit halves
-//     into a per-lane uint32 (exact up to 4 MiB packets); the 64 lane sums are added by
-//     a DPP reduction. The bytes of the head and tail segments that lie outside
-//     [S, E) are read back with v_readlane and subtracted on the scalar unit, so the
-//     sum is exact (not just congruent) and can be folded like the reference's.
-//   * Little-endian halves at even absolute addresses pair byte (2i, 2i+1) with 2i as
-//     the LOW byte; the reference pairs relative to the packet start with p[0] as the
-//     HIGH byte. So the folded sum is byte-swapped iff S is even (for odd S the two
-//     pairings coincide with the roles already swapped). Byte-swap is x*256 mod 0xFFFF,
-//     and folding never turns a nonzero sum into 0, so the 0x0000-vs-0xFFFF
+// How (MI355X-first; DESIGN.md sections 4-5):
+//   * A wave owns a contiguous run of 64-packet chunks. Per chunk, lane j computes packet
+//     j's load parameters (aligned base, segment count, head/tail mask indices) in VALU,
+//     and lane j ends up holding packet j's result: ONE coalesced 128-byte store.
+//   * Packets are processed one per wave, P at a time: packet [S, E) is read as the
+//     16-byte-aligned segments A0 = S & ~15, A0+16, ... through a buffer descriptor of
+//     16 * nseg bytes (lane k loads segment k; buffer_load_dwordx4 ... nt, 1 KiB per wave
+//     instruction; the range check zeroes slots past the packet). The head segment's bytes
+//     before S and the tail segment's bytes from E on are masked (constant tables, one
+//     v_bitop3 per dword on the lane that holds them).
+//   * Each lane accumulates its dwords in two add-with-carry chains (v_addc_co_u32, one op
+//     per dword): a ones'-complement sum, congruent mod 0xFFFF to the sum of the 16-bit
+//     halves and 0 only for all-zero input. Folded to 17 bits per chain, the 64 lanes are
+//     added exactly (< 2^24) by a DPP row scan.
+//   * Little-endian halves at even absolute addresses pair byte (2i, 2i+1) with 2i as the
+//     LOW byte; the reference pairs relative to the packet start with p[0] as the HIGH
+//     byte. So the folded sum is byte-swapped iff S is even. A byte swap is x*256 mod
+//     0xFFFF and folding never turns a nonzero sum into 0, so the 0x0000-vs-0xFFFF
 //     representation matches the reference exactly (0 iff every byte is 0).
-//   * HBM-bound integer reduction: no MFMA, no LDS needed (the cross-lane sum is DPP).
+//   * HBM-bound integer reduction: no MFMA, no LDS (the cross-lane sum is DPP).
 
 #include <hip/hip_runtime.h>
 

@@ -160,3 +160,20 @@ def test_cpp_header_accumulate_golden(golden):
 def test_chain_to_chunks_covers_tot_len(golden):
     for c in golden["chain"]["chains"]:
         assert sum(l for _, l in chain_to_chunks(c)) == c["tot_len"]
+
+
+def test_host_hook_variants_match_oracle(oracle):
+    """Portable / SSE2 / AVX2 bodies of the hook (host_hook.cc) against the oracle."""
+    lib = A._lib.load()
+    f = lib.aipstack_chksum_host_variant
+    f.restype = ctypes.c_uint16
+    f.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t]
+    rng = np.random.default_rng(17)
+    buf = rng.integers(0, 256, size=140000, dtype=np.uint8)
+    buf[70000:] = 0xFF
+    for t in range(4000):
+        o = int(rng.integers(0, 70000 if t % 2 else 64))
+        ln = min(int(rng.integers(0, 65536 if t % 50 == 0 else 3000)), 65535, buf.size - o)
+        want = oracle.inverted(buf, o, ln)
+        for v in (0, 1, 2):
+            assert f(v, buf.ctypes.data + o, ln) == want, (v, o, ln)
