@@ -68,6 +68,8 @@ def parse():
     p.add_argument("--cpu-reps", type=int, default=15,
                    help="timed single-thread passes of the CPU baseline sample")
     p.add_argument("--no-parity", action="store_true")
+    p.add_argument("--per-launch", action="store_true",
+                   help="after the timed region, time each launch with its own event pair")
     p.add_argument("--e2e", action="store_true",
                    help="end-to-end mode: batch in HOST memory, results to HOST memory "
                         "(host-memory streaming engine; PCIe-inclusive). Prints its own line.")
@@ -235,10 +237,13 @@ def main():
     if world > 1:
         # control plane only (barriers + max of times); no data-path collective
         dist.init_process_group("gloo", rank=rank, world_size=world)
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
-    if A.device_check(local_rank) != A.AIPSTACK_CHKSUM_OK:
-        raise SystemExit(f"rank {rank}: device {local_rank} is not a usable gfx950 device")
+    # AIPSTACK_BENCH_FORCE_DEVICE: rehearsal of the multi-rank flow on a 1-GPU box (every
+    # rank on that device). Never set by the driver; ranks then own their LOCAL_RANK GPU.
+    device = int(os.environ.get("AIPSTACK_BENCH_FORCE_DEVICE", local_rank))
+    torch.cuda.set_device(device)
+    dev = torch.device("cuda", device)
+    if A.device_check(device) != A.AIPSTACK_CHKSUM_OK:
+        raise SystemExit(f"rank {rank}: device {device} is not a usable gfx950 device")
 
     layout, n, plen = CONFIGS[args.config]
     stream = torch.cuda.current_stream()
@@ -297,6 +302,19 @@ def main():
         dist.barrier()
     avg_kernel_s = ev0.elapsed_time(ev1) / 1e3 / args.steps
 
+    # Diagnostic, AFTER the timed region (not part of `value`): per-launch event pairs,
+    # to expose outliers / clock ramps that the bracketed average smooths over.
+    per_launch = []
+    if args.per_launch:
+        pairs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                 for _ in range(args.steps)]
+        for a, b in pairs:
+            a.record(stream)
+            step()
+            b.record(stream)
+        torch.cuda.synchronize()
+        per_launch = sorted(a.elapsed_time(b) * 1e3 for a, b in pairs)
+
     t = torch.tensor([elapsed], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -354,6 +372,9 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": _pmc_traffic(args.config),
             "kernel_us": round(avg_kernel_s * 1e6, 2),
+            **({"per_launch_us": {"min": round(per_launch[0], 2),
+                                  "median": round(per_launch[len(per_launch) // 2], 2),
+                                  "max": round(per_launch[-1], 2)}} if per_launch else {}),
             "algorithmic_bytes_per_launch": alg,
         },
         "cpu_baseline": cpu,
@@ -376,7 +397,8 @@ def e2e(args, rank, world, local_rank, layout, n, plen):
     off, total = spec["offsets"], spec["total"]
     host = host_shard(spec)
     out = np.empty(n, dtype=np.uint16)
-    eng = A.ChksumEngine(local_rank, chunk_bytes=args.e2e_chunk_mib << 20,
+    eng = A.ChksumEngine(int(os.environ.get("AIPSTACK_BENCH_FORCE_DEVICE", local_rank)),
+                         chunk_bytes=args.e2e_chunk_mib << 20,
                          nstreams=args.e2e_streams)
     if not args.e2e_pageable:
         eng.register(host)
@@ -398,6 +420,19 @@ def e2e(args, rank, world, local_rank, layout, n, plen):
     if world > 1:
         dist.barrier()
     import torch
+    # Diagnostic, AFTER the timed region (not part of `value`): per-launch event pairs,
+    # to expose outliers / clock ramps that the bracketed average smooths over.
+    per_launch = []
+    if args.per_launch:
+        pairs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                 for _ in range(args.steps)]
+        for a, b in pairs:
+            a.record(stream)
+            step()
+            b.record(stream)
+        torch.cuda.synchronize()
+        per_launch = sorted(a.elapsed_time(b) * 1e3 for a, b in pairs)
+
     t = torch.tensor([elapsed], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
