@@ -127,3 +127,58 @@ def test_udp_zero_checksum_and_short_frames(frames, oracle):
     assert _one(fr, oracle) == RX["DROP_L4_MALFORMED"]
     assert _one(b"\x00" * 13, oracle) == RX["NOT_IP4"]
     assert _one(bytes(12) + b"\x08\x00" + bytes(10), oracle) == RX["DROP_IP_MALFORMED"]
+
+
+# ---- edge-case frames (tests/golden/frame_cases.py) ------------------------------------
+
+def _edge_frames():
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import frame_cases
+    return frame_cases
+
+
+def test_edge_frames_cover_every_verdict(oracle):
+    fc = _edge_frames()
+    buf, off = fc.pack(fc.frames())
+    v = oracle.rx_verify_batch(buf, off)
+    counts = np.bincount(v, minlength=9)
+    assert np.all(counts > 0), counts.tolist()
+
+
+def test_edge_frames_zero_sum_checksums_verify(oracle):
+    """L4 data whose sum is 0 mod 0xFFFF: the computed checksum is 0x0000; a field of
+    0xFFFF (the other zero) verifies too (Chksum.h:245-250 folds both to 0xFFFF)."""
+    fc = _edge_frames()
+    frs = fc.frames(seed=99, n=4000)
+    hits = {0: 0, 0xFFFF: 0}
+    for fr in frs:
+        b = np.frombuffer(fr, dtype=np.uint8)
+        if oracle.rx_verify_batch(b.copy(), np.array([0, len(fr)], dtype=np.uint64))[0] != RX["ACCEPT"]:
+            continue
+        if fr[23] not in (1, 6):
+            continue
+        l4 = 14 + (fr[14] & 15) * 4
+        co = l4 + (16 if fr[23] == 6 else 2)
+        c = be16(fr, co)
+        if c not in hits:
+            continue
+        hits[c] += 1
+        alt = bytearray(fr)
+        alt[co:co + 2] = (c ^ 0xFFFF).to_bytes(2, "big")
+        a = np.frombuffer(bytes(alt), dtype=np.uint8).copy()
+        assert oracle.rx_verify_batch(a, np.array([0, len(fr)], dtype=np.uint64))[0] == RX["ACCEPT"]
+    assert hits[0] > 5 and hits[0xFFFF] > 5, hits
+
+
+def test_edge_frames_fill_then_verify(oracle):
+    fc = _edge_frames()
+    buf, off = fc.pack(fc.frames())
+    st = oracle.tx_fill_batch(buf, off)
+    v = oracle.rx_verify_batch(buf, off)
+    filled = st == RX["ACCEPT"]
+    assert filled.sum() > 1000
+    assert np.all(v[filled] == RX["ACCEPT"])
+    # statuses other than ACCEPT are exactly the verdicts that stop before an L4 sum
+    assert np.all(st[~filled] == v[~filled])

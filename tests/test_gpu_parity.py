@@ -8,6 +8,7 @@ batches and packets, ragged counts, odd base pointers, len 65535, FINAL flag, se
 """
 import os
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -416,3 +417,36 @@ def test_fill_then_verify_on_gpu():
     v = _np(A.rx_verify(dbuf, doff))
     assert np.array_equal(st, v)
     assert set(np.unique(v).tolist()) <= {0, 3, 6, 8}
+
+
+def _edge_frames(seed, n):
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import frame_cases
+    return frame_cases.pack(frame_cases.frames(seed, n))
+
+
+@pytest.mark.parametrize("shift", [0, 1, 7, 13])
+def test_rx_verify_edge_frames(oracle, shift):
+    """tests/golden/frame_cases.py: every verdict, IPv4 options, padding, zero-sum L4 data,
+    one mutation in 40 % of frames; the whole batch starts `shift` bytes into a buffer."""
+    buf, off = _edge_frames(20251015 + shift, 3000)
+    big = np.zeros(buf.size + shift, dtype=np.uint8)
+    big[shift:] = buf
+    got = _np(A.rx_verify(_d(big), _d(off + np.uint64(shift))))
+    want = oracle.rx_verify_batch(buf, off)
+    assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
+    assert np.all(np.bincount(want, minlength=9) > 0)
+
+
+@pytest.mark.parametrize("shift", [0, 3])
+def test_tx_fill_edge_frames(oracle, shift):
+    buf, off = _edge_frames(7 + shift, 3000)
+    big = np.zeros(buf.size + shift, dtype=np.uint8)
+    big[shift:] = buf
+    dbig = _d(big)
+    st = _np(A.tx_fill(dbig, _d(off + np.uint64(shift))))
+    want = buf.copy()
+    want_st = oracle.tx_fill_batch(want, off)
+    assert np.array_equal(st, want_st)
+    got = _np(dbig)[shift:]
+    assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
