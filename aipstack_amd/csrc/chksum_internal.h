@@ -13,8 +13,12 @@ int check_hip(hipError_t e);
 int device_cu_count();
 
 // Frames a wave of the Rx-verify / Tx-fill kernels keeps in flight (tunable "frames":
-// 1, 2 or 4; default 2).
+// 2, 4 or 8; default 4).
 int tuning_frames_in_flight();
+
+// Resident-wave budget per CU the grids are sized to (tunable "waves_per_cu"; 0 = each
+// kernel's default).
+int tuning_waves_per_cu();
 
 }  // namespace aipstack_amd
 

@@ -303,9 +303,13 @@ int launch_chain(const uint64_t *d_addr, const uint32_t *d_len, const uint64_t *
 
 }  // namespace
 
+int tuning_waves_per_cu() {
+    return tuning().waves_per_cu.load(std::memory_order_relaxed);
+}
+
 int tuning_frames_in_flight() {
     const int f = tuning().frames.load(std::memory_order_relaxed);
-    return (f == 1 || f == 2 || f == 4) ? f : 2;
+    return (f == 2 || f == 4 || f == 8) ? f : 4;
 }
 
 }  // namespace aipstack_amd

@@ -6,13 +6,11 @@
 //              (ip/IpStack.h:425-453, tcp/IpTcpProto_output.h:1251-1277,
 //              udp/IpUdpProto.h:164-179, ip/IpStack.h:1164-1190).
 //
-// One wave per frame, 64-frame chunks per wave (CSR frame offsets, as the checksum CSR
-// batch). A frame is read ONCE from HBM: the aligned segments covering it are loaded
-// through a range-checked buffer descriptor (as PacketLoad does); lanes 0-7 copy the first
-// 128 bytes into the wave's LDS slot, where the Ethernet / IPv4 / L4 header fields are
-// parsed and the IPv4 header words are summed (one lane per word); the L4 checksum is a
-// masked sum over the same loaded segments (segment range, head/tail byte masks and, for
-// Tx, the checksum field itself masked out), reduced across the wave with DPP.
+// 64-frame chunks per wave (CSR frame offsets, as the checksum CSR batch). The header
+// decisions run one frame per LANE (VALU), from the frame's first 112 aligned bytes; the
+// L4 checksums run one frame per WAVE over just the bytes they cover, with the CSR
+// batch's loads, masks and DPP reduction. Each frame's bytes come from HBM once (the
+// header bytes are re-read from L2 by the L4 pass).
 
 #include <hip/hip_runtime.h>
 
@@ -25,7 +23,10 @@
 namespace aipstack_amd {
 namespace {
 
-constexpr int kStageBytes = 128;  // bytes [A0, A0 + 128) cover frame bytes [0, 112)
+// Frame bytes [0, 97) cover every header field the kernels read from any start alignment:
+// 14 (Ethernet) + 60 (IPv4 with options) + 8 (UDP header) + 15 (S & 15).
+constexpr int kHdrSegs = 7;
+constexpr int kHdrDwords = 21;  // frame bytes [0, 84) realigned to the frame start
 
 // Zero bytes b and b+1 (b+1 < 16) of a 16-byte segment, as four dwords.
 constexpr uint32_t not_pair_dword(int b, int d) {
@@ -47,85 +48,14 @@ __device__ __forceinline__ uint32_t bswap32(uint32_t x) {
     return __builtin_bswap32(x);
 }
 
-// Wave-uniform read of 4 frame bytes [x, x+4) (x relative to A0) from the LDS stage, as a
-// little-endian dword.
-__device__ __forceinline__ uint32_t stage4(const uint32_t *st, int x) {
-    const uint32_t lo = st[x >> 2], hi = st[(x >> 2) + 1];
-    const uint32_t r = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(x & 3));
-    return __builtin_amdgcn_readfirstlane(r);
-}
-// This lane's share of the masked sum of the frame bytes [r0, r1) relative to A0, except
-// the two bytes at fx (fx < 0: none), over the segments the wave has loaded (group 0 in
-// fl.v, further groups loaded here): the lane's 18-bit folded ones'-complement sum. Summed
-// over the wave (< 2^24) it is congruent mod 0xFFFF to the little-endian 16-bit halves of
-// those bytes and 0 iff they are all 0.
-template <int U, bool NT>
-__device__ __forceinline__ uint32_t range_lane(PacketLoad<U, NT> &fl, int r0, int r1, int fx,
-                                               int lane, uint32_t voff) {
-    if (r1 <= r0)
-        return 0;
-    const int k0 = r0 >> 4, k1 = (r1 - 1) >> 4;
-    const u32x4 hm = load_mask(kMaskFrom[r0 & 15]);
-    const u32x4 tm = load_mask(kMaskTo[r1 - 16 * k1]);
-    const int kx = fx >= 0 ? fx >> 4 : -2;
-    const int bx = fx >= 0 ? fx & 15 : 0;
-    const u32x4 xm = load_mask(kMaskNotPair[bx]);   // bytes bx, bx+1 of segment kx
-    const u32x4 xm2 = load_mask(kMaskFrom[1]);      // byte 0 of segment kx+1 (bx == 15)
-    const int kx2 = (fx >= 0 && bx == 15) ? kx + 1 : -2;
-    Eac a0, a1;
-    for (int g = 0; g <= k1; g += kWave * U) {
-        if (g > 0) {
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                fl.v[u] = load_segment<NT>(fl.rsrc, voff, (uint32_t)((g + u * kWave) * 16));
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int k = g + u * kWave + lane;
-            const uint32_t in = (k >= k0 && k <= k1) ? ~0u : 0u;
-            u32x4 x = fl.v[u];
-            apply_mask(x, hm, k == k0 ? 0u : ~0u);
-            apply_mask(x, tm, k == k1 ? 0u : ~0u);
-            if (fx >= 0) {  // wave-uniform: Tx only
-                apply_mask(x, xm, k == kx ? 0u : ~0u);
-                apply_mask(x, xm2, k == kx2 ? 0u : ~0u);
-            }
-            a0.add(x[0] & in);
-            a1.add(x[1] & in);
-            a0.add(x[2] & in);
-            a1.add(x[3] & in);
-        }
-    }
-    const uint32_t s0 = a0.finish(), s1 = a1.finish();
-    return (s0 & 0xFFFFu) + (s0 >> 16) + (s1 & 0xFFFFu) + (s1 >> 16);
+// (a & ~m) | (b & m): one v_bfi_b32. Used instead of `c ? x[i + k] : x[i]`, which LLVM
+// canonicalises into a dynamically indexed load (a private array in scratch).
+__device__ __forceinline__ uint32_t blend(uint32_t m, uint32_t a, uint32_t b) {
+    return (a & ~m) | (b & m);
 }
 
-// Two wave sums at once: the two DPP chains interleave, so neither waits on its own
-// data-hazard slots. Results wave-uniform.
-__device__ __forceinline__ void wave_sum2(uint32_t &a, uint32_t &b) {
-#define AIPSTACK_DPP2(ctrl, rowmask)                                                     \
-    a += __builtin_amdgcn_update_dpp(0u, a, ctrl, rowmask, 0xF, false);                  \
-    b += __builtin_amdgcn_update_dpp(0u, b, ctrl, rowmask, 0xF, false);
-    AIPSTACK_DPP2(0x111, 0xF)
-    AIPSTACK_DPP2(0x112, 0xF)
-    AIPSTACK_DPP2(0x114, 0xF)
-    AIPSTACK_DPP2(0x118, 0xF)
-    AIPSTACK_DPP2(0x142, 0xA)
-    AIPSTACK_DPP2(0x143, 0xC)
-#undef AIPSTACK_DPP2
-    a = __builtin_amdgcn_readlane(a, 63);
-    b = __builtin_amdgcn_readlane(b, 63);
-}
-
-// IpChksumAccumulator(words).getChksum() over a little-endian range sum `t` of bytes that
-// start at absolute address `start`: orient (big-endian pairing from `start`), add the
-// header/pseudo-header words with end-around carry, fold, invert (Chksum.h:245-300).
-__device__ __forceinline__ uint32_t finish_chksum(uint32_t words, uint32_t t, uint64_t start) {
-    uint32_t r = fold16(t);
-    if ((start & 1) == 0)
-        r = bswap16(r);
-    const uint64_t m = (uint64_t)words + r;
-    return (~fold16((uint32_t)m + (uint32_t)(m >> 32))) & 0xFFFFu;
+__device__ __forceinline__ uint32_t be16_at(uint32_t le_dword, int byte) {  // byte 0 or 2
+    return ((le_dword >> (8 * byte)) & 0xFFu) << 8 | ((le_dword >> (8 * byte + 8)) & 0xFFu);
 }
 
 __device__ __forceinline__ void store_be16(uint64_t addr, uint32_t v) {
@@ -134,117 +64,144 @@ __device__ __forceinline__ void store_be16(uint64_t addr, uint32_t v) {
     p[1] = (uint8_t)v;
 }
 
-// One frame, its segment loads already issued into fl: stage the header, parse, sum,
-// decide (and for Tx, write the checksums). Returns the AIPSTACK_RX_* verdict / status.
-template <bool TX, int U, bool NT>
-__device__ __forceinline__ int process_frame(PacketLoad<U, NT> &fl, uint64_t S, int len,
-                                             uint32_t *st, int lane, uint32_t voff) {
-    const int rs = fl.rel_s;
-    // stage frame bytes [0, 112) (segments 0..7) in this wave's LDS slot
-    if (lane < kStageBytes / 16) {
-        st[4 * lane + 0] = fl.v[0][0];
-        st[4 * lane + 1] = fl.v[0][1];
-        st[4 * lane + 2] = fl.v[0][2];
-        st[4 * lane + 3] = fl.v[0][3];
-    }
-    __builtin_amdgcn_wave_barrier();
-    // all fixed-offset header dwords in one batch of LDS reads
-    const uint32_t w12 = stage4(st, rs + 12);  // EtherType | version/IHL | TOS
-    const uint32_t w16 = stage4(st, rs + 16);  // total length | ident
-    const uint32_t w20 = stage4(st, rs + 20);  // flags/offset | TTL | protocol
-    const uint32_t w28 = stage4(st, rs + 28);
-    const uint32_t w24 = stage4(st, rs + 24);
-    const uint32_t w32 = stage4(st, rs + 32);
-    const uint32_t ethertype = ((w12 & 0xFFu) << 8) | ((w12 >> 8) & 0xFFu);
-    // ---- Ethernet (EthIpIface.h:370-384)
-    if (len < 14 || ethertype != 0x0800)
-        return AIPSTACK_RX_NOT_IP4;
-    // ---- IPv4 header checks (IpStack.h:938-990)
+// What the header pass decides for one frame (lane j <-> frame j of the chunk).
+struct FrameLane {
+    uint64_t l4s, l4e;  // the bytes the L4 checksum covers; l4s == l4e: no L4 sum
+    uint32_t words;     // IpChksumAccumulator words added before them (pseudo-header)
+    uint32_t hchk;      // IPv4 header checksum over the header (Tx: with the field as 0)
+    uint32_t fx;        // Tx: L4 checksum field, bytes from (l4s & ~15)
+    int fld;            // Tx: L4 checksum field, bytes from the frame start
+    int pre;            // the verdict / status when no L4 sum decides it
+    bool ip_ok;         // the IPv4 header parsed (Tx writes its checksum)
+    bool udp;           // Tx: a computed 0 is sent as 0xFFFF
+};
+
+// Header pass, one frame per lane, all in VALU: realign the frame's first bytes from the
+// aligned segments, then the checks of EthIpIface::recvFrame (eth/EthIpIface.h:367-390),
+// IpStack::processRecvedIp4Packet (ip/IpStack.h:936-1044) and the L4 entry checks
+// (tcp/IpTcpProto_input.h:68-100, udp/IpUdpProto.h:470-490, 631-652, ip/IpStack.h:1093-1130);
+// the send side fills the same fields (ip/IpStack.h:425-453, tcp/IpTcpProto_output.h:1251-1277,
+// udp/IpUdpProto.h:164-179, ip/IpStack.h:1164-1190).
+template <bool TX>
+__device__ __forceinline__ FrameLane parse_lane(const u32x4 (&seg)[kHdrSegs], uint64_t S,
+                                                int len) {
+    uint32_t raw[4 * kHdrSegs];
+#pragma unroll
+    for (int i = 0; i < kHdrSegs; ++i)
+#pragma unroll
+        for (int d = 0; d < 4; ++d) raw[4 * i + d] = seg[i][d];
+    // f[i] = frame bytes [4i, 4i + 4) as a little-endian dword: shift by S & 15 bytes
+    const uint32_t rs = (uint32_t)S & 15u;
+    const uint32_t q2 = (rs & 8u) ? ~0u : 0u, q1 = (rs & 4u) ? ~0u : 0u;
+    uint32_t t1[kHdrDwords + 2], t2[kHdrDwords + 1], f[kHdrDwords];
+#pragma unroll
+    for (int i = 0; i < kHdrDwords + 2; ++i) t1[i] = blend(q2, raw[i], raw[i + 2]);
+#pragma unroll
+    for (int i = 0; i < kHdrDwords + 1; ++i) t2[i] = blend(q1, t1[i], t1[i + 1]);
+#pragma unroll
+    for (int i = 0; i < kHdrDwords; ++i) f[i] = __builtin_amdgcn_alignbyte(t2[i + 1], t2[i], rs & 3u);
+
+    FrameLane r;
+    r.l4s = r.l4e = S;
+    r.words = 0;
+    r.fx = 0;
+    r.fld = 0;
+    r.udp = false;
+    r.ip_ok = false;
+    // ---- Ethernet + IPv4 header checks (eth/EthIpIface.h:370-384, ip/IpStack.h:938-990)
+    const uint32_t ethertype = be16_at(f[3], 0);
+    const uint32_t vihl = (f[3] >> 16) & 0xFFu;
+    const int hl = vihl == 0x45u ? 20 : (int)(vihl & 0xFu) * 4;
+    const int total_len = (int)be16_at(f[4], 0);
     const int plen = len - 14;
-    if (plen < 20)
-        return AIPSTACK_RX_DROP_IP_MALFORMED;
-    const uint32_t vihl = (w12 >> 16) & 0xFFu;
-    int hl = 20;
-    if (vihl != 0x45) {
-        hl = (int)(vihl & 0xFu) * 4;
-        if ((vihl >> 4) != 4 || hl < 20 || hl > plen)
-            return AIPSTACK_RX_DROP_IP_MALFORMED;
+    if (len < 14 || ethertype != 0x0800u) {
+        r.pre = AIPSTACK_RX_NOT_IP4;
+    } else if (plen < 20 || (vihl >> 4) != 4u || hl < 20 || hl > plen || total_len < hl ||
+               total_len > plen) {
+        r.pre = AIPSTACK_RX_DROP_IP_MALFORMED;
+    } else {
+        r.ip_ok = true;
+        r.pre = -1;
     }
-    const int total_len = (int)(((w16 & 0xFFu) << 8) | ((w16 >> 8) & 0xFFu));
-    if (total_len < hl || total_len > plen)
-        return AIPSTACK_RX_DROP_IP_MALFORMED;
-    const uint32_t flags_off = ((w20 & 0xFFu) << 8) | ((w20 >> 8) & 0xFFu);
-    const bool fragment = (flags_off & 0x3FFFu) != 0;                  // IpStack.h:1020
-    const uint32_t proto = w20 >> 24;
-    const uint32_t src = bswap32((w24 >> 16) | (w28 << 16));
-    const uint32_t dst = bswap32((w28 >> 16) | (w32 << 16));
-    // ---- L4: which bytes the checksum covers, or a verdict without one
+    // ---- IPv4 header sum: dwords of frame bytes [14 + 4m, 18 + 4m), m < hl / 4. Their
+    // little-endian halves pair (14 + 2i, 15 + 2i) with the even byte low: byte-swapped
+    // big-endian words, so the folded sum is swapped back once (x * 256 * 256 = x).
+    Eac hs;
+#pragma unroll
+    for (int m = 0; m < 15; ++m) {
+        uint32_t w = __builtin_amdgcn_alignbyte(f[4 + m], f[3 + m], 2);
+        if (TX && m == 2) w &= 0xFFFFu;  // header checksum field as 0 (bytes 24-25)
+        hs.add(w & (4 * m < hl ? ~0u : 0u));
+    }
+    r.hchk = (~bswap16(fold16(hs.finish()))) & 0xFFFFu;
+    if (!r.ip_ok)
+        return r;
+    if (!TX && r.hchk != 0) {                                       // ip/IpStack.h:1016
+        r.pre = AIPSTACK_RX_DROP_IP_CHKSUM;
+        return r;
+    }
+    const uint32_t flags_off = be16_at(f[5], 0);
+    const uint32_t proto = f[5] >> 24;
+    if ((flags_off & 0x3FFFu) != 0) {                               // ip/IpStack.h:1020
+        r.pre = AIPSTACK_RX_FRAGMENT;
+        return r;
+    }
+    const uint32_t src = bswap32(__builtin_amdgcn_alignbyte(f[7], f[6], 2));
+    const uint32_t dst = bswap32(__builtin_amdgcn_alignbyte(f[8], f[7], 2));
+    const uint32_t pseudo = (src >> 16) + (src & 0xFFFFu) + (dst >> 16) + (dst & 0xFFFFu);
     const int dg = 14 + hl;
     const int dlen = total_len - hl;
-    const uint32_t pseudo_sa = (src >> 16) + (src & 0xFFFFu) + (dst >> 16) + (dst & 0xFFFFu);
-    int l4len = -1, fld = 0, l4verdict = AIPSTACK_RX_ACCEPT_OTHER;
-    uint32_t words = 0;
-    bool udp = false;
-    if (!fragment) {
-        if (proto == 6) {                                              // TCP
-            if (dlen < 20) l4verdict = AIPSTACK_RX_DROP_L4_MALFORMED;
-            else { l4len = dlen; fld = dg + 16; words = pseudo_sa + 6 + (uint32_t)dlen; }
-        } else if (proto == 17) {                                      // UDP
-            if (dlen < 8) {
-                l4verdict = AIPSTACK_RX_DROP_L4_MALFORMED;
-            } else {
-                const uint32_t w = stage4(st, rs + dg + 4);
-                const int ulen = (int)(((w & 0xFFu) << 8) | ((w >> 8) & 0xFFu));
-                const uint32_t ucs = ((w >> 8) & 0xFF00u) | (w >> 24);
-                if (ulen < 8 || ulen > dlen) {
-                    l4verdict = AIPSTACK_RX_DROP_L4_MALFORMED;
-                } else if (!TX && ucs == 0) {
-                    l4verdict = AIPSTACK_RX_ACCEPT_NO_CHKSUM;          // IpUdpProto.h:637
-                } else {
-                    l4len = ulen; fld = dg + 6; words = pseudo_sa + 17 + (uint32_t)ulen;
-                    udp = true;
-                }
-            }
-        } else if (proto == 1) {                                       // ICMP
-            if (dlen < 8) l4verdict = AIPSTACK_RX_DROP_L4_MALFORMED;
-            else { l4len = dlen; fld = dg + 2; }
+    // UDP length + checksum: frame bytes [dg + 4, dg + 8), i.e. dwords 4 + hl/4 and 5 + hl/4
+    const int h = hl >> 2;
+    uint32_t ulo = f[9], uhi = f[10];
+#pragma unroll
+    for (int hh = 6; hh <= 15; ++hh) {
+        const uint32_t sel = h == hh ? ~0u : 0u;
+        ulo = blend(sel, ulo, f[4 + hh]);
+        uhi = blend(sel, uhi, f[5 + hh]);
+    }
+    const uint32_t uw = __builtin_amdgcn_alignbyte(uhi, ulo, 2);
+    int l4len = -1, fo = 0;
+    r.pre = AIPSTACK_RX_ACCEPT_OTHER;
+    if (proto == 6) {                                               // TCP
+        if (dlen < 20) r.pre = AIPSTACK_RX_DROP_L4_MALFORMED;
+        else { l4len = dlen; fo = 16; r.words = pseudo + 6u + (uint32_t)dlen; }
+    } else if (proto == 17) {                                       // UDP
+        const int ulen = (int)be16_at(uw, 0);
+        if (dlen < 8 || ulen < 8 || ulen > dlen) {
+            r.pre = AIPSTACK_RX_DROP_L4_MALFORMED;
+        } else if (!TX && be16_at(uw, 2) == 0) {
+            r.pre = AIPSTACK_RX_ACCEPT_NO_CHKSUM;                   // udp/IpUdpProto.h:637
+        } else {
+            l4len = ulen; fo = 6; r.words = pseudo + 17u + (uint32_t)ulen; r.udp = true;
         }
+    } else if (proto == 1) {                                        // ICMP
+        if (dlen < 8) r.pre = AIPSTACK_RX_DROP_L4_MALFORMED;
+        else { l4len = dlen; fo = 2; }
     }
-    // ---- both sums, one interleaved reduction: header word `lane` (LDS), L4 bytes (regs)
-    uint32_t hw = 0;
-    if (2 * lane < hl && !(TX && lane == 5)) {
-        const uint8_t *sb = reinterpret_cast<const uint8_t *>(st);
-        const int o = rs + 14 + 2 * lane;
-        hw = ((uint32_t)sb[o] << 8) | sb[o + 1];
+    if (l4len >= 0) {
+        r.pre = AIPSTACK_RX_ACCEPT;
+        r.l4s = S + (uint64_t)dg;
+        r.l4e = r.l4s + (uint64_t)l4len;
+        r.fld = dg + fo;
+        r.fx = ((uint32_t)r.l4s & 15u) + (uint32_t)fo;  // < 32: lanes 0-2 of slot 0
     }
-    const int r0 = rs + dg;
-    uint32_t lw = l4len >= 0 ? range_lane<U, NT>(fl, r0, r0 + l4len, TX ? rs + fld : -1, lane, voff)
-                             : 0u;
-    wave_sum2(hw, lw);
-    const uint32_t hchk = (~fold16(hw)) & 0xFFFFu;                     // IpStack.h:1016
-    if (TX) {
-        if (lane == 0) store_be16(S + 24, hchk);
-    } else if (hchk != 0) {
-        return AIPSTACK_RX_DROP_IP_CHKSUM;
-    }
-    if (fragment)
-        return AIPSTACK_RX_FRAGMENT;
-    if (l4len < 0)
-        return l4verdict;
-    uint32_t chk = finish_chksum(words, lw, S + (uint64_t)dg);
-    if (TX) {
-        if (udp && chk == 0) chk = 0xFFFFu;                            // IpUdpProto.h:176-178
-        if (lane == 0) store_be16(S + (uint64_t)fld, chk);
-        return AIPSTACK_RX_ACCEPT;
-    }
-    return chk == 0 ? AIPSTACK_RX_ACCEPT : AIPSTACK_RX_DROP_L4_CHKSUM;
+    return r;
 }
 
+// Rx verify / Tx fill of n frames at CSR offsets. A wave walks 64-frame chunks:
+//   (B) lane j loads frame j's first 112 aligned bytes (one buffer descriptor per chunk)
+//       and parses its headers (parse_lane): the L4 byte range, pseudo-header words and
+//       the verdict when no L4 sum is needed;
+//   (C) the frames that need an L4 sum are summed one per wave, P in flight, exactly as
+//       the CSR checksum batch sums packets (PacketLoad over the L4 range); for Tx the
+//       checksum field is masked out of the sum;
+//   (D) lane j finishes frame j: verdict (one coalesced 64-byte store), and for Tx the
+//       IPv4 header and L4 checksums written in place.
 template <bool TX, int U, int P, bool NT>
 __global__ __launch_bounds__(kBlock) void frame_kernel(CsrDesc desc, uint64_t n,
                                                        uint32_t chunks_per_wave,
                                                        uint8_t *__restrict__ status) {
-    __shared__ uint32_t stage_all[kWavesPerBlock][P][kStageBytes / 4 + 1];
     const int lane = threadIdx.x & (kWave - 1);
     const uint32_t wave_in_block = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerBlock + wave_in_block;
@@ -252,37 +209,87 @@ __global__ __launch_bounds__(kBlock) void frame_kernel(CsrDesc desc, uint64_t n,
     uint64_t c = wave * chunks_per_wave;
     const uint64_t c_end = min(c + chunks_per_wave, nchunks);
     const uint32_t voff = (uint32_t)lane * 16u;
+    const uint32_t not_lane0 = lane == 0 ? 0u : ~0u;
 
     for (; c < c_end; ++c) {
         const uint64_t p0 = c * kWave;
         const auto chunk = desc.begin_chunk(p0, n, lane);
         const int cnt = (int)min((uint64_t)kWave, n - p0);
-        uint32_t verdicts = 0;
-        for (int j0 = 0; j0 < cnt; j0 += P) {
-            PacketLoad<U, NT> fl[P];
-            uint64_t S[P];
-            int len[P];
+        uint64_t S, E;
+        desc.lane_bounds(chunk, lane, S, E);
+        const uint64_t l64 = E - S;
+        const int len = (lane >= cnt || l64 >= (1ull << 31)) ? 0 : (int)l64;  // 0: NOT_IP4
+        // (B) headers: aligned segments [A0_j, A0_j + 112) through one range-checked
+        // descriptor over the chunk's aligned span (never past the 16-byte blocks holding
+        // the chunk's bytes; slots past it read 0).
+        const uint64_t base = (__builtin_amdgcn_readfirstlane((uint32_t)S) & ~15u) |
+                              ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(S >> 32)) << 32);
+        const uint64_t span = ((desc.base + chunk.end_off + 15u) & ~(uint64_t)15) - base;
+        const uint32_t hrec = __builtin_amdgcn_readfirstlane(
+            span > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)span);  // uniform: SGPR descriptor
+        const __amdgpu_buffer_rsrc_t hrsrc = __builtin_amdgcn_make_buffer_rsrc(
+            reinterpret_cast<void *>(base), (short)0, hrec, 0x00020000);
+        const uint32_t hoff = (uint32_t)((S & ~(uint64_t)15) - base);
+        u32x4 seg[kHdrSegs];
 #pragma unroll
-            for (int q = 0; q < P; ++q) {  // P frames' loads in flight
-                uint64_t s = 0, e = 0;
-                if (j0 + q < cnt)
-                    desc.bounds(chunk, j0 + q, s, e);
-                const uint64_t l64 = e - s;
-                len[q] = l64 >= (1ull << 31) ? 0 : (int)l64;  // out of contract: empty
-                S[q] = s;
-                fl[q].issue(s, s + (uint64_t)len[q], voff);
+        for (int i = 0; i < kHdrSegs; ++i) seg[i] = load_segment<false>(hrsrc, hoff, 16u * i);
+        const FrameLane fl = parse_lane<TX>(seg, S, len);
+        const bool need = fl.l4e != fl.l4s;
+        const LaneMeta meta = lane_meta(fl.l4s, fl.l4e);
+
+        // (C) L4 sums, one frame per wave, P frames' loads in flight
+        uint64_t todo = __builtin_amdgcn_ballot_w64(need);
+        uint32_t sums = 0;
+        while (todo) {
+            PacketLoad<U, NT> pk[P];
+            int jq[P];
+            uint32_t fxq[P];
+#pragma unroll
+            for (int q = 0; q < P; ++q) {
+                const bool valid = todo != 0;
+                const int j = valid ? (int)__builtin_ctzll(todo) : 0;
+                todo &= todo - 1;
+                jq[q] = valid ? j : -1;
+                const uint64_t a0 = ((uint64_t)__builtin_amdgcn_readlane(meta.a0_hi, j) << 32) |
+                                    (uint32_t)__builtin_amdgcn_readlane(meta.a0_lo, j);
+                const uint32_t packed =
+                    valid ? (uint32_t)__builtin_amdgcn_readlane(meta.packed, j) : 16u << 4;
+                fxq[q] = TX ? (uint32_t)__builtin_amdgcn_readlane(fl.fx, j) : 0u;
+                pk[q].issue_meta(a0, packed, voff);
             }
 #pragma unroll
             for (int q = 0; q < P; ++q) {
-                const int v = process_frame<TX, U, NT>(fl[q], S[q], len[q],
-                                                       stage_all[wave_in_block][q], lane, voff);
-                verdicts = (lane == j0 + q) ? (uint32_t)v : verdicts;
+                if (TX) {  // the checksum field itself is summed as 0
+                    const int fx = (int)fxq[q];
+                    apply_mask(pk[q].v[0], load_mask(kMaskNotPair[fx & 15]),
+                               lane == (fx >> 4) ? 0u : ~0u);
+                    apply_mask(pk[q].v[0], load_mask(kMaskFrom[1]),
+                               ((fx & 15) == 15 && lane == (fx >> 4) + 1) ? 0u : ~0u);
+                }
+                const uint32_t t = pk[q].finish(lane, voff, not_lane0);  // wave-uniform
+                sums = (lane == jq[q]) ? t : sums;
             }
-            // the stage slots are rewritten by the next frames: reads before writes
-            __builtin_amdgcn_wave_barrier();
+        }
+
+        // (D) per-lane finish
+        uint32_t r = fold16(sums);
+        if ((meta.packed & 1u) == 0)  // L4 start even: little-endian pairing -> big-endian
+            r = bswap16(r);
+        const uint64_t m = (uint64_t)fl.words + r;
+        uint32_t chk = (~fold16((uint32_t)m + (uint32_t)(m >> 32))) & 0xFFFFu;
+        int v = fl.pre;
+        if (TX) {
+            if (fl.ip_ok)
+                store_be16(S + 24, fl.hchk);
+            if (need) {
+                if (fl.udp && chk == 0) chk = 0xFFFFu;              // udp/IpUdpProto.h:176-178
+                store_be16(S + (uint64_t)fl.fld, chk);
+            }
+        } else if (need) {
+            v = chk == 0 ? AIPSTACK_RX_ACCEPT : AIPSTACK_RX_DROP_L4_CHKSUM;
         }
         if (lane < cnt)
-            status[p0 + lane] = (uint8_t)verdicts;
+            status[p0 + lane] = (uint8_t)v;
     }
 }
 
@@ -292,7 +299,8 @@ int launch_frames(const void *d_base, const uint64_t *d_offsets, uint64_t n, uin
     const uint64_t nchunks = (n + kWave - 1) / kWave;
     const int cus = device_cu_count();
     if (cus <= 0) return AIPSTACK_CHKSUM_EHIP;
-    const uint64_t target_waves = (uint64_t)cus * 128;
+    const int wpc = tuning_waves_per_cu();
+    const uint64_t target_waves = (uint64_t)cus * (wpc > 0 ? wpc : 128);
     uint64_t cpw = (nchunks + target_waves - 1) / target_waves;
     if (cpw == 0) cpw = 1;
     const uint64_t waves = (nchunks + cpw - 1) / cpw;
@@ -300,17 +308,13 @@ int launch_frames(const void *d_base, const uint64_t *d_offsets, uint64_t n, uin
     if (blocks > 0x7FFFFFFFull || cpw > 0xFFFFFFFFull) return AIPSTACK_CHKSUM_EINVAL;
     CsrDesc desc{(uint64_t)(uintptr_t)d_base, d_offsets};
     switch (tuning_frames_in_flight()) {
-        case 1:
-            hipLaunchKernelGGL((frame_kernel<TX, 2, 1, true>), dim3((unsigned)blocks), dim3(kBlock),
-                               0, stream, desc, n, (uint32_t)cpw, d_status);
-            break;
-        case 4:
-            hipLaunchKernelGGL((frame_kernel<TX, 2, 4, true>), dim3((unsigned)blocks), dim3(kBlock),
-                               0, stream, desc, n, (uint32_t)cpw, d_status);
-            break;
-        default:
-            hipLaunchKernelGGL((frame_kernel<TX, 2, 2, true>), dim3((unsigned)blocks), dim3(kBlock),
-                               0, stream, desc, n, (uint32_t)cpw, d_status);
+#define AIPSTACK_LAUNCH_FRAMES(P)                                                          \
+    hipLaunchKernelGGL((frame_kernel<TX, 2, P, true>), dim3((unsigned)blocks), dim3(kBlock), \
+                       0, stream, desc, n, (uint32_t)cpw, d_status)
+        case 2: AIPSTACK_LAUNCH_FRAMES(2); break;
+        case 8: AIPSTACK_LAUNCH_FRAMES(8); break;
+        default: AIPSTACK_LAUNCH_FRAMES(4);
+#undef AIPSTACK_LAUNCH_FRAMES
     }
     return check_hip(hipGetLastError());
 }

@@ -162,7 +162,9 @@ def _build(rng, peer):
             l4 = _craft_zero_sum(l4, coff, extra)
         struct.pack_into(">H", l4, coff, 0)
         c = chksum(bytes(l4), extra)
-        if proto == 17 and c == 0:
+        if proto == 17 and rng.chance(1, 10):
+            c = 0                                       # UDP without a checksum
+        elif proto == 17 and c == 0:
             c = 0xFFFF                                  # udp/IpUdpProto.h:176-178
         elif craft and c == 0 and rng.chance(1, 2):
             c = 0xFFFF                                  # the other zero, must verify too

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Launch-parameter sweep of the batch checksum kernel, interleaved in ONE process.
+"""Launch-parameter sweep of the batch checksum and frame kernels, interleaved in ONE process.
 
 Each variant sets the library tunables (aipstack_chksum_tune), launches the batch, and is
 timed with HIP events on the launch stream; variants are interleaved round by round (so
@@ -8,6 +8,7 @@ to the first one's and, for a prefix, to the oracle. Prints one JSON object per 
 (median/min kernel us, GB/s of algorithmic bytes, fraction of 8 TB/s) to stdout.
 
     python tools/sweep.py --config A --rounds 8 [--variants "U,P,NT,WPC;..."]
+    python tools/sweep.py --config RX [--variants "F,WPC;..."]   (frames in flight, waves/CU)
 """
 from __future__ import annotations
 
@@ -29,15 +30,18 @@ DEFAULT_VARIANTS = {
          "3,2,1,128;3,4,1,128",
     "C": "0,0,1,0;2,2,1,0;2,4,1,0;2,8,1,0;1,4,1,0;1,8,1,0;2,4,0,0;2,4,1,64;2,4,1,256;"
          "2,8,1,64;2,8,1,256;1,8,1,64",
+    "RX": "0,0;2,0;8,0;4,64;4,256;8,64",
+    "TX": "0,0;2,0;8,0;4,64;4,256;8,64",
 }
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", default="A", choices=["A", "B", "C"])
+    ap.add_argument("--config", default="A", choices=["A", "B", "C", "RX", "TX"])
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--reps", type=int, default=5, help="launches per variant per round")
-    ap.add_argument("--variants", default=None, help='"U,P,NT,WPC;..." (0 = automatic)')
+    ap.add_argument("--variants", default=None,
+                    help='"U,P,NT,WPC;..." or, for RX/TX, "F,WPC;..." (0 = automatic)')
     args = ap.parse_args()
 
     import torch
@@ -52,9 +56,30 @@ def main():
         n, plen, layout = 1 << 20, 1500, "strided"
     elif args.config == "B":
         n, plen, layout = 256 << 10, 9000, "strided"
-    else:
+    elif args.config == "C":
         n, plen, layout = 2 << 20, None, "csr"
-    if layout == "strided":
+    else:
+        n, plen, layout = 1 << 20, None, args.config.lower()
+    if layout in ("rx", "tx"):
+        fbuf, off = synth.frames_host(n, seed=synth.SEED_DATA, max_payload=1460)
+        orc0 = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "libchksum_oracle.so"))
+        orc0.oracle_tx_fill_batch.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_uint64,
+                                                                      ctypes.c_void_p]
+        orc0.oracle_rx_verify_batch.argtypes = orc0.oracle_tx_fill_batch.argtypes
+        o64 = off.astype(np.uint64)
+        st = np.empty(n, dtype=np.uint8)
+        if layout == "rx":
+            orc0.oracle_tx_fill_batch(fbuf.ctypes.data, o64.ctypes.data, n, st.ctypes.data)
+            want_rx = np.empty(n, dtype=np.uint8)
+            orc0.oracle_rx_verify_batch(fbuf.ctypes.data, o64.ctypes.data, n, want_rx.ctypes.data)
+        else:
+            want_tx = fbuf.copy()
+            orc0.oracle_tx_fill_batch(want_tx.ctypes.data, o64.ctypes.data, n, st.ctypes.data)
+        total = int(off[-1])
+        buf = torch.from_numpy(fbuf).to(dev)
+        d_off = torch.from_numpy(off).to(dev)
+        alg = total + 8 * (n + 1) + n + (4 * n if layout == "tx" else 0)
+    elif layout == "strided":
         total = n * plen
         buf = torch.empty(total, dtype=torch.uint8, device=dev)
         synth.fill_device(buf, synth.SEED_DATA)
@@ -67,16 +92,25 @@ def main():
         d_off = torch.from_numpy(off).to(dev)
         synth.apply_classes_device(buf, d_off)
         alg = total + 2 * n + 8 * (n + 1)
-    out = torch.empty(n, dtype=torch.uint16, device=dev)
+    out = torch.empty(n, dtype=torch.uint8 if layout in ("rx", "tx") else torch.uint16,
+                      device=dev)
 
     def run():
-        if layout == "strided":
+        if layout == "rx":
+            A.rx_verify(buf, d_off, out=out, stream=stream)
+        elif layout == "tx":
+            A.tx_fill(buf, d_off, out=out, stream=stream)
+        elif layout == "strided":
             A.chksum_batch_strided(buf, plen, plen, n, out=out, stream=stream)
         else:
             A.chksum_batch_csr(buf, d_off, out=out, stream=stream)
 
     variants = []
     for v in (args.variants or DEFAULT_VARIANTS[args.config]).split(";"):
+        if layout in ("rx", "tx"):
+            f, wpc = (int(x) for x in v.split(","))
+            variants.append({"frames": f, "waves_per_cu": wpc})
+            continue
         u, p, nt, wpc = (int(x) for x in v.split(","))
         variants.append({"unroll": u, "packets": p, "nontemporal": nt, "waves_per_cu": wpc})
 
@@ -85,12 +119,21 @@ def main():
             assert lib.aipstack_chksum_tune(k.encode(), val) == 0
         lib.aipstack_chksum_tune(b"chunks_per_wave", 0)
 
+    def check(got):
+        if layout == "rx":
+            return bool(np.array_equal(got, want_rx))
+        if layout == "tx":
+            return bool(np.array_equal(buf.cpu().numpy(), want_tx))
+        return bool(np.array_equal(got[:m], want))
+
     # reference output: oracle on a prefix
+    m = min(n, 65536)
     orc = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "libchksum_oracle.so"))
     host = buf.cpu().numpy()
-    m = min(n, 65536)
     want = np.empty(m, dtype=np.uint16)
-    if layout == "strided":
+    if layout in ("rx", "tx"):
+        pass
+    elif layout == "strided":
         orc.oracle_batch_strided.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
                                              ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32]
         orc.oracle_batch_strided(host.ctypes.data, plen, plen, m, want.ctypes.data, 0)
@@ -111,7 +154,7 @@ def main():
         got = out.cpu().numpy()
         if first is None:
             first = got.copy()
-        ok[vi] = bool(np.array_equal(got, first) and np.array_equal(got[:m], want))
+        ok[vi] = bool(np.array_equal(got, first) and check(got))
     for _ in range(args.rounds):
         for vi, v in enumerate(variants):
             apply(v)
