@@ -299,6 +299,12 @@ struct PacketLoad {
 
     // not_lane0 = ~0 on every lane but lane 0 (where it is 0).
     __device__ __forceinline__ uint32_t finish(int lane, uint32_t voff, uint32_t not_lane0) {
+        return wave_sum(lane_partial(lane, voff, not_lane0));
+    }
+
+    // This lane's share of finish() before the cross-lane sum (< 2^18 per lane), so that a
+    // wave can reduce several packets' partials together (wave_sum_n).
+    __device__ __forceinline__ uint32_t lane_partial(int lane, uint32_t voff, uint32_t not_lane0) {
         if (nseg == 0)
             return 0;
         const int last = nseg - 1;
@@ -316,9 +322,28 @@ struct PacketLoad {
         }
         // fold each chain to 17 bits (nonzero stays nonzero): 2 x 64 lanes x 0x1FFFE < 2^24
         const uint32_t s0 = acc0.finish(), s1 = acc1.finish();
-        return wave_sum((s0 & 0xFFFFu) + (s0 >> 16) + (s1 & 0xFFFFu) + (s1 >> 16));
+        return (s0 & 0xFFFFu) + (s0 >> 16) + (s1 & 0xFFFFu) + (s1 >> 16);
     }
 };
+
+// wave_sum of N values at once: the N DPP chains interleave, so each chain's data-hazard
+// wait states are filled by the others' instructions instead of s_nop. Results
+// wave-uniform.
+template <int N>
+__device__ __forceinline__ void wave_sum_n(uint32_t (&v)[N]) {
+#define AIPSTACK_DPP_N(ctrl, rowmask)                                                     \
+    _Pragma("unroll") for (int i = 0; i < N; ++i)                                         \
+        v[i] += __builtin_amdgcn_update_dpp(0u, v[i], ctrl, rowmask, 0xF, false);
+    AIPSTACK_DPP_N(0x111, 0xF)
+    AIPSTACK_DPP_N(0x112, 0xF)
+    AIPSTACK_DPP_N(0x114, 0xF)
+    AIPSTACK_DPP_N(0x118, 0xF)
+    AIPSTACK_DPP_N(0x142, 0xA)
+    AIPSTACK_DPP_N(0x143, 0xC)
+#undef AIPSTACK_DPP_N
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] = __builtin_amdgcn_readlane(v[i], 63);
+}
 
 // Sum over the 64 lanes (DPP row scan + row broadcasts); result valid in lane 63,
 // returned wave-uniform via readlane.

@@ -84,11 +84,12 @@ __global__ __launch_bounds__(kBlock) void chksum_batch_kernel(Desc desc, uint64_
                     j0 + q < cnt ? (uint32_t)__builtin_amdgcn_readlane(meta.packed, j) : 16u << 4;
                 pk[q].issue_meta(a0, packed, voff);
             }
+            uint32_t part[P];
 #pragma unroll
-            for (int q = 0; q < P; ++q) {
-                const uint32_t t = pk[q].finish(lane, voff, not_lane0);  // wave-uniform
-                sums = (lane == j0 + q) ? t : sums;
-            }
+            for (int q = 0; q < P; ++q) part[q] = pk[q].lane_partial(lane, voff, not_lane0);
+            wave_sum_n<P>(part);  // wave-uniform
+#pragma unroll
+            for (int q = 0; q < P; ++q) sums = (lane == j0 + q) ? part[q] : sums;
         }
         // Finalise the chunk's 64 results together (VALU, one packet per lane).
         uint32_t r = fold16(sums);

@@ -244,6 +244,8 @@ __global__ __launch_bounds__(kBlock) void frame_kernel(CsrDesc desc, uint64_t n,
             PacketLoad<U, NT> pk[P];
             int jq[P];
             uint32_t fxq[P];
+            u32x4 xmq[P];  // Tx: the not-pair mask of the checksum field, fetched at issue
+            uint32_t part[P];
 #pragma unroll
             for (int q = 0; q < P; ++q) {
                 const bool valid = todo != 0;
@@ -255,20 +257,22 @@ __global__ __launch_bounds__(kBlock) void frame_kernel(CsrDesc desc, uint64_t n,
                 const uint32_t packed =
                     valid ? (uint32_t)__builtin_amdgcn_readlane(meta.packed, j) : 16u << 4;
                 fxq[q] = TX ? (uint32_t)__builtin_amdgcn_readlane(fl.fx, j) : 0u;
+                if (TX) xmq[q] = load_mask(kMaskNotPair[fxq[q] & 15u]);
                 pk[q].issue_meta(a0, packed, voff);
             }
 #pragma unroll
             for (int q = 0; q < P; ++q) {
                 if (TX) {  // the checksum field itself is summed as 0
                     const int fx = (int)fxq[q];
-                    apply_mask(pk[q].v[0], load_mask(kMaskNotPair[fx & 15]),
-                               lane == (fx >> 4) ? 0u : ~0u);
-                    apply_mask(pk[q].v[0], load_mask(kMaskFrom[1]),
-                               ((fx & 15) == 15 && lane == (fx >> 4) + 1) ? 0u : ~0u);
+                    apply_mask(pk[q].v[0], xmq[q], lane == (fx >> 4) ? 0u : ~0u);
+                    // a field straddling two segments: byte 0 of the next one
+                    pk[q].v[0][0] &= ((fx & 15) == 15 && lane == (fx >> 4) + 1) ? ~0xFFu : ~0u;
                 }
-                const uint32_t t = pk[q].finish(lane, voff, not_lane0);  // wave-uniform
-                sums = (lane == jq[q]) ? t : sums;
+                part[q] = pk[q].lane_partial(lane, voff, not_lane0);
             }
+            wave_sum_n<P>(part);  // wave-uniform
+#pragma unroll
+            for (int q = 0; q < P; ++q) sums = (lane == jq[q]) ? part[q] : sums;
         }
 
         // (D) per-lane finish
@@ -279,12 +283,16 @@ __global__ __launch_bounds__(kBlock) void frame_kernel(CsrDesc desc, uint64_t n,
         uint32_t chk = (~fold16((uint32_t)m + (uint32_t)(m >> 32))) & 0xFFFFu;
         int v = fl.pre;
         if (TX) {
-            if (fl.ip_ok)
+#ifndef AIPSTACK_EXP_TX_STORES
+#define AIPSTACK_EXP_TX_STORES 3
+#endif
+            if ((AIPSTACK_EXP_TX_STORES & 1) && fl.ip_ok)
                 store_be16(S + 24, fl.hchk);
             if (need) {
                 if (fl.udp && chk == 0) chk = 0xFFFFu;              // udp/IpUdpProto.h:176-178
-                store_be16(S + (uint64_t)fl.fld, chk);
+                if (AIPSTACK_EXP_TX_STORES & 2) store_be16(S + (uint64_t)fl.fld, chk);
             }
+            if (AIPSTACK_EXP_TX_STORES != 3 && chk == 0x1234u && fl.hchk == 0x4321u) v = 9;
         } else if (need) {
             v = chk == 0 ? AIPSTACK_RX_ACCEPT : AIPSTACK_RX_DROP_L4_CHKSUM;
         }
