@@ -283,16 +283,12 @@ __global__ __launch_bounds__(kBlock) void frame_kernel(CsrDesc desc, uint64_t n,
         uint32_t chk = (~fold16((uint32_t)m + (uint32_t)(m >> 32))) & 0xFFFFu;
         int v = fl.pre;
         if (TX) {
-#ifndef AIPSTACK_EXP_TX_STORES
-#define AIPSTACK_EXP_TX_STORES 3
-#endif
-            if ((AIPSTACK_EXP_TX_STORES & 1) && fl.ip_ok)
+            if (fl.ip_ok)
                 store_be16(S + 24, fl.hchk);
             if (need) {
                 if (fl.udp && chk == 0) chk = 0xFFFFu;              // udp/IpUdpProto.h:176-178
-                if (AIPSTACK_EXP_TX_STORES & 2) store_be16(S + (uint64_t)fl.fld, chk);
+                store_be16(S + (uint64_t)fl.fld, chk);
             }
-            if (AIPSTACK_EXP_TX_STORES != 3 && chk == 0x1234u && fl.hchk == 0x4321u) v = 9;
         } else if (need) {
             v = chk == 0 ? AIPSTACK_RX_ACCEPT : AIPSTACK_RX_DROP_L4_CHKSUM;
         }
