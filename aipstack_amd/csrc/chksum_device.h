@@ -345,6 +345,53 @@ __device__ __forceinline__ void wave_sum_n(uint32_t (&v)[N]) {
     for (int i = 0; i < N; ++i) v[i] = __builtin_amdgcn_readlane(v[i], 63);
 }
 
+// No per-packet adjustment (see sum_lane_packets).
+struct NoMaskHook {
+    template <class PK>
+    __device__ __forceinline__ void issue(int, int) {}
+    template <class PK>
+    __device__ __forceinline__ void apply(int, PK &, int) {}
+};
+
+// The packets of a 64-packet chunk whose lanes are set in `todo` (wave-uniform), each
+// summed by the whole wave with P packets' loads in flight; lane j receives packet j's
+// exact halves-sum (< 2^24; 0 iff all its bytes are 0), other lanes 0. `meta` is the
+// per-lane LaneMeta. hook.issue(q, j) runs when packet j's loads are issued into slot q,
+// hook.apply(q, pk, lane) just before slot q is reduced (e.g. to mask a field).
+template <int U, int P, bool NT, class Hook>
+__device__ __forceinline__ uint32_t sum_lane_packets(const LaneMeta &meta, uint64_t todo,
+                                                     int lane, uint32_t voff,
+                                                     uint32_t not_lane0, Hook &hook) {
+    uint32_t sums = 0;
+    while (todo) {
+        PacketLoad<U, NT> pk[P];
+        int jq[P];
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+            const bool valid = todo != 0;
+            const int j = valid ? (int)__builtin_ctzll(todo) : 0;
+            todo &= todo - 1;
+            jq[q] = valid ? j : -1;
+            const uint64_t a0 = ((uint64_t)__builtin_amdgcn_readlane(meta.a0_hi, j) << 32) |
+                                (uint32_t)__builtin_amdgcn_readlane(meta.a0_lo, j);
+            const uint32_t packed =
+                valid ? (uint32_t)__builtin_amdgcn_readlane(meta.packed, j) : 16u << 4;
+            hook.template issue<PacketLoad<U, NT>>(q, j);
+            pk[q].issue_meta(a0, packed, voff);
+        }
+        uint32_t part[P];
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+            hook.apply(q, pk[q], lane);
+            part[q] = pk[q].lane_partial(lane, voff, not_lane0);
+        }
+        wave_sum_n<P>(part);  // wave-uniform
+#pragma unroll
+        for (int q = 0; q < P; ++q) sums = (lane == jq[q]) ? part[q] : sums;
+    }
+    return sums;
+}
+
 // Sum over the 64 lanes (DPP row scan + row broadcasts); result valid in lane 63,
 // returned wave-uniform via readlane.
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {

@@ -71,26 +71,11 @@ __global__ __launch_bounds__(kBlock) void chksum_batch_kernel(Desc desc, uint64_
         desc.lane_bounds(chunk, lane, lS, lE);
         if (lane >= cnt) lE = lS;  // past the batch: empty
         const LaneMeta meta = lane_meta(lS, lE);
-        uint32_t sums = 0;  // lane j: exact halves-sum of packet j (< 2^24)
-        // P packets at a time: all their first-group loads in flight, then reduce each.
-        for (int j0 = 0; j0 < cnt; j0 += P) {
-            PacketLoad<U, NT> pk[P];
-#pragma unroll
-            for (int q = 0; q < P; ++q) {
-                const int j = min(j0 + q, kWave - 1);  // j0 + q >= cnt: an empty lane
-                const uint64_t a0 = ((uint64_t)__builtin_amdgcn_readlane(meta.a0_hi, j) << 32) |
-                                    (uint32_t)__builtin_amdgcn_readlane(meta.a0_lo, j);
-                const uint32_t packed =
-                    j0 + q < cnt ? (uint32_t)__builtin_amdgcn_readlane(meta.packed, j) : 16u << 4;
-                pk[q].issue_meta(a0, packed, voff);
-            }
-            uint32_t part[P];
-#pragma unroll
-            for (int q = 0; q < P; ++q) part[q] = pk[q].lane_partial(lane, voff, not_lane0);
-            wave_sum_n<P>(part);  // wave-uniform
-#pragma unroll
-            for (int q = 0; q < P; ++q) sums = (lane == j0 + q) ? part[q] : sums;
-        }
+        // lane j: exact halves-sum of packet j (< 2^24); empty packets are skipped
+        NoMaskHook hook;
+        const uint32_t sums = sum_lane_packets<U, P, NT>(
+            meta, __builtin_amdgcn_ballot_w64((meta.packed >> 9) != 0), lane, voff, not_lane0,
+            hook);
         // Finalise the chunk's 64 results together (VALU, one packet per lane).
         uint32_t r = fold16(sums);
         if ((meta.packed & 1u) == 0)  // S even (A0 is 16-aligned, so S & 1 = rel_s & 1)
@@ -122,50 +107,118 @@ __global__ __launch_bounds__(kBlock) void chksum_batch_kernel(Desc desc, uint64_
 // swapped an even number of times. With the kernel's little-endian sum of the chunk at
 // address a_k, that is: byte-swap the folded chunk sum iff parity(a_k) == parity(q_k).
 // ---------------------------------------------------------------------------------
-template <int U, bool NT>
+//
+// A wave owns 64 chains and walks their chunks (contiguous in the table) 64 at a time,
+// chunk <-> lane: coalesced loads of the chunk table; the chunk's chain from the chain
+// starts marked in LDS and a max-scan; its logical-position parity from a ballot of odd
+// lengths (prefix popcounts) plus the parity carried in from the previous 64 chunks; the
+// chunk sums one per wave, P in flight (sum_lane_packets, as the CSR batch); then each
+// oriented chunk sum is added into its chain's LDS accumulator.
+// ---------------------------------------------------------------------------------
+
+// Inclusive max-scan over the wave of non-decreasing-where-set values (-1 = unset).
+__device__ __forceinline__ int wave_max_scan(int v) {
+#define AIPSTACK_MAXSCAN(ctrl, rowmask) \
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, ctrl, rowmask, 0xF, false));
+    AIPSTACK_MAXSCAN(0x111, 0xF)
+    AIPSTACK_MAXSCAN(0x112, 0xF)
+    AIPSTACK_MAXSCAN(0x114, 0xF)
+    AIPSTACK_MAXSCAN(0x118, 0xF)
+    AIPSTACK_MAXSCAN(0x142, 0xA)
+    AIPSTACK_MAXSCAN(0x143, 0xC)
+#undef AIPSTACK_MAXSCAN
+    return v;
+}
+
+__device__ __forceinline__ uint32_t parity_below(uint64_t mask, uint32_t s) {  // s in 0..64
+    const uint64_t below = s == 0 ? 0ull : (~0ull >> (64u - s));
+    return (uint32_t)__builtin_popcountll(mask & below) & 1u;
+}
+
+template <int U, int P, bool NT>
 __global__ __launch_bounds__(kBlock) void chksum_chain_kernel(
     const uint64_t *__restrict__ chunk_addr, const uint32_t *__restrict__ chunk_len,
     const uint64_t *__restrict__ index, const uint32_t *__restrict__ states, uint64_t n,
     uint32_t chunks_per_wave, uint16_t *__restrict__ out, uint32_t flags) {
+    __shared__ uint32_t lds_acc[kWavesPerBlock][kWave];  // per-chain sum of chunk sums
+    __shared__ int lds_mark[kWavesPerBlock][kWave];      // chain starting at chunk lane
     const int lane = threadIdx.x & (kWave - 1);
     const uint32_t wave_in_block = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerBlock + wave_in_block;
-    const uint64_t nchunks = (n + kWave - 1) / kWave;
+    const uint64_t ngroups = (n + kWave - 1) / kWave;
     uint64_t c = wave * chunks_per_wave;
-    const uint64_t c_end = min(c + chunks_per_wave, nchunks);
+    const uint64_t c_end = min(c + chunks_per_wave, ngroups);
     const bool final_flag = (flags & AIPSTACK_CHKSUM_FINAL) != 0;
     const uint32_t voff = (uint32_t)lane * 16u;
     const uint32_t not_lane0 = lane == 0 ? 0u : ~0u;
-    CsrDesc idx_desc{0, index};  // reuse the CSR offset walk for the chunk index
+    uint32_t *acc = lds_acc[wave_in_block];
+    int *mark = lds_mark[wave_in_block];
+    CsrDesc idx_desc{0, index};  // the chain index walks like CSR offsets
 
     for (; c < c_end; ++c) {
         const uint64_t p0 = c * kWave;
-        const auto chunk = idx_desc.begin_chunk(p0, n, lane);
+        const auto grp = idx_desc.begin_chunk(p0, n, lane);
         const int cnt = (int)min((uint64_t)kWave, n - p0);
-        uint32_t state = 0;
-        if (states != nullptr && p0 + lane < n)
-            state = states[p0 + lane];
-        uint32_t sums = 0;  // lane j: sum of chain j's orientation-corrected chunk sums
-        for (int j = 0; j < cnt; ++j) {
-            uint64_t k0, k1;
-            idx_desc.bounds(chunk, j, k0, k1);
-            uint32_t acc = 0;   // <= nchunks * 0xFFFF
-            uint32_t pos = 0;   // parity of the logical position
-            for (uint64_t k = k0; k < k1; ++k) {
-                const uint64_t a = chunk_addr[k];
-                const uint32_t l = chunk_len[k];
-                PacketLoad<U, NT> pk;
-                pk.issue(a, a + l, voff);
-                uint32_t r = fold16(pk.finish(lane, voff, not_lane0));
-                if ((uint32_t)(a & 1) == pos)
-                    r = bswap16(r);
-                acc += r;
-                pos ^= l & 1;
+        const uint32_t state = (states != nullptr && p0 + lane < n) ? states[p0 + lane] : 0u;
+        // chain `lane` = chunks [cs, ce) (relative to the group's first chunk K0)
+        uint64_t cs64, ce64;
+        idx_desc.lane_bounds(grp, lane, cs64, ce64);
+        const uint64_t K0 = idx_desc.offset_of(grp, 0);
+        const uint64_t K1 = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(grp.end_off >> 32))
+                             << 32) | __builtin_amdgcn_readfirstlane((uint32_t)grp.end_off);
+        const bool chain_nonempty = lane < cnt && ce64 > cs64;
+        const uint32_t cs = (uint32_t)(cs64 - K0);  // < 2^32 chunks per group (contract)
+        acc[lane] = 0;
+        int carry_cid = -1;      // chain of the last chunk of the previous 64
+        uint32_t carry_par = 0;  // its logical position parity after that chunk
+        for (uint64_t kb = K0; kb < K1; kb += kWave) {
+            const uint32_t kr = (uint32_t)(kb - K0);
+            const uint64_t k = kb + (uint64_t)lane;
+            const bool valid = k < K1;
+            uint64_t a = 0;
+            uint32_t l = 0;
+            if (valid) {
+                a = chunk_addr[k];
+                l = chunk_len[k];
             }
-            sums = (lane == j) ? acc : sums;
+            // which chain: the last chain starting at or before this chunk
+            mark[lane] = -1;
+            __builtin_amdgcn_wave_barrier();
+            if (chain_nonempty && cs >= kr && cs - kr < (uint32_t)kWave)
+                mark[cs - kr] = lane;
+            __builtin_amdgcn_wave_barrier();
+            int cid = wave_max_scan(mark[lane]);
+            if (cid < 0) cid = carry_cid;  // continues a chain from the previous 64
+            __builtin_amdgcn_wave_barrier();
+            // logical position parity: odd lengths before this chunk within its chain
+            const uint64_t odd = __builtin_amdgcn_ballot_w64(valid && (l & 1u));
+            const uint32_t scs = (uint32_t)__builtin_amdgcn_ds_bpermute(max(cid, 0) << 2, (int)cs);
+            const bool before = scs < kr;  // the chain began in an earlier 64
+            const uint32_t s = before ? 0u : scs - kr;
+            uint32_t q = parity_below(odd, (uint32_t)lane) ^ parity_below(odd, s);
+            if (before) q ^= carry_par;
+            // chunk sums, one per wave
+            const LaneMeta meta = lane_meta(a, a + (uint64_t)l);
+            NoMaskHook hook;
+            const uint32_t sums = sum_lane_packets<U, P, NT>(
+                meta, __builtin_amdgcn_ballot_w64(valid && (meta.packed >> 9) != 0), lane, voff,
+                not_lane0, hook);
+            uint32_t r = fold16(sums);
+            if ((uint32_t)(a & 1) == q)
+                r = bswap16(r);
+            if (valid && r != 0)
+                __hip_atomic_fetch_add(&acc[cid], r, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+            // carry to the next 64 chunks
+            const int last = (int)min((uint64_t)(kWave - 1), K1 - kb - 1);
+            carry_cid = __builtin_amdgcn_readlane(cid, last);
+            carry_par = __builtin_amdgcn_readlane(q ^ (l & 1u), last);
         }
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t sum = acc[lane];  // <= chunks * 0xFFFF
+        __builtin_amdgcn_wave_barrier();
         // m_sum = state (+) chain sum with end-around carry; getChksum folds and inverts.
-        const uint64_t t = (uint64_t)state + fold16(sums);
+        const uint64_t t = (uint64_t)state + fold16(sum);
         uint32_t r = fold16((uint32_t)t + (uint32_t)(t >> 32));
         r = final_flag ? (~r & 0xFFFFu) : r;
         if (lane < cnt)
@@ -284,7 +337,7 @@ int launch(const Desc &desc, uint64_t n, uint32_t max_len, uint16_t *d_out, uint
     return AIPSTACK_CHKSUM_EINVAL;
 }
 
-template <int U, bool NT>
+template <int U, int P, bool NT>
 int launch_chain(const uint64_t *d_addr, const uint32_t *d_len, const uint64_t *d_index,
                  const uint32_t *d_states, uint64_t n, uint16_t *d_out, uint32_t flags,
                  hipStream_t stream) {
@@ -297,7 +350,7 @@ int launch_chain(const uint64_t *d_addr, const uint32_t *d_len, const uint64_t *
     const uint64_t waves = (nchunks + cpw - 1) / cpw;
     const uint64_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
     if (blocks > 0x7FFFFFFFull || cpw > 0xFFFFFFFFull) return AIPSTACK_CHKSUM_EINVAL;
-    hipLaunchKernelGGL((chksum_chain_kernel<U, NT>), dim3((unsigned)blocks), dim3(kBlock), 0,
+    hipLaunchKernelGGL((chksum_chain_kernel<U, P, NT>), dim3((unsigned)blocks), dim3(kBlock), 0,
                        stream, d_addr, d_len, d_index, d_states, n, (uint32_t)cpw, d_out, flags);
     return check_hip(hipGetLastError());
 }
@@ -375,8 +428,8 @@ extern "C" int aipstack_chksum_batch_chain(const uint64_t *d_chunk_addr,
     if (n > (1ull << 40)) return AIPSTACK_CHKSUM_EINVAL;
     // Chains are mostly short pieces (headers, ring-buffer halves): U = 2 covers 2 KiB.
     return tuning().nontemporal.load(std::memory_order_relaxed)
-               ? launch_chain<2, true>(d_chunk_addr, d_chunk_len, d_chunk_index, d_states, n,
+               ? launch_chain<2, 4, true>(d_chunk_addr, d_chunk_len, d_chunk_index, d_states, n,
                                        d_out, flags, (hipStream_t)stream)
-               : launch_chain<2, false>(d_chunk_addr, d_chunk_len, d_chunk_index, d_states, n,
+               : launch_chain<2, 4, false>(d_chunk_addr, d_chunk_len, d_chunk_index, d_states, n,
                                         d_out, flags, (hipStream_t)stream);
 }

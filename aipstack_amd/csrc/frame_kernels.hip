@@ -189,6 +189,27 @@ __device__ __forceinline__ FrameLane parse_lane(const u32x4 (&seg)[kHdrSegs], ui
     return r;
 }
 
+// Tx: the L4 checksum field is summed as 0. Its offset from the L4 range's aligned base
+// (< 32: lanes 0-2 of slot 0) is read per frame at issue, with its not-pair mask.
+template <int P>
+struct TxFieldHook {
+    uint32_t fx_lane;  // FrameLane::fx of this lane's frame
+    uint32_t fxq[P];
+    u32x4 xmq[P];
+    template <class PK>
+    __device__ __forceinline__ void issue(int q, int j) {
+        fxq[q] = (uint32_t)__builtin_amdgcn_readlane(fx_lane, j);
+        xmq[q] = load_mask(kMaskNotPair[fxq[q] & 15u]);
+    }
+    template <class PK>
+    __device__ __forceinline__ void apply(int q, PK &pk, int lane) {
+        const int fx = (int)fxq[q];
+        apply_mask(pk.v[0], xmq[q], lane == (fx >> 4) ? 0u : ~0u);
+        // a field straddling two segments: byte 0 of the next one
+        pk.v[0][0] &= ((fx & 15) == 15 && lane == (fx >> 4) + 1) ? ~0xFFu : ~0u;
+    }
+};
+
 // Rx verify / Tx fill of n frames at CSR offsets. A wave walks 64-frame chunks:
 //   (B) lane j loads frame j's first 112 aligned bytes (one buffer descriptor per chunk)
 //       and parses its headers (parse_lane): the L4 byte range, pseudo-header words and
@@ -238,41 +259,15 @@ __global__ __launch_bounds__(kBlock) void frame_kernel(CsrDesc desc, uint64_t n,
         const LaneMeta meta = lane_meta(fl.l4s, fl.l4e);
 
         // (C) L4 sums, one frame per wave, P frames' loads in flight
-        uint64_t todo = __builtin_amdgcn_ballot_w64(need);
-        uint32_t sums = 0;
-        while (todo) {
-            PacketLoad<U, NT> pk[P];
-            int jq[P];
-            uint32_t fxq[P];
-            u32x4 xmq[P];  // Tx: the not-pair mask of the checksum field, fetched at issue
-            uint32_t part[P];
-#pragma unroll
-            for (int q = 0; q < P; ++q) {
-                const bool valid = todo != 0;
-                const int j = valid ? (int)__builtin_ctzll(todo) : 0;
-                todo &= todo - 1;
-                jq[q] = valid ? j : -1;
-                const uint64_t a0 = ((uint64_t)__builtin_amdgcn_readlane(meta.a0_hi, j) << 32) |
-                                    (uint32_t)__builtin_amdgcn_readlane(meta.a0_lo, j);
-                const uint32_t packed =
-                    valid ? (uint32_t)__builtin_amdgcn_readlane(meta.packed, j) : 16u << 4;
-                fxq[q] = TX ? (uint32_t)__builtin_amdgcn_readlane(fl.fx, j) : 0u;
-                if (TX) xmq[q] = load_mask(kMaskNotPair[fxq[q] & 15u]);
-                pk[q].issue_meta(a0, packed, voff);
-            }
-#pragma unroll
-            for (int q = 0; q < P; ++q) {
-                if (TX) {  // the checksum field itself is summed as 0
-                    const int fx = (int)fxq[q];
-                    apply_mask(pk[q].v[0], xmq[q], lane == (fx >> 4) ? 0u : ~0u);
-                    // a field straddling two segments: byte 0 of the next one
-                    pk[q].v[0][0] &= ((fx & 15) == 15 && lane == (fx >> 4) + 1) ? ~0xFFu : ~0u;
-                }
-                part[q] = pk[q].lane_partial(lane, voff, not_lane0);
-            }
-            wave_sum_n<P>(part);  // wave-uniform
-#pragma unroll
-            for (int q = 0; q < P; ++q) sums = (lane == jq[q]) ? part[q] : sums;
+        uint32_t sums;
+        const uint64_t todo = __builtin_amdgcn_ballot_w64(need);
+        if (TX) {
+            TxFieldHook<P> hook;
+            hook.fx_lane = fl.fx;
+            sums = sum_lane_packets<U, P, NT>(meta, todo, lane, voff, not_lane0, hook);
+        } else {
+            NoMaskHook hook;
+            sums = sum_lane_packets<U, P, NT>(meta, todo, lane, voff, not_lane0, hook);
         }
 
         // (D) per-lane finish

@@ -42,6 +42,8 @@ CONFIGS = {
     # SURVEY 8(f) rows 2-3 (not BASELINE metric lines): raw Ethernet frames
     "RX": ("rx", 1 << 20, None),
     "TX": ("tx", 1 << 20, None),
+    # chained + seeded (TCP Tx shape)
+    "CHAIN": ("chain", 1 << 20, None),
 }
 WORKLOAD_NAMES = {
     "A": "1M x 1500B Ethernet-MTU packets per GPU, IP checksum (BASELINE configs[1]; x8 = configs[4])",
@@ -51,7 +53,10 @@ WORKLOAD_NAMES = {
           "Rx verify: IPv4 header + L4 checksum verdicts",
     "TX": "1M raw Ethernet frames per GPU (same mix), Tx fill: IPv4 header + L4 checksums "
           "written in place",
+    "CHAIN": "1M TCP-Tx-shaped chains per GPU: IpChksumAccumulator(pseudo-header State)"
+             ".getChksum(20B header node + 1460B payload in 2 chunks split at a random point)",
 }
+CHAIN_HDR_STRIDE, CHAIN_HDR, CHAIN_PAYLOAD = 32, 20, 1460
 
 
 def log(*a):
@@ -96,8 +101,8 @@ def shard_spec(config, rank, world, n=None):
         spec["total"] = n * plen
         spec["byte_offset"] = rank * n * plen
         spec["offsets"] = None
-    elif layout in ("rx", "tx"):
-        # each rank synthesises its own frames (seed per rank): frames are independent
+    elif layout in ("rx", "tx", "chain"):
+        # each rank synthesises its own frames / chains (seed per rank): they are independent
         spec["seed"] = synth.SEED_DATA + 1000 * rank
         spec["byte_offset"] = 0
         spec["offsets"] = None  # known after synthesis
@@ -133,13 +138,66 @@ def host_shard(spec):
 
 def algorithmic_bytes(layout, n, total_payload):
     """L bytes read + 2 bytes written per packet (+8 B offset for CSR).
-    Frames: L read + 8 B offset + 1 B verdict/status (+ 4 B of checksums written, Tx)."""
+    Frames: L read + 8 B offset + 1 B verdict/status (+ 4 B of checksums written, Tx).
+    Chains: chunk bytes + 12 B (address, length) per chunk + 8 B index + 4 B state + 2 B
+    result per chain (3 chunks per chain here)."""
+    if layout == "chain":
+        return total_payload + 3 * 12 * n + 8 * (n + 1) + 4 * n + 2 * n
     if layout in ("rx", "tx"):
         return total_payload + 9 * n + 8 + (4 * n if layout == "tx" else 0)
     b = total_payload + 2 * n
     if layout == "csr":
         b += 8 * (n + 1)
     return b
+
+
+def make_chains(spec, dev):
+    """CHAIN workload: chain i = a 20-B header node (TCP header, 32-B stride header area)
+    + 1460 payload bytes split into two chunks at a random point (a send ring wrapping,
+    tcp/IpTcpProto_output.h:1251-1277), seeded with a random pseudo-header State. Device
+    tensors plus the host copies parity needs."""
+    import torch
+    from aipstack_amd import synth
+    n = spec["n"]
+    hdr_bytes = CHAIN_HDR_STRIDE * n
+    buf = torch.empty(hdr_bytes + CHAIN_PAYLOAD * n, dtype=torch.uint8, device=dev)
+    synth.fill_device(buf, spec["seed"])
+    rng = np.random.default_rng(spec["seed"])
+    split = rng.integers(1, CHAIN_PAYLOAD, n).astype(np.uint64)
+    base = buf.data_ptr()
+    i = np.arange(n, dtype=np.uint64)
+    addr = np.empty(3 * n, dtype=np.uint64)
+    lens = np.empty(3 * n, dtype=np.uint32)
+    addr[0::3] = base + CHAIN_HDR_STRIDE * i
+    lens[0::3] = CHAIN_HDR
+    addr[1::3] = base + hdr_bytes + CHAIN_PAYLOAD * i
+    lens[1::3] = split
+    addr[2::3] = addr[1::3] + split
+    lens[2::3] = CHAIN_PAYLOAD - split
+    index = np.arange(n + 1, dtype=np.uint64) * 3
+    states = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    return {
+        "buf": buf, "base": base, "n": n,
+        "addr_host": addr, "len_host": lens, "index_host": index, "states_host": states,
+        "addr": torch.from_numpy(addr.view(np.int64)).to(dev),
+        "len": torch.from_numpy(lens.view(np.int32)).to(dev),
+        "index": torch.from_numpy(index.view(np.int64)).to(dev),
+        "states": torch.from_numpy(states.view(np.int32)).to(dev),
+        "payload": (CHAIN_HDR + CHAIN_PAYLOAD) * n,
+    }
+
+
+def chain_check(chain, got):
+    """Every chain against the C oracle (oracle_batch_chain) over a host copy."""
+    host = chain["buf"].cpu().numpy()
+    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "libchksum_oracle.so"))
+    lib.oracle_batch_chain.argtypes = [ctypes.c_void_p, ctypes.c_uint64] + \
+        [ctypes.c_void_p] * 4 + [ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32]
+    want = np.empty(chain["n"], dtype=np.uint16)
+    lib.oracle_batch_chain(host.ctypes.data, chain["base"], chain["addr_host"].ctypes.data,
+                           chain["len_host"].ctypes.data, chain["index_host"].ctypes.data,
+                           chain["states_host"].ctypes.data, chain["n"], want.ctypes.data, 1)
+    return "bit-exact (every chain vs oracle)" if np.array_equal(got, want) else "MISMATCH"
 
 
 def cpu_baseline(spec):
@@ -248,6 +306,8 @@ def main():
     layout, n, plen = CONFIGS[args.config]
     stream = torch.cuda.current_stream()
     if args.e2e:
+        if layout not in ("strided", "csr"):
+            raise SystemExit("--e2e covers the packet configs A, B, C")
         return e2e(args, rank, world, local_rank, layout, n, plen)
 
     # ---- this rank's shard, generated in place (global packets [rank*n, (rank+1)*n))
@@ -257,6 +317,9 @@ def main():
         buf = torch.from_numpy(frames_host).to(dev)
         d_off = torch.from_numpy(spec["offsets"]).to(dev)
         status = torch.empty(n, dtype=torch.uint8, device=dev)
+    if layout == "chain":
+        chain = make_chains(spec, dev)
+        spec["total"] = chain["payload"]
     off_host = spec["offsets"]
     byte_offset = spec["byte_offset"]
     total = spec["total"]
@@ -276,6 +339,9 @@ def main():
             A.chksum_batch_csr(buf, d_off, out=out, stream=stream)
         elif layout == "rx":
             A.rx_verify(buf, d_off, out=status, stream=stream)
+        elif layout == "chain":
+            A.chksum_batch_chain(chain["addr"], chain["len"], chain["index"], chain["states"],
+                                 out=out, final=True, stream=stream)
         else:  # tx: idempotent (the filled fields are excluded from their own sums)
             A.tx_fill(buf, d_off, out=status, stream=stream)
 
@@ -329,6 +395,9 @@ def main():
     if rank == 0 and layout in ("rx", "tx"):
         if not args.no_parity:
             parity = frames_check(spec, frames_host, buf.cpu().numpy(), status.cpu().numpy())
+    elif rank == 0 and layout == "chain":
+        if not args.no_parity:
+            parity = chain_check(chain, out.cpu().numpy())
     elif rank == 0:
         host_out = out.cpu().numpy()
         if not args.no_cpu_baseline and world == 1:
@@ -358,8 +427,9 @@ def main():
             "workload": WORKLOAD_NAMES[args.config],
             "config": args.config,
             "packets_per_gpu": n,
-            "packet_bytes": plen if plen else ("64-1500 (mixed)" if layout == "csr"
-                                                else "60-1514 (frames)"),
+            "packet_bytes": plen if plen else {"csr": "64-1500 (mixed)",
+                                                "chain": "20 + 1460 in 3 chunks"}.get(
+                                                    layout, "60-1514 (frames)"),
             "payload_bytes_per_gpu": payload,
             "layout": layout,
             "parallelism": f"disjoint packet shards x{world}, no collective",

@@ -17,6 +17,7 @@
  */
 #include <stddef.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "chksum_oracle.h"
 
@@ -125,4 +126,34 @@ void oracle_batch_seeded_csr(const void *base, const uint64_t *offsets,
         size_t l = (size_t)(offsets[i + 1] - offsets[i]);
         out[i] = oracle_chksum_chain(states[i], &p, &l, 1);
     }
+}
+
+/* n chains (the C-ABI's aipstack_chksum_batch_chain): chain i = chunks
+ * [index[i], index[i+1]), chunk k = len[k] bytes at address addr[k], which is read at
+ * base + (addr[k] - addr_bias) (a host copy of device memory). states == NULL: state 0.
+ * flags bit 0 = the final checksum (IpChksumAccumulator::getChksum), else its NOT. */
+void oracle_batch_chain(const void *base, uint64_t addr_bias, const uint64_t *addr,
+                        const uint32_t *len, const uint64_t *index, const uint32_t *states,
+                        uint64_t n, uint16_t *out, uint32_t flags)
+{
+    const unsigned char *b = (const unsigned char *)base;
+    size_t cap = 0;
+    const void **ptrs = NULL;
+    size_t *lens = NULL;
+    for (uint64_t i = 0; i < n; i++) {
+        const size_t m = (size_t)(index[i + 1] - index[i]);
+        if (m > cap) {
+            cap = m * 2;
+            ptrs = (const void **)realloc((void *)ptrs, cap * sizeof *ptrs);
+            lens = (size_t *)realloc(lens, cap * sizeof *lens);
+        }
+        for (size_t k = 0; k < m; k++) {
+            ptrs[k] = b + (addr[index[i] + k] - addr_bias);
+            lens[k] = len[index[i] + k];
+        }
+        const uint16_t v = oracle_chksum_chain(states ? states[i] : 0u, ptrs, lens, m);
+        out[i] = (flags & 1u) ? v : (uint16_t)~v;
+    }
+    free((void *)ptrs);
+    free(lens);
 }

@@ -19,6 +19,9 @@ void oracle_batch_csr(const void *base, const uint64_t *offsets, uint64_t n,
                       uint16_t *out, uint32_t flags);
 void oracle_batch_seeded_csr(const void *base, const uint64_t *offsets,
                              const uint32_t *states, uint64_t n, uint16_t *out);
+void oracle_batch_chain(const void *base, uint64_t addr_bias, const uint64_t *addr,
+                        const uint32_t *len, const uint64_t *index, const uint32_t *states,
+                        uint64_t n, uint16_t *out, uint32_t flags);
 
 #ifdef __cplusplus
 }
