@@ -347,22 +347,153 @@ __device__ __forceinline__ void wave_sum_n(uint32_t (&v)[N]) {
 
 // No per-packet adjustment (see sum_lane_packets).
 struct NoMaskHook {
+    static constexpr bool kField = false;
     template <class PK>
     __device__ __forceinline__ void issue(int, int) {}
     template <class PK>
     __device__ __forceinline__ void apply(int, PK &, int) {}
+    __device__ __forceinline__ int row_field(int) { return -64; }
 };
 
-// The packets of a 64-packet chunk whose lanes are set in `todo` (wave-uniform), each
+// ---------------------------------------------------------------------------------
+// Row mode: packets of at most 16 aligned segments (<= 241 bytes at worst alignment),
+// four per wave instruction. Row r (lanes 16r..16r+15) holds one packet; lane k of the
+// row loads the packet's segment k with a per-lane address (its row's LaneMeta fetched
+// with ds_bpermute), masks its own head/tail bytes in VALU, and the 16 lanes of a row are
+// added by a 4-step row DPP scan. Same sum as the wave mode (an end-around-carry sum of
+// the masked little-endian dwords), at a quarter of the per-packet instructions.
+// ---------------------------------------------------------------------------------
+constexpr uint32_t kRowSegs = 16;
+
+// Row groups (of four packets) a kernel keeps in flight; 0 = no row mode. Per kernel
+// family, measured; overridable at build time for experiments.
+#ifndef AIPSTACK_ROWS_STRIDED
+#define AIPSTACK_ROWS_STRIDED 0
+#endif
+#ifndef AIPSTACK_ROWS_CSR
+#define AIPSTACK_ROWS_CSR 0
+#endif
+#ifndef AIPSTACK_ROWS_FRAMES
+#define AIPSTACK_ROWS_FRAMES 0
+#endif
+#ifndef AIPSTACK_ROWS_CHAIN
+#define AIPSTACK_ROWS_CHAIN 2
+#endif
+
+__device__ u32x4 g_zero_segment;  // a valid address for rows without a packet
+
+// Keep bytes [a, b) of a little-endian dword (a, b clamped to 0..4).
+__device__ __forceinline__ uint32_t dword_keep(int a, int b) {
+    a = min(max(a, 0), 4);
+    b = min(max(b, 0), 4);
+    return b > a ? ((0xFFFFFFFFu >> (32 - 8 * (b - a))) << (8 * a)) : 0u;
+}
+
+template <bool NT>
+__device__ __forceinline__ u32x4 load_lane_segment(uint64_t addr) {
+    const u32x4 *p = reinterpret_cast<const u32x4 *>(addr);
+    if constexpr (NT)
+        return __builtin_nontemporal_load(p);
+    else
+        return *p;
+}
+
+template <int kRowGroups, bool NT, class Hook>
+__device__ __forceinline__ uint32_t sum_row_packets(const LaneMeta &meta, uint64_t todo,
+                                                    int lane, uint32_t sums, Hook &hook) {
+    const int row = lane >> 4, k = lane & 15;
+    while (todo) {
+        u32x4 v[kRowGroups];
+        int jr[kRowGroups][4];
+        uint32_t packed_l[kRowGroups];
+        int src_l[kRowGroups];
+#pragma unroll
+        for (int g = 0; g < kRowGroups; ++g) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const bool valid = todo != 0;
+                jr[g][r] = valid ? (int)__builtin_ctzll(todo) : -1;
+                todo &= todo - 1;
+            }
+            int src = jr[g][0];
+            src = row == 1 ? jr[g][1] : src;
+            src = row == 2 ? jr[g][2] : src;
+            src = row == 3 ? jr[g][3] : src;
+            const int from = max(src, 0) << 2;
+            const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(from, (int)meta.a0_lo);
+            const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(from, (int)meta.a0_hi);
+            const uint32_t packed = (uint32_t)__builtin_amdgcn_ds_bpermute(from, (int)meta.packed);
+            const uint32_t nseg = packed >> 9;  // 1..16 for a row packet
+            const uint32_t kk = min((uint32_t)k, nseg - 1u);
+            const uint64_t addr = src >= 0
+                                      ? ((((uint64_t)hi << 32) | lo) + 16u * (uint64_t)kk)
+                                      : (uint64_t)(uintptr_t)&g_zero_segment;
+            v[g] = load_lane_segment<NT>(addr);
+            packed_l[g] = packed;
+            src_l[g] = src;
+        }
+        uint32_t part[kRowGroups];
+#pragma unroll
+        for (int g = 0; g < kRowGroups; ++g) {
+            const uint32_t packed = packed_l[g];
+            const int nseg = (int)(packed >> 9);
+            const bool in = src_l[g] >= 0 && k < nseg;
+            const int lo = k == 0 ? (int)(packed & 15u) : 0;
+            const int hi = k == nseg - 1 ? (int)((packed >> 4) & 31u) : 16;
+            int fx = -64;  // a 2-byte field summed as 0, bytes from the packet's A0
+            if constexpr (Hook::kField)
+                fx = hook.row_field(max(src_l[g], 0)) - 16 * k;
+            Eac a;
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                uint32_t m = dword_keep(lo - 4 * d, hi - 4 * d);
+                if constexpr (Hook::kField)
+                    m &= ~dword_keep(fx - 4 * d, fx + 2 - 4 * d);
+                a.add(v[g][d] & (in ? m : 0u));
+            }
+            const uint32_t s0 = a.finish();
+            part[g] = (s0 & 0xFFFFu) + (s0 >> 16);  // < 2^17; 16 lanes < 2^21
+        }
+        // row sums: 4-step row scan, interleaved across the groups; lane 16r+15 = row r
+#define AIPSTACK_ROW_STEP(ctrl)                                                             \
+    _Pragma("unroll") for (int g = 0; g < kRowGroups; ++g)                                   \
+        part[g] += __builtin_amdgcn_update_dpp(0u, part[g], ctrl, 0xF, 0xF, false);
+        AIPSTACK_ROW_STEP(0x111)
+        AIPSTACK_ROW_STEP(0x112)
+        AIPSTACK_ROW_STEP(0x114)
+        AIPSTACK_ROW_STEP(0x118)
+#undef AIPSTACK_ROW_STEP
+#pragma unroll
+        for (int g = 0; g < kRowGroups; ++g)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const uint32_t t = (uint32_t)__builtin_amdgcn_readlane(part[g], 16 * r + 15);
+                sums = (lane == jr[g][r]) ? t : sums;
+            }
+    }
+    return sums;
+}
+
+// The packets of a 64-packet chunk whose lanes are set in `todo` (wave-uniform): with
+// RG > 0, those of at most 16 segments four per wave instruction (sum_row_packets, RG
+// groups in flight); the others each
 // summed by the whole wave with P packets' loads in flight; lane j receives packet j's
 // exact halves-sum (< 2^24; 0 iff all its bytes are 0), other lanes 0. `meta` is the
 // per-lane LaneMeta. hook.issue(q, j) runs when packet j's loads are issued into slot q,
 // hook.apply(q, pk, lane) just before slot q is reduced (e.g. to mask a field).
-template <int U, int P, bool NT, class Hook>
+template <int U, int P, int RG, bool NT, class Hook>
 __device__ __forceinline__ uint32_t sum_lane_packets(const LaneMeta &meta, uint64_t todo,
                                                      int lane, uint32_t voff,
                                                      uint32_t not_lane0, Hook &hook) {
     uint32_t sums = 0;
+    if constexpr (RG > 0) {
+        const uint64_t small =
+            todo & __builtin_amdgcn_ballot_w64((meta.packed >> 9) <= kRowSegs);
+        if (small) {
+            sums = sum_row_packets<RG, NT>(meta, small, lane, sums, hook);
+            todo &= ~small;
+        }
+    }
     while (todo) {
         PacketLoad<U, NT> pk[P];
         int jq[P];

@@ -73,9 +73,10 @@ __global__ __launch_bounds__(kBlock) void chksum_batch_kernel(Desc desc, uint64_
         const LaneMeta meta = lane_meta(lS, lE);
         // lane j: exact halves-sum of packet j (< 2^24); empty packets are skipped
         NoMaskHook hook;
-        const uint32_t sums = sum_lane_packets<U, P, NT>(
-            meta, __builtin_amdgcn_ballot_w64((meta.packed >> 9) != 0), lane, voff, not_lane0,
-            hook);
+        const uint32_t sums =
+            sum_lane_packets<U, P, Desc::kCsr ? AIPSTACK_ROWS_CSR : AIPSTACK_ROWS_STRIDED, NT>(
+                meta, __builtin_amdgcn_ballot_w64((meta.packed >> 9) != 0), lane, voff,
+                not_lane0, hook);
         // Finalise the chunk's 64 results together (VALU, one packet per lane).
         uint32_t r = fold16(sums);
         if ((meta.packed & 1u) == 0)  // S even (A0 is 16-aligned, so S & 1 = rel_s & 1)
@@ -200,7 +201,7 @@ __global__ __launch_bounds__(kBlock) void chksum_chain_kernel(
             // chunk sums, one per wave
             const LaneMeta meta = lane_meta(a, a + (uint64_t)l);
             NoMaskHook hook;
-            const uint32_t sums = sum_lane_packets<U, P, NT>(
+            const uint32_t sums = sum_lane_packets<U, P, AIPSTACK_ROWS_CHAIN, NT>(
                 meta, __builtin_amdgcn_ballot_w64(valid && (meta.packed >> 9) != 0), lane, voff,
                 not_lane0, hook);
             uint32_t r = fold16(sums);

@@ -193,6 +193,7 @@ __device__ __forceinline__ FrameLane parse_lane(const u32x4 (&seg)[kHdrSegs], ui
 // (< 32: lanes 0-2 of slot 0) is read per frame at issue, with its not-pair mask.
 template <int P>
 struct TxFieldHook {
+    static constexpr bool kField = true;
     uint32_t fx_lane;  // FrameLane::fx of this lane's frame
     uint32_t fxq[P];
     u32x4 xmq[P];
@@ -200,6 +201,10 @@ struct TxFieldHook {
     __device__ __forceinline__ void issue(int q, int j) {
         fxq[q] = (uint32_t)__builtin_amdgcn_readlane(fx_lane, j);
         xmq[q] = load_mask(kMaskNotPair[fxq[q] & 15u]);
+    }
+    // row mode: the field offset of the frame in lane `src`
+    __device__ __forceinline__ int row_field(int src) {
+        return __builtin_amdgcn_ds_bpermute(src << 2, (int)fx_lane);
     }
     template <class PK>
     __device__ __forceinline__ void apply(int q, PK &pk, int lane) {
@@ -264,10 +269,12 @@ __global__ __launch_bounds__(kBlock) void frame_kernel(CsrDesc desc, uint64_t n,
         if (TX) {
             TxFieldHook<P> hook;
             hook.fx_lane = fl.fx;
-            sums = sum_lane_packets<U, P, NT>(meta, todo, lane, voff, not_lane0, hook);
+            sums = sum_lane_packets<U, P, AIPSTACK_ROWS_FRAMES, NT>(meta, todo, lane, voff,
+                                                                  not_lane0, hook);
         } else {
             NoMaskHook hook;
-            sums = sum_lane_packets<U, P, NT>(meta, todo, lane, voff, not_lane0, hook);
+            sums = sum_lane_packets<U, P, AIPSTACK_ROWS_FRAMES, NT>(meta, todo, lane, voff,
+                                                                  not_lane0, hook);
         }
 
         // (D) per-lane finish
