@@ -23,26 +23,14 @@
 namespace aipstack_amd {
 namespace {
 
-// Frame bytes [0, 97) cover every header field the kernels read from any start alignment:
-// 14 (Ethernet) + 60 (IPv4 with options) + 8 (UDP header) + 15 (S & 15).
-constexpr int kHdrSegs = 7;
+// Frame bytes [0, 82) hold every header field the kernels read: 14 (Ethernet) + 60 (IPv4
+// with options) + 8 (UDP header); from A0 = S & ~15 that is at most 97 bytes. The header
+// pass loads from A0 up to the next 32-byte boundary past them (7 or 8 segments), so the
+// L4 pass starts on a fresh 32-byte sector and no sector is fetched twice.
+constexpr int kHdrSegs = 8;
 constexpr int kHdrDwords = 21;  // frame bytes [0, 84) realigned to the frame start
+constexpr uint32_t kHdrNeed = 97;
 
-// Zero bytes b and b+1 (b+1 < 16) of a 16-byte segment, as four dwords.
-constexpr uint32_t not_pair_dword(int b, int d) {
-    uint32_t m = 0xFFFFFFFFu;
-    for (int i = 0; i < 4; ++i)
-        if (4 * d + i == b || 4 * d + i == b + 1) m &= ~(0xFFu << (8 * i));
-    return m;
-}
-#define AIPSTACK_NOT_PAIR(b) \
-    {not_pair_dword(b, 0), not_pair_dword(b, 1), not_pair_dword(b, 2), not_pair_dword(b, 3)}
-__constant__ uint32_t kMaskNotPair[16][4] = {
-    AIPSTACK_NOT_PAIR(0),  AIPSTACK_NOT_PAIR(1),  AIPSTACK_NOT_PAIR(2),  AIPSTACK_NOT_PAIR(3),
-    AIPSTACK_NOT_PAIR(4),  AIPSTACK_NOT_PAIR(5),  AIPSTACK_NOT_PAIR(6),  AIPSTACK_NOT_PAIR(7),
-    AIPSTACK_NOT_PAIR(8),  AIPSTACK_NOT_PAIR(9),  AIPSTACK_NOT_PAIR(10), AIPSTACK_NOT_PAIR(11),
-    AIPSTACK_NOT_PAIR(12), AIPSTACK_NOT_PAIR(13), AIPSTACK_NOT_PAIR(14), AIPSTACK_NOT_PAIR(15)};
-#undef AIPSTACK_NOT_PAIR
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) {
     return __builtin_bswap32(x);
@@ -66,10 +54,12 @@ __device__ __forceinline__ void store_be16(uint64_t addr, uint32_t v) {
 
 // What the header pass decides for one frame (lane j <-> frame j of the chunk).
 struct FrameLane {
-    uint64_t l4s, l4e;  // the bytes the L4 checksum covers; l4s == l4e: no L4 sum
+    uint64_t l4s;       // first byte the L4 checksum covers (its parity orients the sum)
+    uint64_t cs, ce;    // the L4 bytes past the header pass's blocks: [cs, ce), maybe empty
+    uint32_t part;      // ones'-complement sum of the L4 bytes inside the header blocks
+    bool l4;            // an L4 checksum is computed
     uint32_t words;     // IpChksumAccumulator words added before them (pseudo-header)
     uint32_t hchk;      // IPv4 header checksum over the header (Tx: with the field as 0)
-    uint32_t fx;        // Tx: L4 checksum field, bytes from (l4s & ~15)
     int fld;            // Tx: L4 checksum field, bytes from the frame start
     int pre;            // the verdict / status when no L4 sum decides it
     bool ip_ok;         // the IPv4 header parsed (Tx writes its checksum)
@@ -84,7 +74,7 @@ struct FrameLane {
 // udp/IpUdpProto.h:164-179, ip/IpStack.h:1164-1190).
 template <bool TX>
 __device__ __forceinline__ FrameLane parse_lane(const u32x4 (&seg)[kHdrSegs], uint64_t S,
-                                                int len) {
+                                                int len, uint32_t hb_end) {
     uint32_t raw[4 * kHdrSegs];
 #pragma unroll
     for (int i = 0; i < kHdrSegs; ++i)
@@ -102,9 +92,10 @@ __device__ __forceinline__ FrameLane parse_lane(const u32x4 (&seg)[kHdrSegs], ui
     for (int i = 0; i < kHdrDwords; ++i) f[i] = __builtin_amdgcn_alignbyte(t2[i + 1], t2[i], rs & 3u);
 
     FrameLane r;
-    r.l4s = r.l4e = S;
+    r.l4s = r.cs = r.ce = S;
+    r.part = 0;
+    r.l4 = false;
     r.words = 0;
-    r.fx = 0;
     r.fld = 0;
     r.udp = false;
     r.ip_ok = false;
@@ -181,39 +172,29 @@ __device__ __forceinline__ FrameLane parse_lane(const u32x4 (&seg)[kHdrSegs], ui
     }
     if (l4len >= 0) {
         r.pre = AIPSTACK_RX_ACCEPT;
+        r.l4 = true;
         r.l4s = S + (uint64_t)dg;
-        r.l4e = r.l4s + (uint64_t)l4len;
         r.fld = dg + fo;
-        r.fx = ((uint32_t)r.l4s & 15u) + (uint32_t)fo;  // < 32: lanes 0-2 of slot 0
+        // L4 bytes inside the loaded blocks [A0, A0 + hb_end): summed here, from the aligned
+        // dwords (little-endian halves at even absolute addresses, as the L4 pass sums); the
+        // rest, [A0 + hb_end, end), by the L4 pass. For Tx the checksum field (always in
+        // the header blocks: fld + 2 <= 92) is summed as 0.
+        const int lo = (int)rs + dg, hi = (int)rs + dg + l4len;
+        const int fx = TX ? (int)rs + r.fld : -64;
+        Eac ps;
+#pragma unroll
+        for (int i = 0; i < 4 * kHdrSegs; ++i) {
+            uint32_t m = dword_keep(lo - 4 * i, min(hi, (int)hb_end) - 4 * i);
+            if (TX) m &= ~dword_keep(fx - 4 * i, fx + 2 - 4 * i);
+            ps.add(raw[i] & m);
+        }
+        r.part = ps.finish();
+        const uint64_t a0 = S & ~(uint64_t)15;
+        r.cs = a0 + hb_end;
+        r.ce = hi > (int)hb_end ? a0 + (uint64_t)hi : r.cs;
     }
     return r;
 }
-
-// Tx: the L4 checksum field is summed as 0. Its offset from the L4 range's aligned base
-// (< 32: lanes 0-2 of slot 0) is read per frame at issue, with its not-pair mask.
-template <int P>
-struct TxFieldHook {
-    static constexpr bool kField = true;
-    uint32_t fx_lane;  // FrameLane::fx of this lane's frame
-    uint32_t fxq[P];
-    u32x4 xmq[P];
-    template <class PK>
-    __device__ __forceinline__ void issue(int q, int j) {
-        fxq[q] = (uint32_t)__builtin_amdgcn_readlane(fx_lane, j);
-        xmq[q] = load_mask(kMaskNotPair[fxq[q] & 15u]);
-    }
-    // row mode: the field offset of the frame in lane `src`
-    __device__ __forceinline__ int row_field(int src) {
-        return __builtin_amdgcn_ds_bpermute(src << 2, (int)fx_lane);
-    }
-    template <class PK>
-    __device__ __forceinline__ void apply(int q, PK &pk, int lane) {
-        const int fx = (int)fxq[q];
-        apply_mask(pk.v[0], xmq[q], lane == (fx >> 4) ? 0u : ~0u);
-        // a field straddling two segments: byte 0 of the next one
-        pk.v[0][0] &= ((fx & 15) == 15 && lane == (fx >> 4) + 1) ? ~0xFFu : ~0u;
-    }
-};
 
 // Rx verify / Tx fill of n frames at CSR offsets. A wave walks 64-frame chunks:
 //   (B) lane j loads frame j's first 112 aligned bytes (one buffer descriptor per chunk)
@@ -252,34 +233,30 @@ __global__ __launch_bounds__(kBlock) void frame_kernel(CsrDesc desc, uint64_t n,
                               ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(S >> 32)) << 32);
         const uint64_t span = ((desc.base + chunk.end_off + 15u) & ~(uint64_t)15) - base;
         const uint32_t hrec = __builtin_amdgcn_readfirstlane(
-            span > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)span);  // uniform: SGPR descriptor
+            span > 0xFFFFFF00ull ? 0xFFFFFF00u : (uint32_t)span);  // uniform: SGPR descriptor
         const __amdgpu_buffer_rsrc_t hrsrc = __builtin_amdgcn_make_buffer_rsrc(
             reinterpret_cast<void *>(base), (short)0, hrec, 0x00020000);
         const uint32_t hoff = (uint32_t)((S & ~(uint64_t)15) - base);
+        // this lane's blocks: A0 up to the first 32-byte boundary past the header bytes
+        // (A0 % 32 + 15 + 97 + 31 < 160, so at most 128 bytes = kHdrSegs segments)
+        const uint32_t a0_32 = (uint32_t)S & 16u;
+        const uint32_t hb_end = ((a0_32 + ((uint32_t)S & 15u) + kHdrNeed + 31u) & ~31u) - a0_32;
         u32x4 seg[kHdrSegs];
 #pragma unroll
-        for (int i = 0; i < kHdrSegs; ++i) seg[i] = load_segment<false>(hrsrc, hoff, 16u * i);
-        const FrameLane fl = parse_lane<TX>(seg, S, len);
-        const bool need = fl.l4e != fl.l4s;
-        const LaneMeta meta = lane_meta(fl.l4s, fl.l4e);
+        for (int i = 0; i < kHdrSegs; ++i)  // past hb_end: out of range, reads 0, no traffic
+            seg[i] = load_segment<false>(hrsrc, 16u * i < hb_end ? hoff + 16u * i : 0xFFFFFFF0u, 0u);
+        const FrameLane fl = parse_lane<TX>(seg, S, len, hb_end);
+        const bool need = fl.ce != fl.cs;
+        const LaneMeta meta = lane_meta(fl.cs, fl.ce);
 
-        // (C) L4 sums, one frame per wave, P frames' loads in flight
-        uint32_t sums;
-        const uint64_t todo = __builtin_amdgcn_ballot_w64(need);
-        if (TX) {
-            TxFieldHook<P> hook;
-            hook.fx_lane = fl.fx;
-            sums = sum_lane_packets<U, P, AIPSTACK_ROWS_FRAMES, NT>(meta, todo, lane, voff,
-                                                                  not_lane0, hook);
-        } else {
-            NoMaskHook hook;
-            sums = sum_lane_packets<U, P, AIPSTACK_ROWS_FRAMES, NT>(meta, todo, lane, voff,
-                                                                  not_lane0, hook);
-        }
+        // (C) the remaining L4 bytes, one frame per wave, P frames' loads in flight
+        NoMaskHook hook;
+        const uint32_t sums = sum_lane_packets<U, P, AIPSTACK_ROWS_FRAMES, NT>(
+            meta, __builtin_amdgcn_ballot_w64(need), lane, voff, not_lane0, hook);
 
-        // (D) per-lane finish
-        uint32_t r = fold16(sums);
-        if ((meta.packed & 1u) == 0)  // L4 start even: little-endian pairing -> big-endian
+        // (D) per-lane finish: both parts (< 2^24 + 2^17), folded, oriented by the L4 start
+        uint32_t r = fold16(sums + fold16(fl.part));
+        if ((fl.l4s & 1u) == 0)  // L4 start even: little-endian pairing -> big-endian
             r = bswap16(r);
         const uint64_t m = (uint64_t)fl.words + r;
         uint32_t chk = (~fold16((uint32_t)m + (uint32_t)(m >> 32))) & 0xFFFFu;
@@ -287,11 +264,11 @@ __global__ __launch_bounds__(kBlock) void frame_kernel(CsrDesc desc, uint64_t n,
         if (TX) {
             if (fl.ip_ok)
                 store_be16(S + 24, fl.hchk);
-            if (need) {
+            if (fl.l4) {
                 if (fl.udp && chk == 0) chk = 0xFFFFu;              // udp/IpUdpProto.h:176-178
                 store_be16(S + (uint64_t)fl.fld, chk);
             }
-        } else if (need) {
+        } else if (fl.l4) {
             v = chk == 0 ? AIPSTACK_RX_ACCEPT : AIPSTACK_RX_DROP_L4_CHKSUM;
         }
         if (lane < cnt)
