@@ -36,6 +36,15 @@ __device__ __forceinline__ uint32_t settle(uint32_t x) {
     return y;
 }
 
+// Lane i gets lane i+1's v; lane 63 gets `last`. The choice is made on the source side
+// (lane 0 supplies `last`) and the ds_bpermute always runs on the full wave. Written as
+// `lane == 63 ? last : __shfl_down(v, 1)`, LLVM may run the permute under an exec mask
+// without lane 63 -- and a permute that reads an inactive lane gets garbage.
+__device__ __forceinline__ uint32_t from_next_lane(uint32_t v, uint32_t last, int lane) {
+    const uint32_t src = lane == 0 ? last : v;
+    return (uint32_t)__builtin_amdgcn_ds_bpermute(((lane + 1) & 63) << 2, (int)src);
+}
+
 struct StridedDesc {
     static constexpr bool kCsr = false;
     uint64_t base;    // absolute address of packet 0
@@ -60,6 +69,8 @@ struct StridedDesc {
         E = S + len;
     }
     __device__ __forceinline__ uint32_t lane_seed(const Chunk &) const { return 0; }
+    // Host: every chunk's packets lie back to back (stream mode always applies).
+    bool back_to_back() const { return stride == len && len < (1u << 17); }
 };
 
 struct CsrDesc {
@@ -95,13 +106,14 @@ struct CsrDesc {
     // This lane's packet as [S, E): its offset and the next lane's (lane 63: end_off).
     __device__ __forceinline__ void lane_bounds(const Chunk &c, int lane, uint64_t &S,
                                                 uint64_t &E) const {
-        const uint32_t nlo = (uint32_t)__shfl_down((int)c.off_lo, 1);
-        const uint32_t nhi = (uint32_t)__shfl_down((int)c.off_hi, 1);
-        const uint64_t next = lane == kWave - 1 ? c.end_off : (((uint64_t)nhi << 32) | nlo);
+        const uint32_t nlo = from_next_lane(c.off_lo, (uint32_t)c.end_off, lane);
+        const uint32_t nhi = from_next_lane(c.off_hi, (uint32_t)(c.end_off >> 32), lane);
+        const uint64_t next = ((uint64_t)nhi << 32) | nlo;
         S = base + (((uint64_t)c.off_hi << 32) | c.off_lo);
         E = base + next;
     }
     __device__ __forceinline__ uint32_t lane_seed(const Chunk &) const { return 0; }
+    bool back_to_back() const { return false; }  // known per chunk only
 };
 
 struct SeededCsrDesc : CsrDesc {
@@ -521,6 +533,132 @@ __device__ __forceinline__ uint32_t sum_lane_packets(const LaneMeta &meta, uint6
         for (int q = 0; q < P; ++q) sums = (lane == jq[q]) ? part[q] : sums;
     }
     return sums;
+}
+
+// ---------------------------------------------------------------------------------
+// Stream mode: a chunk whose 64 packets lie back to back in memory (packet j ends where
+// packet j+1 starts: every CSR batch with non-decreasing offsets, strided batches with
+// stride == len) is read as ONE contiguous byte run, 1 KiB per wave instruction, with no
+// per-packet loads, masks or reductions. Packet sums come from prefix differences:
+//
+//   H(x)  = exact sum of the little-endian 16-bit halves of the bytes [A, x), A = S_0 & ~15
+//           (bytes read through their aligned dwords, the bytes at or above x as 0);
+//   sum_j = H(S_{j+1}) - H(S_j) = the exact halves-sum of packet j's masked dwords.
+//
+// The halves-sum (v_sad_u16 against 0 adds a dword's two halves, one VALU op) is exact,
+// so sum_j is 0 iff every byte of packet j is 0 and is congruent mod 0xFFFF to the
+// little-endian ones'-complement sum: the same value the wave mode produces, folded and
+// oriented identically. A packet of at most 2^17 - 1 bytes has sum_j < 2^32, so H is
+// kept modulo 2^32 (wrap-around subtraction stays exact).
+//
+// Per 1 KiB window: lane k loads segment k (buffer_load_dwordx4, range-checked to the
+// chunk), adds its halves (4 v_sad_u16), and an inclusive DPP scan gives each segment's
+// prefix. Lane j evaluates H(S_j) in the window holding S_j: the prefix before S_j's
+// segment and that segment's dwords (ds_bpermute from the lane that loaded it), masked
+// below S_j. All 64 boundaries are evaluated in parallel, so the cost per window does
+// not depend on how many packets it holds.
+// ---------------------------------------------------------------------------------
+constexpr uint32_t kStreamMaxLen = (1u << 17) - 1u;
+
+__device__ __forceinline__ uint32_t halves(uint32_t x, uint32_t acc) {
+    return __builtin_amdgcn_sad_u16(x, 0u, acc);  // (x & 0xFFFF) + (x >> 16) + acc
+}
+
+// Inclusive prefix sum over the 64 lanes (row scan + row broadcasts).
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xA, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xC, 0xF, false);
+    return v;
+}
+
+// Whether the chunk can take stream mode (wave-uniform): lanes < cnt hold packets
+// [S, E) with E - S <= kStreamMaxLen, and each packet ends where the next one starts.
+__device__ __forceinline__ bool stream_ok(uint64_t S, uint64_t E, int lane, int cnt) {
+    const uint32_t s_lo = (uint32_t)S, s_hi = (uint32_t)(S >> 32);
+    const uint64_t next = ((uint64_t)from_next_lane(s_hi, 0u, lane) << 32) |
+                          from_next_lane(s_lo, 0u, lane);
+    const bool bad = lane < cnt && ((E - S) > kStreamMaxLen || (lane + 1 < cnt && E != next));
+    return __builtin_amdgcn_ballot_w64(bad) == 0;
+}
+
+// Stream mode for one chunk (stream_ok). Lane j < cnt holds packet j = [S, E); returns
+// lane j's exact halves-sum (0 on lanes >= cnt). U windows' loads are issued together;
+// windows past the chunk read zeros (range check) and change nothing.
+template <int U, bool NT>
+__device__ __forceinline__ uint32_t sum_stream_chunk(uint64_t S, uint64_t E, int lane, int cnt,
+                                                     uint32_t voff) {
+    // X1 = end of the chunk's last packet; lanes past the batch sit at X1 (empty)
+    const int lastl = cnt - 1;
+    const uint64_t X1 =
+        ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(E >> 32), lastl) << 32) |
+        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)E, lastl);
+    if (lane >= cnt) S = X1;
+    const uint64_t S0 =
+        ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(S >> 32)) << 32) |
+        (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)S);
+    const uint64_t A = S0 & ~(uint64_t)15;
+    const uint32_t span = (uint32_t)(X1 - A);  // <= 64 * 2^17 + 15
+    const uint32_t nseg = (span + 15u) >> 4;
+    const uint32_t nwin = (nseg + (uint32_t)kWave - 1u) >> 6;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void *>(A), (short)0, (int)(nseg * 16u), 0x00020000);
+    // this lane's boundary S: its window, owner lane (x4 for ds_bpermute), masks below it
+    const uint32_t boff = (uint32_t)(S - A);
+    const uint32_t bwin = boff >> 10;
+    const int bsrc = (int)(((boff >> 4) & 63u) << 2);
+    const int bt = (int)(boff & 15u);
+    uint32_t below[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) below[d] = dword_keep(0, bt - 4 * d);
+    // X1's segment (the last one; past X1 it holds the next chunk's bytes): window, lane
+    const uint32_t xt = span & 15u;
+    const uint32_t xwin = (nseg - 1u) >> 6;
+    const int xlane = (int)((nseg - 1u) & 63u);
+    uint32_t xabove[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) xabove[d] = ~dword_keep(0, (int)xt - 4 * d);
+
+    uint32_t carry = 0;  // H(start of the current window), mod 2^32
+    uint32_t hb = 0;     // H(S) once its window has passed
+    uint32_t x_hi = 0;   // halves of the last segment's bytes at or above X1
+    for (uint32_t w = 0; w < nwin; w += U) {
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            v[u] = load_segment<NT>(rsrc, voff, (w + (uint32_t)u) * 1024u);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t wu = w + (uint32_t)u;
+            const uint32_t s =
+                halves(v[u][0], halves(v[u][1], halves(v[u][2], halves(v[u][3], 0u))));
+            const uint32_t incl = wave_incl_scan(s);
+            const uint32_t excl = incl - s;
+            if (__builtin_amdgcn_ballot_w64(bwin == wu)) {  // boundaries in this window
+                uint32_t part = (uint32_t)__builtin_amdgcn_ds_bpermute(bsrc, (int)excl);
+#pragma unroll
+                for (int d = 0; d < 4; ++d)
+                    part = halves(
+                        (uint32_t)__builtin_amdgcn_ds_bpermute(bsrc, (int)v[u][d]) & below[d],
+                        part);
+                if (bwin == wu) hb = carry + part;
+            }
+            if (wu == xwin && xt != 0) {  // wave-uniform: X1 falls inside this segment
+                uint32_t h = 0;
+#pragma unroll
+                for (int d = 0; d < 4; ++d) h = halves(v[u][d] & xabove[d], h);
+                x_hi = (uint32_t)__builtin_amdgcn_readlane((int)h, xlane);
+            }
+            carry += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        }
+    }
+    const uint32_t hx = carry - x_hi;  // H(X1)
+    if (S == X1) hb = hx;              // covers a boundary at X1 past the last window
+    const uint32_t hn = from_next_lane(hb, hx, lane);  // H(S_{j+1}); lane 63: H(X1)
+    return lane < cnt ? hn - hb : 0u;
 }
 
 // Sum over the 64 lanes (DPP row scan + row broadcasts); result valid in lane 63,

@@ -25,6 +25,11 @@
 //     byte. So the folded sum is byte-swapped iff S is even. A byte swap is x*256 mod
 //     0xFFFF and folding never turns a nonzero sum into 0, so the 0x0000-vs-0xFFFF
 //     representation matches the reference exactly (0 iff every byte is 0).
+//   * Stream mode (chksum_device.h): a chunk whose packets lie back to back (CSR with
+//     non-decreasing offsets, stride == len) skips the per-packet work entirely. The wave
+//     reads the chunk as one contiguous run, 1 KiB per instruction, keeps an exact prefix
+//     of 16-bit-half sums (v_sad_u16 + DPP scan), and each packet's sum is the difference
+//     of the prefixes at its two ends -- the same exact halves-sum as above.
 //   * HBM-bound integer reduction: no MFMA, no LDS (the cross-lane sum is DPP).
 
 #include <hip/hip_runtime.h>
@@ -45,7 +50,7 @@ namespace {
 // ---------------------------------------------------------------------------------
 // The kernel: wave w handles 64-packet chunks [w*cpw, (w+1)*cpw).
 // ---------------------------------------------------------------------------------
-template <class Desc, int U, int P, bool NT, bool SEEDED>
+template <class Desc, int U, int P, bool NT, bool SEEDED, int SU>
 __global__ __launch_bounds__(kBlock) void chksum_batch_kernel(Desc desc, uint64_t n,
                                                               uint32_t chunks_per_wave,
                                                               uint16_t *__restrict__ out,
@@ -70,16 +75,27 @@ __global__ __launch_bounds__(kBlock) void chksum_batch_kernel(Desc desc, uint64_
         uint64_t lS, lE;
         desc.lane_bounds(chunk, lane, lS, lE);
         if (lane >= cnt) lE = lS;  // past the batch: empty
-        const LaneMeta meta = lane_meta(lS, lE);
-        // lane j: exact halves-sum of packet j (< 2^24); empty packets are skipped
-        NoMaskHook hook;
-        const uint32_t sums =
-            sum_lane_packets<U, P, Desc::kCsr ? AIPSTACK_ROWS_CSR : AIPSTACK_ROWS_STRIDED, NT>(
-                meta, __builtin_amdgcn_ballot_w64((meta.packed >> 9) != 0), lane, voff,
-                not_lane0, hook);
+        // lane j: exact halves-sum of packet j (0 iff all its bytes are 0)
+        uint32_t sums = 0;
+        bool streamed = false;
+        if constexpr (SU > 0) {
+            if (stream_ok(lS, lE, lane, cnt)) {
+                // back-to-back packets: the chunk read as one contiguous run
+                sums = sum_stream_chunk<SU, NT>(lS, lE, lane, cnt, voff);
+                streamed = true;
+            }
+        }
+        if (!streamed) {
+            // one packet per wave, P in flight; empty packets are skipped
+            const LaneMeta meta = lane_meta(lS, lE);
+            NoMaskHook hook;
+            sums = sum_lane_packets<U, P, Desc::kCsr ? AIPSTACK_ROWS_CSR : AIPSTACK_ROWS_STRIDED,
+                                    NT>(meta, __builtin_amdgcn_ballot_w64((meta.packed >> 9) != 0),
+                                        lane, voff, not_lane0, hook);
+        }
         // Finalise the chunk's 64 results together (VALU, one packet per lane).
         uint32_t r = fold16(sums);
-        if ((meta.packed & 1u) == 0)  // S even (A0 is 16-aligned, so S & 1 = rel_s & 1)
+        if ((lS & 1u) == 0)  // S even
             r = bswap16(r);  // little-endian pairing -> the reference's big-endian words
         if constexpr (SEEDED) {
             // IpChksumAccumulator(State): m_sum = state; m_sum += r with end-around
@@ -241,6 +257,8 @@ struct Tuning {
     std::atomic<int> frames{0};           // frames in flight per wave (frame kernels)
     std::atomic<int> nontemporal{1};      // 1 = nontemporal (streaming) loads: every byte is
                                           // read once; measured faster on configs A and B
+    std::atomic<int> stream{0};           // stream mode for back-to-back chunks: windows
+                                          // issued together (2, 4, 8); -1 = off
 
     Tuning() {
         auto env = [](const char *k, std::atomic<int> &v) {
@@ -252,6 +270,7 @@ struct Tuning {
         env("AIPSTACK_CHKSUM_PACKETS", packets);
         env("AIPSTACK_CHKSUM_NT", nontemporal);
         env("AIPSTACK_CHKSUM_FRAMES", frames);
+        env("AIPSTACK_CHKSUM_STREAM", stream);
     }
 };
 
@@ -284,7 +303,18 @@ int pick_packets(int u, bool csr) {
     return u <= 2 ? 8 : 1;
 }
 
-template <class Desc, int U, int P, bool NT, bool SEEDED>
+// SU: stream-mode windows issued together (0 = stream mode off). Measured (tools/sweep.py,
+// profiles/r01e): 1500/9000 B strided best at 2 (a wave streams 94-141 KiB per chunk, and
+// occupancy covers the latency), mixed CSR at 8 (stream 2 / 4 / 8 / off: 262 / 258 / 255 /
+// 266 us on config C).
+int pick_stream(bool csr) {
+    const int t = tuning().stream.load(std::memory_order_relaxed);
+    if (t < 0) return 0;
+    if (t == 2 || t == 4 || t == 8) return t;
+    return csr ? 8 : 2;
+}
+
+template <class Desc, int U, int P, bool NT, bool SEEDED, int SU>
 int launch_k(const Desc &desc, uint64_t n, uint16_t *d_out, uint32_t flags,
              hipStream_t stream) {
     const uint64_t nchunks = (n + kWave - 1) / kWave;
@@ -301,27 +331,40 @@ int launch_k(const Desc &desc, uint64_t n, uint16_t *d_out, uint32_t flags,
     const uint64_t waves = (nchunks + cpw - 1) / cpw;
     const uint64_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
     if (blocks > 0x7FFFFFFFull || cpw > 0xFFFFFFFFull) return AIPSTACK_CHKSUM_EINVAL;
-    hipLaunchKernelGGL((chksum_batch_kernel<Desc, U, P, NT, SEEDED>), dim3((unsigned)blocks),
+    hipLaunchKernelGGL((chksum_batch_kernel<Desc, U, P, NT, SEEDED, SU>), dim3((unsigned)blocks),
                        dim3(kBlock), 0, stream, desc, n, (uint32_t)cpw, d_out, flags);
     return check_hip(hipGetLastError());
+}
+
+template <class Desc, int U, int P, bool SEEDED>
+int launch_s(const Desc &desc, uint64_t n, uint16_t *d_out, uint32_t flags,
+             hipStream_t stream) {
+    if (tuning().nontemporal.load(std::memory_order_relaxed) == 0)  // sweeps only
+        return launch_k<Desc, U, P, false, SEEDED, 0>(desc, n, d_out, flags, stream);
+    switch (pick_stream(Desc::kCsr)) {
+        case 0: return launch_k<Desc, U, P, true, SEEDED, 0>(desc, n, d_out, flags, stream);
+        case 2: return launch_k<Desc, U, P, true, SEEDED, 2>(desc, n, d_out, flags, stream);
+        case 8: return launch_k<Desc, U, P, true, SEEDED, 8>(desc, n, d_out, flags, stream);
+        default: return launch_k<Desc, U, P, true, SEEDED, 4>(desc, n, d_out, flags, stream);
+    }
 }
 
 template <class Desc, int U, bool SEEDED>
 int launch_u(const Desc &desc, uint64_t n, uint16_t *d_out, uint32_t flags,
              hipStream_t stream) {
-    const bool nt = tuning().nontemporal.load(std::memory_order_relaxed) != 0;
-    const int p = pick_packets(U, Desc::kCsr);
-#define AIPSTACK_LAUNCH_P(PP)                                                               \
-    case PP:                                                                                \
-        return nt ? launch_k<Desc, U, PP, true, SEEDED>(desc, n, d_out, flags, stream)      \
-                  : launch_k<Desc, U, PP, false, SEEDED>(desc, n, d_out, flags, stream);
+    int p = pick_packets(U, Desc::kCsr);
+    // Every chunk takes stream mode: the per-packet path is never run, so give it the
+    // fewest registers (the kernel's occupancy is set by the larger of the two paths).
+    if (desc.back_to_back() && pick_stream(Desc::kCsr) > 0 &&
+        tuning().nontemporal.load(std::memory_order_relaxed) != 0 &&
+        tuning().packets.load(std::memory_order_relaxed) == 0)
+        p = 1;
     switch (p) {
-        AIPSTACK_LAUNCH_P(1)
-        AIPSTACK_LAUNCH_P(2)
-        AIPSTACK_LAUNCH_P(4)
-        AIPSTACK_LAUNCH_P(8)
+        case 1: return launch_s<Desc, U, 1, SEEDED>(desc, n, d_out, flags, stream);
+        case 2: return launch_s<Desc, U, 2, SEEDED>(desc, n, d_out, flags, stream);
+        case 4: return launch_s<Desc, U, 4, SEEDED>(desc, n, d_out, flags, stream);
+        case 8: return launch_s<Desc, U, 8, SEEDED>(desc, n, d_out, flags, stream);
     }
-#undef AIPSTACK_LAUNCH_P
     return AIPSTACK_CHKSUM_EINVAL;
 }
 
@@ -415,6 +458,7 @@ extern "C" int aipstack_chksum_tune(const char *key, int value) {
     else if (!std::strcmp(key, "packets")) t.packets = value;
     else if (!std::strcmp(key, "nontemporal")) t.nontemporal = value;
     else if (!std::strcmp(key, "frames")) t.frames = value;
+    else if (!std::strcmp(key, "stream")) t.stream = value;
     else return AIPSTACK_CHKSUM_EINVAL;
     return AIPSTACK_CHKSUM_OK;
 }

@@ -152,6 +152,97 @@ def test_lengths(oracle, plen):
     assert np.array_equal(got, want)
 
 
+def _tune(key, value):
+    from aipstack_amd import _lib
+    assert _lib.load().aipstack_chksum_tune(key.encode(), value) == A.AIPSTACK_CHKSUM_OK
+
+
+@pytest.fixture
+def stream_mode():
+    """Yields a setter for the stream-mode tunable; restores automatic afterwards."""
+    yield lambda v: _tune("stream", v)
+    _tune("stream", 0)
+
+
+@pytest.mark.parametrize("su", [2, 4, 8])
+@pytest.mark.parametrize("plen", [0, 1, 2, 3, 15, 16, 17, 31, 33, 1023, 1024, 1025, 1500, 2033,
+                                  9000, 65535])
+def test_stream_mode_back_to_back_strided(oracle, stream_mode, plen, su):
+    """stride == len: every chunk is read as one contiguous run (stream mode)."""
+    stream_mode(su)
+    for n, base in ((1, 0), (63, 3), (65, 1), (300, 13)):
+        if plen * n > 64 << 20:
+            n = 70
+        buf = torch.empty(n * max(plen, 1) + 64, dtype=torch.uint8, device=DEV)
+        synth.fill_device(buf, plen + n)
+        got = _np(A.chksum_batch_strided(buf, plen, plen, n, byte_offset=base))
+        want = oracle.batch_strided(_np(buf), plen, plen, n, base_off=base)
+        assert np.array_equal(got, want), (plen, n, base, np.nonzero(got != want)[0][:8])
+
+
+@pytest.mark.parametrize("su", [-1, 2, 4, 8])
+def test_stream_mode_csr_tiny_and_mixed(oracle, stream_mode, su):
+    """Back-to-back CSR packets from 0 to 65535 bytes, many per 16-byte segment, odd starts,
+    all-0x00 / all-0xFF packets; stream mode (su > 0) and per-packet mode (su = -1)."""
+    stream_mode(su)
+    rng = np.random.default_rng(17)
+    for choice in ([0, 0, 1, 2, 3, 5, 7, 16, 17, 31], [0, 64, 65, 1499, 1500, 9000, 65535],
+                   list(range(0, 200))):
+        n = 20000 if max(choice) < 10000 else 3000
+        lens = rng.choice(choice, size=n)
+        off = np.zeros(n + 1, dtype=np.int64)
+        np.cumsum(lens, out=off[1:])
+        off += 7
+        buf = torch.empty(int(off[-1]) + 64, dtype=torch.uint8, device=DEV)
+        synth.fill_device(buf, n + 5)
+        host = _np(buf)
+        for j in range(0, n, 13):
+            host[off[j]:off[j + 1]] = 0 if j % 2 else 0xFF
+        buf = _d(host)
+        got = _np(A.chksum_batch_csr(buf, _d(off)))
+        want = oracle.batch_csr(host, off)
+        assert np.array_equal(got, want), (choice[:3], np.nonzero(got != want)[0][:8])
+        fin = _np(A.chksum_batch_csr(buf, _d(off), final=True))
+        assert np.array_equal(fin, ~want)
+
+
+def test_stream_mode_off_matches_on_config_c(stream_mode):
+    """Config C through stream mode (2, 4, 8 windows) and per-packet mode: identical."""
+    n = 2 << 20
+    off = synth.mixed_offsets(n)
+    buf = torch.empty(int(off[-1]), dtype=torch.uint8, device=DEV)
+    synth.fill_device(buf, synth.SEED_DATA)
+    doff = _d(off)
+    synth.apply_classes_device(buf, doff)
+    outs = []
+    for su in (-1, 2, 4, 8):
+        stream_mode(su)
+        outs.append(_np(A.chksum_batch_csr(buf, doff)))
+    for o in outs[1:]:
+        assert np.array_equal(o, outs[0])
+
+
+def test_stream_mode_mixed_chunks(oracle):
+    """A CSR batch whose chunks alternate between back to back and not (a decreasing
+    offset, a packet over 2^17 bytes): both modes in one launch."""
+    rng = np.random.default_rng(23)
+    n = 64 * 40
+    lens = rng.integers(0, 2000, size=n)
+    lens[64 * 3 + 5] = 1 << 17          # too long for stream mode: chunk 3 per packet
+    off = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(lens, out=off[1:])
+    bad = 64 * 7 + 8
+    off[bad + 1] = off[bad] - 10        # decreasing: packet `bad` is empty (E < S)
+    buf = torch.empty(int(off[-1]) + 64, dtype=torch.uint8, device=DEV)
+    synth.fill_device(buf, 29)
+    got = _np(A.chksum_batch_csr(buf, _d(off)))
+    host = _np(buf)
+    want = np.array([oracle.inverted(host, int(off[i]), int(max(off[i + 1] - off[i], 0)))
+                     for i in range(n)], dtype=np.uint16)
+    assert want[bad] == 0
+    assert np.array_equal(got, want), np.nonzero(got != want)[0][:8]
+
+
 def test_overlapping_and_zero_stride(oracle):
     buf = torch.empty(70000, dtype=torch.uint8, device=DEV)
     synth.fill_device(buf, 77)

@@ -24,12 +24,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 DEFAULT_VARIANTS = {
-    "A": "0,0,1,0;2,1,1,0;2,2,1,0;2,4,1,0;2,8,1,0;2,8,0,0;2,8,1,32;2,8,1,128;2,8,1,256;"
-         "3,4,1,0;3,8,1,0",
-    "B": "0,0,1,0;3,1,1,0;3,2,1,0;3,4,1,0;3,2,0,0;4,1,1,0;4,2,1,0;2,4,1,0;2,2,1,0;3,2,1,32;"
-         "3,2,1,128;3,4,1,128",
-    "C": "0,0,1,0;2,2,1,0;2,4,1,0;2,8,1,0;1,4,1,0;1,8,1,0;2,4,0,0;2,4,1,64;2,4,1,256;"
-         "2,8,1,64;2,8,1,256;1,8,1,64",
+    "A": "0,0,1,0;0,0,1,0,-1;0,0,1,0,2;0,0,1,0,8;0,0,1,32;0,0,1,128;0,0,1,256;0,0,1,32,8",
+    "B": "0,0,1,0;0,0,1,0,-1;0,0,1,0,2;0,0,1,0,8;0,0,1,32;0,0,1,128;0,0,1,256;0,0,1,32,8",
+    "C": "0,0,1,0;0,0,1,0,-1;0,0,1,0,2;0,0,1,0,8;0,0,1,64;0,0,1,256;0,0,1,64,8;"
+         "0,0,1,32;0,0,1,32,8;0,0,1,32,2",
     "RX": "0,0;2,0;8,0;4,64;4,256;8,64",
     "TX": "0,0;2,0;8,0;4,64;4,256;8,64",
 }
@@ -41,7 +39,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--reps", type=int, default=5, help="launches per variant per round")
     ap.add_argument("--variants", default=None,
-                    help='"U,P,NT,WPC;..." or, for RX/TX, "F,WPC;..." (0 = automatic)')
+                    help='"U,P,NT,WPC[,SU];..." or, for RX/TX, "F,WPC;..." (0 = automatic; '
+                         'SU = stream-mode windows 2/4/8, -1 = stream mode off)')
     args = ap.parse_args()
 
     import torch
@@ -111,8 +110,11 @@ def main():
             f, wpc = (int(x) for x in v.split(","))
             variants.append({"frames": f, "waves_per_cu": wpc})
             continue
-        u, p, nt, wpc = (int(x) for x in v.split(","))
-        variants.append({"unroll": u, "packets": p, "nontemporal": nt, "waves_per_cu": wpc})
+        f = [int(x) for x in v.split(",")]
+        u, p, nt, wpc = f[:4]
+        su = f[4] if len(f) > 4 else 0
+        variants.append({"unroll": u, "packets": p, "nontemporal": nt, "waves_per_cu": wpc,
+                         "stream": su})
 
     def apply(v):
         for k, val in v.items():
