@@ -585,9 +585,105 @@ __device__ __forceinline__ bool stream_ok(uint64_t S, uint64_t E, int lane, int 
     return __builtin_amdgcn_ballot_w64(bad) == 0;
 }
 
+// H at NB boundaries per lane over the wave-uniform byte run [A, X1) (A 16-aligned, the run
+// < 2^32 bytes). begin() issues the first U windows' loads, so that a kernel can overlap
+// them with other work (the frame kernels' header parse); prefixes() then gives
+// h[k] = H(b[k]) for every b[k] in [A, X1], and hx = H(X1). Windows past the run read
+// zeros (range check) and change nothing.
+template <int U, bool NT>
+struct StreamRun {
+    uint64_t A, X1;
+    uint32_t nseg, nwin;
+    __amdgpu_buffer_rsrc_t rsrc;
+    u32x4 v[U];
+
+    __device__ __forceinline__ void begin(uint64_t a, uint64_t x1, uint32_t voff) {
+        A = a;
+        X1 = x1;
+        nseg = ((uint32_t)(X1 - A) + 15u) >> 4;
+        nwin = (nseg + (uint32_t)kWave - 1u) >> 6;
+        rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(A), (short)0,
+                                                 (int)(nseg * 16u), 0x00020000);
+        issue(0, voff);
+    }
+
+    // In window order: the loop consumes them in that order with counted waits
+    // (s_waitcnt vmcnt(U - 1 - u)); the scheduler barriers stop LLVM from reordering them.
+    __device__ __forceinline__ void issue(uint32_t w, uint32_t voff) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            v[u] = load_segment<NT>(rsrc, voff, (w + (uint32_t)u) * 1024u);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+
+    template <int NB>
+    __device__ __forceinline__ void prefixes(const uint64_t (&b)[NB], uint32_t (&h)[NB],
+                                             uint32_t &hx, uint32_t voff) {
+        // each boundary: its window, owner lane (x4 for ds_bpermute), dword masks below it
+        uint32_t bwin[NB];
+        int bsrc[NB];
+        uint32_t below[NB][4];
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+            const uint32_t boff = (uint32_t)(b[k] - A);
+            bwin[k] = boff >> 10;
+            bsrc[k] = (int)(((boff >> 4) & 63u) << 2);
+#pragma unroll
+            for (int d = 0; d < 4; ++d) below[k][d] = dword_keep(0, (int)(boff & 15u) - 4 * d);
+            h[k] = 0;
+        }
+        // X1's segment (the last one; past X1 it holds bytes outside the run): window, lane
+        const uint32_t xt = (uint32_t)(X1 - A) & 15u;
+        const uint32_t xwin = (nseg - 1u) >> 6;
+        const int xlane = (int)((nseg - 1u) & 63u);
+        uint32_t xabove[4];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) xabove[d] = ~dword_keep(0, (int)xt - 4 * d);
+
+        uint32_t carry = 0;  // H(start of the current window), mod 2^32
+        uint32_t x_hi = 0;   // halves of the last segment's bytes at or above X1
+        for (uint32_t w = 0; w < nwin;) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t wu = w + (uint32_t)u;
+                const uint32_t s =
+                    halves(v[u][0], halves(v[u][1], halves(v[u][2], halves(v[u][3], 0u))));
+                const uint32_t incl = wave_incl_scan(s);
+                const uint32_t excl = incl - s;
+#pragma unroll
+                for (int k = 0; k < NB; ++k) {
+                    if (__builtin_amdgcn_ballot_w64(bwin[k] == wu)) {  // boundaries in window
+                        uint32_t part = (uint32_t)__builtin_amdgcn_ds_bpermute(bsrc[k], (int)excl);
+#pragma unroll
+                        for (int d = 0; d < 4; ++d)
+                            part = halves(
+                                (uint32_t)__builtin_amdgcn_ds_bpermute(bsrc[k], (int)v[u][d]) &
+                                    below[k][d],
+                                part);
+                        if (bwin[k] == wu) h[k] = carry + part;
+                    }
+                }
+                if (wu == xwin && xt != 0) {  // wave-uniform: X1 falls inside this segment
+                    uint32_t hh = 0;
+#pragma unroll
+                    for (int d = 0; d < 4; ++d) hh = halves(v[u][d] & xabove[d], hh);
+                    x_hi = (uint32_t)__builtin_amdgcn_readlane((int)hh, xlane);
+                }
+                carry += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+            }
+            w += U;
+            if (w < nwin) issue(w, voff);
+        }
+        hx = carry - x_hi;  // H(X1)
+#pragma unroll
+        for (int k = 0; k < NB; ++k)
+            if (b[k] == X1) h[k] = hx;  // a boundary at X1 may lie past the last window
+    }
+};
+
 // Stream mode for one chunk (stream_ok). Lane j < cnt holds packet j = [S, E); returns
-// lane j's exact halves-sum (0 on lanes >= cnt). U windows' loads are issued together;
-// windows past the chunk read zeros (range check) and change nothing.
+// lane j's exact halves-sum (0 on lanes >= cnt).
 template <int U, bool NT>
 __device__ __forceinline__ uint32_t sum_stream_chunk(uint64_t S, uint64_t E, int lane, int cnt,
                                                      uint32_t voff) {
@@ -600,65 +696,14 @@ __device__ __forceinline__ uint32_t sum_stream_chunk(uint64_t S, uint64_t E, int
     const uint64_t S0 =
         ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(S >> 32)) << 32) |
         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)S);
-    const uint64_t A = S0 & ~(uint64_t)15;
-    const uint32_t span = (uint32_t)(X1 - A);  // <= 64 * 2^17 + 15
-    const uint32_t nseg = (span + 15u) >> 4;
-    const uint32_t nwin = (nseg + (uint32_t)kWave - 1u) >> 6;
-    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<void *>(A), (short)0, (int)(nseg * 16u), 0x00020000);
-    // this lane's boundary S: its window, owner lane (x4 for ds_bpermute), masks below it
-    const uint32_t boff = (uint32_t)(S - A);
-    const uint32_t bwin = boff >> 10;
-    const int bsrc = (int)(((boff >> 4) & 63u) << 2);
-    const int bt = (int)(boff & 15u);
-    uint32_t below[4];
-#pragma unroll
-    for (int d = 0; d < 4; ++d) below[d] = dword_keep(0, bt - 4 * d);
-    // X1's segment (the last one; past X1 it holds the next chunk's bytes): window, lane
-    const uint32_t xt = span & 15u;
-    const uint32_t xwin = (nseg - 1u) >> 6;
-    const int xlane = (int)((nseg - 1u) & 63u);
-    uint32_t xabove[4];
-#pragma unroll
-    for (int d = 0; d < 4; ++d) xabove[d] = ~dword_keep(0, (int)xt - 4 * d);
-
-    uint32_t carry = 0;  // H(start of the current window), mod 2^32
-    uint32_t hb = 0;     // H(S) once its window has passed
-    uint32_t x_hi = 0;   // halves of the last segment's bytes at or above X1
-    for (uint32_t w = 0; w < nwin; w += U) {
-        u32x4 v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            v[u] = load_segment<NT>(rsrc, voff, (w + (uint32_t)u) * 1024u);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t wu = w + (uint32_t)u;
-            const uint32_t s =
-                halves(v[u][0], halves(v[u][1], halves(v[u][2], halves(v[u][3], 0u))));
-            const uint32_t incl = wave_incl_scan(s);
-            const uint32_t excl = incl - s;
-            if (__builtin_amdgcn_ballot_w64(bwin == wu)) {  // boundaries in this window
-                uint32_t part = (uint32_t)__builtin_amdgcn_ds_bpermute(bsrc, (int)excl);
-#pragma unroll
-                for (int d = 0; d < 4; ++d)
-                    part = halves(
-                        (uint32_t)__builtin_amdgcn_ds_bpermute(bsrc, (int)v[u][d]) & below[d],
-                        part);
-                if (bwin == wu) hb = carry + part;
-            }
-            if (wu == xwin && xt != 0) {  // wave-uniform: X1 falls inside this segment
-                uint32_t h = 0;
-#pragma unroll
-                for (int d = 0; d < 4; ++d) h = halves(v[u][d] & xabove[d], h);
-                x_hi = (uint32_t)__builtin_amdgcn_readlane((int)h, xlane);
-            }
-            carry += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-        }
-    }
-    const uint32_t hx = carry - x_hi;  // H(X1)
-    if (S == X1) hb = hx;              // covers a boundary at X1 past the last window
-    const uint32_t hn = from_next_lane(hb, hx, lane);  // H(S_{j+1}); lane 63: H(X1)
-    return lane < cnt ? hn - hb : 0u;
+    // the run spans <= 64 * 2^17 + 15 bytes (stream_ok)
+    StreamRun<U, NT> run;
+    run.begin(S0 & ~(uint64_t)15, X1, voff);
+    const uint64_t bs[1] = {S};
+    uint32_t hb[1], hx;
+    run.prefixes(bs, hb, hx, voff);
+    const uint32_t hn = from_next_lane(hb[0], hx, lane);  // H(S_{j+1}); lane 63: H(X1)
+    return lane < cnt ? hn - hb[0] : 0u;
 }
 
 // Sum over the 64 lanes (DPP row scan + row broadcasts); result valid in lane 63,

@@ -20,6 +20,10 @@ int tuning_frames_in_flight();
 // kernel's default).
 int tuning_waves_per_cu();
 
+// Stream-mode windows a wave issues together (tunable "stream": 2, 4, 8; 0 = stream mode
+// off), with the default of the given kernel family when the tunable is automatic.
+int tuning_stream_windows(int family_default);
+
 }  // namespace aipstack_amd
 
 #endif

@@ -307,12 +307,7 @@ int pick_packets(int u, bool csr) {
 // profiles/r01e): 1500/9000 B strided best at 2 (a wave streams 94-141 KiB per chunk, and
 // occupancy covers the latency), mixed CSR at 8 (stream 2 / 4 / 8 / off: 262 / 258 / 255 /
 // 266 us on config C).
-int pick_stream(bool csr) {
-    const int t = tuning().stream.load(std::memory_order_relaxed);
-    if (t < 0) return 0;
-    if (t == 2 || t == 4 || t == 8) return t;
-    return csr ? 8 : 2;
-}
+int pick_stream(bool csr) { return tuning_stream_windows(csr ? 8 : 2); }
 
 template <class Desc, int U, int P, bool NT, bool SEEDED, int SU>
 int launch_k(const Desc &desc, uint64_t n, uint16_t *d_out, uint32_t flags,
@@ -403,6 +398,13 @@ int launch_chain(const uint64_t *d_addr, const uint32_t *d_len, const uint64_t *
 
 int tuning_waves_per_cu() {
     return tuning().waves_per_cu.load(std::memory_order_relaxed);
+}
+
+int tuning_stream_windows(int family_default) {
+    const int t = tuning().stream.load(std::memory_order_relaxed);
+    if (t < 0) return 0;
+    if (t == 2 || t == 4 || t == 8) return t;
+    return family_default;
 }
 
 int tuning_frames_in_flight() {

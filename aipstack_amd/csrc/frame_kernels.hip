@@ -28,7 +28,7 @@ namespace {
 // pass loads from A0 up to the next 32-byte boundary past them (7 or 8 segments), so the
 // L4 pass starts on a fresh 32-byte sector and no sector is fetched twice.
 constexpr int kHdrSegs = 8;
-constexpr int kHdrDwords = 21;  // frame bytes [0, 84) realigned to the frame start
+constexpr int kHdrDwords = 23;  // frame bytes [0, 92) realigned to the frame start
 constexpr uint32_t kHdrNeed = 97;
 
 
@@ -46,15 +46,19 @@ __device__ __forceinline__ uint32_t be16_at(uint32_t le_dword, int byte) {  // b
     return ((le_dword >> (8 * byte)) & 0xFFu) << 8 | ((le_dword >> (8 * byte + 8)) & 0xFFu);
 }
 
+// One global_store_short at any byte address: ROCm runs gfx9 in unaligned-access mode, so
+// an odd address is one store instruction, not two byte stores (the frame fields sit at
+// S + 24 and S + fld, odd whenever the frame starts at an odd address).
+typedef uint16_t u16_any_align __attribute__((aligned(1)));
 __device__ __forceinline__ void store_be16(uint64_t addr, uint32_t v) {
-    uint8_t *p = reinterpret_cast<uint8_t *>(addr);
-    p[0] = (uint8_t)(v >> 8);
-    p[1] = (uint8_t)v;
+    *reinterpret_cast<u16_any_align *>(addr) = (uint16_t)bswap16(v);
 }
 
 // What the header pass decides for one frame (lane j <-> frame j of the chunk).
 struct FrameLane {
     uint64_t l4s;       // first byte the L4 checksum covers (its parity orients the sum)
+    uint64_t l4e;       // one past the last (stream mode)
+    uint32_t fhalf;     // Tx, stream mode: the checksum field's bytes as they enter H
     uint64_t cs, ce;    // the L4 bytes past the header pass's blocks: [cs, ce), maybe empty
     uint32_t part;      // ones'-complement sum of the L4 bytes inside the header blocks
     bool l4;            // an L4 checksum is computed
@@ -72,7 +76,9 @@ struct FrameLane {
 // (tcp/IpTcpProto_input.h:68-100, udp/IpUdpProto.h:470-490, 631-652, ip/IpStack.h:1093-1130);
 // the send side fills the same fields (ip/IpStack.h:425-453, tcp/IpTcpProto_output.h:1251-1277,
 // udp/IpUdpProto.h:164-179, ip/IpStack.h:1164-1190).
-template <bool TX>
+// STREAM: the L4 sum comes from stream prefixes over [l4s, l4e) (minus the Tx field's
+// bytes, fhalf), so the partial sum over the header blocks and [cs, ce) are not needed.
+template <bool TX, bool STREAM>
 __device__ __forceinline__ FrameLane parse_lane(const u32x4 (&seg)[kHdrSegs], uint64_t S,
                                                 int len, uint32_t hb_end) {
     uint32_t raw[4 * kHdrSegs];
@@ -92,7 +98,8 @@ __device__ __forceinline__ FrameLane parse_lane(const u32x4 (&seg)[kHdrSegs], ui
     for (int i = 0; i < kHdrDwords; ++i) f[i] = __builtin_amdgcn_alignbyte(t2[i + 1], t2[i], rs & 3u);
 
     FrameLane r;
-    r.l4s = r.cs = r.ce = S;
+    r.l4s = r.l4e = r.cs = r.ce = S;
+    r.fhalf = 0;
     r.part = 0;
     r.l4 = false;
     r.words = 0;
@@ -175,6 +182,21 @@ __device__ __forceinline__ FrameLane parse_lane(const u32x4 (&seg)[kHdrSegs], ui
         r.l4 = true;
         r.l4s = S + (uint64_t)dg;
         r.fld = dg + fo;
+        if constexpr (STREAM) {
+            r.l4e = r.l4s + (uint64_t)l4len;
+            if constexpr (TX) {
+                // the field (frame bytes fld, fld + 1; fld = 0 or 2 mod 4, fld <= 90) is
+                // half fld & 2 of f[fld / 4]; in H its two bytes pair with their absolute
+                // neighbours: as stored if S + fld is even, byte-swapped if odd
+                const int k = r.fld >> 2;
+                uint32_t fw = f[9];
+#pragma unroll
+                for (int i = 10; i < kHdrDwords; ++i) fw = blend(k == i ? ~0u : 0u, fw, f[i]);
+                const uint32_t fv = (fw >> (8 * (r.fld & 2))) & 0xFFFFu;
+                r.fhalf = ((S + (uint64_t)r.fld) & 1u) ? bswap16(fv) : fv;
+            }
+            return r;
+        }
         // L4 bytes inside the loaded blocks [A0, A0 + hb_end): summed here, from the aligned
         // dwords (little-endian halves at even absolute addresses, as the L4 pass sums); the
         // rest, [A0 + hb_end, end), by the L4 pass. For Tx the checksum field (always in
@@ -205,7 +227,11 @@ __device__ __forceinline__ FrameLane parse_lane(const u32x4 (&seg)[kHdrSegs], ui
 //       checksum field is masked out of the sum;
 //   (D) lane j finishes frame j: verdict (one coalesced 64-byte store), and for Tx the
 //       IPv4 header and L4 checksums written in place.
-template <bool TX, int U, int P, bool NT>
+//
+// Stream mode (SU > 0, chunks whose frames lie back to back): (C) is replaced by stream
+// prefixes over the chunk's frames (chksum_device.h): each frame's L4 sum is
+// H(l4e) - H(l4s), minus the Tx checksum field's bytes; no per-frame loads or reductions.
+template <bool TX, int U, int P, bool NT, int SU>
 __global__ __launch_bounds__(kBlock) void frame_kernel(CsrDesc desc, uint64_t n,
                                                        uint32_t chunks_per_wave,
                                                        uint8_t *__restrict__ status) {
@@ -245,17 +271,44 @@ __global__ __launch_bounds__(kBlock) void frame_kernel(CsrDesc desc, uint64_t n,
 #pragma unroll
         for (int i = 0; i < kHdrSegs; ++i)  // past hb_end: out of range, reads 0, no traffic
             seg[i] = load_segment<false>(hrsrc, 16u * i < hb_end ? hoff + 16u * i : 0xFFFFFFF0u, 0u);
-        const FrameLane fl = parse_lane<TX>(seg, S, len, hb_end);
-        const bool need = fl.ce != fl.cs;
-        const LaneMeta meta = lane_meta(fl.cs, fl.ce);
+        FrameLane fl;
+        uint32_t r;
+        bool streamed = false;
+        if constexpr (SU > 0) {
+            if (stream_ok(S, E, lane, cnt)) {
+                // (C') stream prefixes at each frame's L4 start and end. The first windows'
+                // loads go out now, behind the header loads, and arrive during the parse.
+                const int lastl = cnt - 1;
+                const uint64_t X1 =
+                    ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(E >> 32), lastl)
+                     << 32) |
+                    (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)E, lastl);
+                StreamRun<SU, NT> run;
+                run.begin(base, X1, voff);
+                fl = parse_lane<TX, true>(seg, S, len, hb_end);
+                // frames without an L4 sum (and lanes past the batch) put both at X1
+                const bool use = lane < cnt && fl.l4;
+                const uint64_t bs[2] = {use ? fl.l4s : X1, use ? fl.l4e : X1};
+                uint32_t h[2], hx;
+                run.prefixes(bs, h, hx, voff);
+                r = fold16(h[1] - h[0] - fl.fhalf);  // exact halves-sum, < 2^32
+                streamed = true;
+            }
+        }
+        if (!streamed) {
+            fl = parse_lane<TX, false>(seg, S, len, hb_end);
+            const bool need = fl.ce != fl.cs;
+            const LaneMeta meta = lane_meta(fl.cs, fl.ce);
 
-        // (C) the remaining L4 bytes, one frame per wave, P frames' loads in flight
-        NoMaskHook hook;
-        const uint32_t sums = sum_lane_packets<U, P, AIPSTACK_ROWS_FRAMES, NT>(
-            meta, __builtin_amdgcn_ballot_w64(need), lane, voff, not_lane0, hook);
+            // (C) the remaining L4 bytes, one frame per wave, P frames' loads in flight
+            NoMaskHook hook;
+            const uint32_t sums = sum_lane_packets<U, P, AIPSTACK_ROWS_FRAMES, NT>(
+                meta, __builtin_amdgcn_ballot_w64(need), lane, voff, not_lane0, hook);
+            // both parts (< 2^24 + 2^17), folded
+            r = fold16(sums + fold16(fl.part));
+        }
 
-        // (D) per-lane finish: both parts (< 2^24 + 2^17), folded, oriented by the L4 start
-        uint32_t r = fold16(sums + fold16(fl.part));
+        // (D) per-lane finish: oriented by the L4 start
         if ((fl.l4s & 1u) == 0)  // L4 start even: little-endian pairing -> big-endian
             r = bswap16(r);
         const uint64_t m = (uint64_t)fl.words + r;
@@ -290,15 +343,24 @@ int launch_frames(const void *d_base, const uint64_t *d_offsets, uint64_t n, uin
     const uint64_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
     if (blocks > 0x7FFFFFFFull || cpw > 0xFFFFFFFFull) return AIPSTACK_CHKSUM_EINVAL;
     CsrDesc desc{(uint64_t)(uintptr_t)d_base, d_offsets};
-    switch (tuning_frames_in_flight()) {
-#define AIPSTACK_LAUNCH_FRAMES(P)                                                          \
-    hipLaunchKernelGGL((frame_kernel<TX, 2, P, true>), dim3((unsigned)blocks), dim3(kBlock), \
+    const int su = tuning_stream_windows(8);  // measured: 8 > 4 > off > 2 (RX and TX)
+#define AIPSTACK_LAUNCH_FRAMES(P, SU)                                                          \
+    hipLaunchKernelGGL((frame_kernel<TX, 2, P, true, SU>), dim3((unsigned)blocks), dim3(kBlock), \
                        0, stream, desc, n, (uint32_t)cpw, d_status)
-        case 2: AIPSTACK_LAUNCH_FRAMES(2); break;
-        case 8: AIPSTACK_LAUNCH_FRAMES(8); break;
-        default: AIPSTACK_LAUNCH_FRAMES(4);
-#undef AIPSTACK_LAUNCH_FRAMES
+#define AIPSTACK_LAUNCH_FRAMES_SU(P)              \
+    switch (su) {                                 \
+        case 0: AIPSTACK_LAUNCH_FRAMES(P, 0); break; \
+        case 2: AIPSTACK_LAUNCH_FRAMES(P, 2); break; \
+        case 8: AIPSTACK_LAUNCH_FRAMES(P, 8); break; \
+        default: AIPSTACK_LAUNCH_FRAMES(P, 4);     \
     }
+    switch (tuning_frames_in_flight()) {
+        case 2: AIPSTACK_LAUNCH_FRAMES_SU(2); break;
+        case 8: AIPSTACK_LAUNCH_FRAMES_SU(8); break;
+        default: AIPSTACK_LAUNCH_FRAMES_SU(4);
+    }
+#undef AIPSTACK_LAUNCH_FRAMES_SU
+#undef AIPSTACK_LAUNCH_FRAMES
     return check_hip(hipGetLastError());
 }
 

@@ -28,8 +28,8 @@ DEFAULT_VARIANTS = {
     "B": "0,0,1,0;0,0,1,0,-1;0,0,1,0,2;0,0,1,0,8;0,0,1,32;0,0,1,128;0,0,1,256;0,0,1,32,8",
     "C": "0,0,1,0;0,0,1,0,-1;0,0,1,0,2;0,0,1,0,8;0,0,1,64;0,0,1,256;0,0,1,64,8;"
          "0,0,1,32;0,0,1,32,8;0,0,1,32,2",
-    "RX": "0,0;2,0;8,0;4,64;4,256;8,64",
-    "TX": "0,0;2,0;8,0;4,64;4,256;8,64",
+    "RX": "0,0;0,0,-1;0,0,2;0,0,8;2,0;4,64;4,256;2,64,2;2,256,2",
+    "TX": "0,0;0,0,-1;0,0,2;0,0,8;2,0;4,64;4,256;2,64,2;2,256,2",
 }
 
 
@@ -39,7 +39,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--reps", type=int, default=5, help="launches per variant per round")
     ap.add_argument("--variants", default=None,
-                    help='"U,P,NT,WPC[,SU];..." or, for RX/TX, "F,WPC;..." (0 = automatic; '
+                    help='"U,P,NT,WPC[,SU];..." or, for RX/TX, "F,WPC[,SU];..." (0 = automatic; '
                          'SU = stream-mode windows 2/4/8, -1 = stream mode off)')
     args = ap.parse_args()
 
@@ -107,8 +107,9 @@ def main():
     variants = []
     for v in (args.variants or DEFAULT_VARIANTS[args.config]).split(";"):
         if layout in ("rx", "tx"):
-            f, wpc = (int(x) for x in v.split(","))
-            variants.append({"frames": f, "waves_per_cu": wpc})
+            f = [int(x) for x in v.split(",")]
+            variants.append({"frames": f[0], "waves_per_cu": f[1],
+                             "stream": f[2] if len(f) > 2 else 0})
             continue
         f = [int(x) for x in v.split(",")]
         u, p, nt, wpc = f[:4]
