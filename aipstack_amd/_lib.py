@@ -11,7 +11,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libaipstack_chksum.so")
+# AIPSTACK_AMD_LIB: load another build instead (A/B experiments, tools/sweep.py --lib).
+LIB_PATH = os.environ.get("AIPSTACK_AMD_LIB") or os.path.join(_HERE, "lib", "libaipstack_chksum.so")
 
 # Every symbol include/aipstack_amd/*.h declares, with its ctypes signature.
 _c_u16 = ctypes.c_uint16

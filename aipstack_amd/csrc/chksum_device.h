@@ -590,13 +590,15 @@ __device__ __forceinline__ bool stream_ok(uint64_t S, uint64_t E, int lane, int 
 // them with other work (the frame kernels' header parse); prefixes() then gives
 // h[k] = H(b[k]) for every b[k] in [A, X1], and hx = H(X1). Windows past the run read
 // zeros (range check) and change nothing.
-template <int U, bool NT>
+template <int U, bool NT, int PRE = U>
 struct StreamRun {
     uint64_t A, X1;
     uint32_t nseg, nwin;
     __amdgpu_buffer_rsrc_t rsrc;
     u32x4 v[U];
 
+    // Issues windows [0, PRE) now (the rest of the first U when prefixes() starts): a
+    // kernel that overlaps begin() with register-hungry work keeps only PRE in flight.
     __device__ __forceinline__ void begin(uint64_t a, uint64_t x1, uint32_t voff) {
         A = a;
         X1 = x1;
@@ -604,14 +606,16 @@ struct StreamRun {
         nwin = (nseg + (uint32_t)kWave - 1u) >> 6;
         rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(A), (short)0,
                                                  (int)(nseg * 16u), 0x00020000);
-        issue(0, voff);
+        issue<0, PRE>(0, voff);
     }
 
-    // In window order: the loop consumes them in that order with counted waits
-    // (s_waitcnt vmcnt(U - 1 - u)); the scheduler barriers stop LLVM from reordering them.
+    // Slots [U0, U1) <- windows w + U0 .. w + U1 - 1, in window order: the loop consumes
+    // them in that order with counted waits (s_waitcnt vmcnt(U - 1 - u)); the scheduler
+    // barriers stop LLVM from reordering them.
+    template <int U0, int U1>
     __device__ __forceinline__ void issue(uint32_t w, uint32_t voff) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
+        for (int u = U0; u < U1; ++u) {
             v[u] = load_segment<NT>(rsrc, voff, (w + (uint32_t)u) * 1024u);
             __builtin_amdgcn_sched_barrier(0);
         }
@@ -641,6 +645,7 @@ struct StreamRun {
 #pragma unroll
         for (int d = 0; d < 4; ++d) xabove[d] = ~dword_keep(0, (int)xt - 4 * d);
 
+        if constexpr (PRE < U) issue<PRE, U>(0, voff);
         uint32_t carry = 0;  // H(start of the current window), mod 2^32
         uint32_t x_hi = 0;   // halves of the last segment's bytes at or above X1
         for (uint32_t w = 0; w < nwin;) {
@@ -673,7 +678,7 @@ struct StreamRun {
                 carry += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
             }
             w += U;
-            if (w < nwin) issue(w, voff);
+            if (w < nwin) issue<0, U>(w, voff);
         }
         hx = carry - x_hi;  // H(X1)
 #pragma unroll
@@ -681,6 +686,68 @@ struct StreamRun {
             if (b[k] == X1) h[k] = hx;  // a boundary at X1 may lie past the last window
     }
 };
+
+// Minimum / maximum over the 64 lanes (DPP row scan + row broadcasts), wave-uniform.
+#define AIPSTACK_WAVE_REDUCE(name, op, ident)                                                \
+    __device__ __forceinline__ int name(int v) {                                             \
+        v = op(v, __builtin_amdgcn_update_dpp((int)(ident), v, 0x111, 0xF, 0xF, false));     \
+        v = op(v, __builtin_amdgcn_update_dpp((int)(ident), v, 0x112, 0xF, 0xF, false));     \
+        v = op(v, __builtin_amdgcn_update_dpp((int)(ident), v, 0x114, 0xF, 0xF, false));     \
+        v = op(v, __builtin_amdgcn_update_dpp((int)(ident), v, 0x118, 0xF, 0xF, false));     \
+        v = op(v, __builtin_amdgcn_update_dpp((int)(ident), v, 0x142, 0xA, 0xF, false));     \
+        v = op(v, __builtin_amdgcn_update_dpp((int)(ident), v, 0x143, 0xC, 0xF, false));     \
+        return __builtin_amdgcn_readlane(v, 63);                                             \
+    }
+AIPSTACK_WAVE_REDUCE(wave_min_i32, min, 0x7FFFFFFF)
+AIPSTACK_WAVE_REDUCE(wave_max_i32, max, 0x80000000u)
+#undef AIPSTACK_WAVE_REDUCE
+
+// Stream runs for chunks that lie close together in memory but not back to back (the
+// chain kernel: header nodes in one area, payload chunks in another). The candidates
+// (lanes in `cand`, chunk [a, a + l), l <= kStreamMaxLen) are tried as one run over
+// their address hull; a sparse hull (more than 2x their bytes + 2 KiB) is split once at
+// its middle and each half tried. A dense set's chunk sums are H(a + l) - H(a) over its
+// run: exact halves-sums, as the per-chunk path gives. Returns the lanes done, whose
+// sums are written to `sums`.
+template <int U, bool NT>
+__device__ __forceinline__ uint64_t stream_dense_chunks(uint64_t a, uint32_t l, int lane,
+                                                        uint64_t cand, uint32_t &sums,
+                                                        uint32_t voff) {
+    if (!cand) return 0;
+    // addresses relative to the first candidate; chunks over 2^30 bytes away never stream
+    const int first = (int)__builtin_ctzll(cand);
+    const uint64_t base =
+        ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(a >> 32), first) << 32) |
+        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)a, first);
+    const int64_t rel = (int64_t)(a - base);
+    cand &= __builtin_amdgcn_ballot_w64(rel > -(1ll << 30) && rel < (1ll << 30));
+    const int rs = (int)rel, re = (int)rel + (int)l;
+    uint64_t done = 0, half0 = 0, half1 = 0;
+    for (int t = 0; t < 3; ++t) {  // the whole set, then its two halves
+        const uint64_t m = t == 0 ? cand : (t == 1 ? half0 : half1);
+        if (!m) continue;
+        const bool in = ((m >> lane) & 1u) != 0;
+        const int lo = wave_min_i32(in ? rs : 0x7FFFFFFF);
+        const int hi = wave_max_i32(in ? re : (int)0x80000000u);
+        const uint32_t tot = wave_sum(in ? l : 0u);  // <= 64 * 2^17
+        if ((uint32_t)(hi - lo) <= 2u * tot + 2048u) {
+            const uint64_t X1 = base + (uint64_t)(int64_t)hi;
+            StreamRun<U, NT> run;
+            run.begin((base + (uint64_t)(int64_t)lo) & ~(uint64_t)15, X1, voff);
+            const uint64_t bs[2] = {in ? a : X1, in ? a + l : X1};
+            uint32_t h[2], hx;
+            run.prefixes(bs, h, hx, voff);
+            if (in) sums = h[1] - h[0];
+            done |= m;
+            if (t == 0) break;
+        } else if (t == 0) {
+            const int mid = lo + (int)((uint32_t)(hi - lo) >> 1);
+            half0 = m & __builtin_amdgcn_ballot_w64(rs < mid);
+            half1 = m & ~half0;
+        }
+    }
+    return done;
+}
 
 // Stream mode for one chunk (stream_ok). Lane j < cnt holds packet j = [S, E); returns
 // lane j's exact halves-sum (0 on lanes >= cnt).

@@ -152,7 +152,7 @@ __device__ __forceinline__ uint32_t parity_below(uint64_t mask, uint32_t s) {  /
     return (uint32_t)__builtin_popcountll(mask & below) & 1u;
 }
 
-template <int U, int P, bool NT>
+template <int U, int P, bool NT, int SU>
 __global__ __launch_bounds__(kBlock) void chksum_chain_kernel(
     const uint64_t *__restrict__ chunk_addr, const uint32_t *__restrict__ chunk_len,
     const uint64_t *__restrict__ index, const uint32_t *__restrict__ states, uint64_t n,
@@ -214,12 +214,20 @@ __global__ __launch_bounds__(kBlock) void chksum_chain_kernel(
             const uint32_t s = before ? 0u : scs - kr;
             uint32_t q = parity_below(odd, (uint32_t)lane) ^ parity_below(odd, s);
             if (before) q ^= carry_par;
-            // chunk sums, one per wave
-            const LaneMeta meta = lane_meta(a, a + (uint64_t)l);
-            NoMaskHook hook;
-            const uint32_t sums = sum_lane_packets<U, P, AIPSTACK_ROWS_CHAIN, NT>(
-                meta, __builtin_amdgcn_ballot_w64(valid && (meta.packed >> 9) != 0), lane, voff,
-                not_lane0, hook);
+            // chunk sums: stream runs over sets of chunks that lie close together, the
+            // rest one chunk per wave (P in flight; small ones four per instruction)
+            uint32_t sums = 0;
+            uint64_t todo = __builtin_amdgcn_ballot_w64(valid && l != 0);
+            if constexpr (SU > 0)
+                todo &= ~stream_dense_chunks<SU, NT>(
+                    a, l, lane, todo & __builtin_amdgcn_ballot_w64(l <= kStreamMaxLen), sums,
+                    voff);
+            if (todo) {
+                const LaneMeta meta = lane_meta(a, a + (uint64_t)l);
+                NoMaskHook hook;
+                sums |= sum_lane_packets<U, P, AIPSTACK_ROWS_CHAIN, NT>(meta, todo, lane, voff,
+                                                                       not_lane0, hook);
+            }
             uint32_t r = fold16(sums);
             if ((uint32_t)(a & 1) == q)
                 r = bswap16(r);
@@ -376,7 +384,7 @@ int launch(const Desc &desc, uint64_t n, uint32_t max_len, uint16_t *d_out, uint
     return AIPSTACK_CHKSUM_EINVAL;
 }
 
-template <int U, int P, bool NT>
+template <int U, int P, bool NT, int SU>
 int launch_chain(const uint64_t *d_addr, const uint32_t *d_len, const uint64_t *d_index,
                  const uint32_t *d_states, uint64_t n, uint16_t *d_out, uint32_t flags,
                  hipStream_t stream) {
@@ -389,7 +397,7 @@ int launch_chain(const uint64_t *d_addr, const uint32_t *d_len, const uint64_t *
     const uint64_t waves = (nchunks + cpw - 1) / cpw;
     const uint64_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
     if (blocks > 0x7FFFFFFFull || cpw > 0xFFFFFFFFull) return AIPSTACK_CHKSUM_EINVAL;
-    hipLaunchKernelGGL((chksum_chain_kernel<U, P, NT>), dim3((unsigned)blocks), dim3(kBlock), 0,
+    hipLaunchKernelGGL((chksum_chain_kernel<U, P, NT, SU>), dim3((unsigned)blocks), dim3(kBlock), 0,
                        stream, d_addr, d_len, d_index, d_states, n, (uint32_t)cpw, d_out, flags);
     return check_hip(hipGetLastError());
 }
@@ -474,9 +482,15 @@ extern "C" int aipstack_chksum_batch_chain(const uint64_t *d_chunk_addr,
     if (!d_chunk_addr || !d_chunk_len || !d_chunk_index || !d_out) return AIPSTACK_CHKSUM_EINVAL;
     if (n > (1ull << 40)) return AIPSTACK_CHKSUM_EINVAL;
     // Chains are mostly short pieces (headers, ring-buffer halves): U = 2 covers 2 KiB.
-    return tuning().nontemporal.load(std::memory_order_relaxed)
-               ? launch_chain<2, 4, true>(d_chunk_addr, d_chunk_len, d_chunk_index, d_states, n,
-                                       d_out, flags, (hipStream_t)stream)
-               : launch_chain<2, 4, false>(d_chunk_addr, d_chunk_len, d_chunk_index, d_states, n,
-                                        d_out, flags, (hipStream_t)stream);
+#define AIPSTACK_LAUNCH_CHAIN(NT, SU)                                                          \
+    return launch_chain<2, 4, NT, SU>(d_chunk_addr, d_chunk_len, d_chunk_index, d_states, n, \
+                                      d_out, flags, (hipStream_t)stream)
+    if (!tuning().nontemporal.load(std::memory_order_relaxed)) AIPSTACK_LAUNCH_CHAIN(false, 0);
+    switch (tuning_stream_windows(4)) {
+        case 0: AIPSTACK_LAUNCH_CHAIN(true, 0);
+        case 2: AIPSTACK_LAUNCH_CHAIN(true, 2);
+        case 8: AIPSTACK_LAUNCH_CHAIN(true, 8);
+        default: AIPSTACK_LAUNCH_CHAIN(true, 4);
+    }
+#undef AIPSTACK_LAUNCH_CHAIN
 }

@@ -50,8 +50,15 @@ __device__ __forceinline__ uint32_t be16_at(uint32_t le_dword, int byte) {  // b
 // an odd address is one store instruction, not two byte stores (the frame fields sit at
 // S + 24 and S + fld, odd whenever the frame starts at an odd address).
 typedef uint16_t u16_any_align __attribute__((aligned(1)));
+#ifndef AIPSTACK_TX_STORE_MODE  // experiments only (tools/sweep.py --lib): 1 = nontemporal,
+#define AIPSTACK_TX_STORE_MODE 0   // 2 = no field stores (measures their cost; wrong output)
+#endif
 __device__ __forceinline__ void store_be16(uint64_t addr, uint32_t v) {
+#if AIPSTACK_TX_STORE_MODE == 0
     *reinterpret_cast<u16_any_align *>(addr) = (uint16_t)bswap16(v);
+#elif AIPSTACK_TX_STORE_MODE == 1
+    __builtin_nontemporal_store((uint16_t)bswap16(v), reinterpret_cast<u16_any_align *>(addr));
+#endif
 }
 
 // What the header pass decides for one frame (lane j <-> frame j of the chunk).
@@ -231,8 +238,13 @@ __device__ __forceinline__ FrameLane parse_lane(const u32x4 (&seg)[kHdrSegs], ui
 // Stream mode (SU > 0, chunks whose frames lie back to back): (C) is replaced by stream
 // prefixes over the chunk's frames (chksum_device.h): each frame's L4 sum is
 // H(l4e) - H(l4s), minus the Tx checksum field's bytes; no per-frame loads or reductions.
+// Stream windows issued before the header parse (the rest after it): all of them hold
+// ~4 * SU more VGPRs through the parse.
+#ifndef AIPSTACK_FRAME_PREFETCH
+#define AIPSTACK_FRAME_PREFETCH(SU) ((SU) / 2)
+#endif
 template <bool TX, int U, int P, bool NT, int SU>
-__global__ __launch_bounds__(kBlock) void frame_kernel(CsrDesc desc, uint64_t n,
+__global__ __launch_bounds__(kBlock, 4) void frame_kernel(CsrDesc desc, uint64_t n,
                                                        uint32_t chunks_per_wave,
                                                        uint8_t *__restrict__ status) {
     const int lane = threadIdx.x & (kWave - 1);
@@ -283,7 +295,7 @@ __global__ __launch_bounds__(kBlock) void frame_kernel(CsrDesc desc, uint64_t n,
                     ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(E >> 32), lastl)
                      << 32) |
                     (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)E, lastl);
-                StreamRun<SU, NT> run;
+                StreamRun<SU, NT, AIPSTACK_FRAME_PREFETCH(SU)> run;
                 run.begin(base, X1, voff);
                 fl = parse_lane<TX, true>(seg, S, len, hb_end);
                 // frames without an L4 sum (and lanes past the batch) put both at X1

@@ -175,8 +175,9 @@ int aipstack_chksum_device_check(int device);
  * "chunks_per_wave", "unroll" (segments per lane issued up front, 1..4), "packets"
  * (packets a wave keeps in flight: 1, 2, 4, 8), "nontemporal" (0/1), "frames" (frames
  * in flight per wave in Rx verify / Tx fill: 2, 4, 8), "stream" (1 KiB windows a wave
- * issues together when a 64-packet chunk lies back to back in memory: 2, 4, 8; -1 turns
- * this stream mode off, so every packet is summed on its own). Process-wide;
+ * issues together in stream mode -- a 64-packet or 64-frame chunk that lies back to back
+ * in memory, or chain chunks that lie close together: 2, 4, 8; -1 turns stream mode off,
+ * so every packet, frame or chunk is summed on its own). Process-wide;
  * results never depend on them. Returns _OK or _EINVAL for an unknown key. */
 int aipstack_chksum_tune(const char *key, int value);
 

@@ -383,9 +383,12 @@ def _chain_tables(golden, db):
             np.array(want, dtype=np.uint16))
 
 
-def test_chain_golden_reference_cases(golden):
+@pytest.mark.parametrize("su", [0, -1])
+def test_chain_golden_reference_cases(golden, stream_mode, su):
     """All 3,609 reference chain cases (the 512-node 0x00FF KAT, the chain==flat splits,
-    scatter chains with states/offsets/tot_len) in ONE GPU batch."""
+    scatter chains with states/offsets/tot_len) in ONE GPU batch; with and without the
+    stream runs over chunks that lie close together."""
+    stream_mode(su)
     db = _d(golden["blob"])
     addr, ln, idx, st, want = _chain_tables(golden, db)
     got = _np(A.chksum_batch_chain(_d(addr.view(np.int64)), _d(ln.view(np.int32)),
@@ -422,9 +425,11 @@ def test_chain_flatten_and_null_states(oracle):
     assert np.array_equal(got, np.array(want, dtype=np.uint16))
 
 
-def test_chain_tcp_tx_shape(oracle):
+@pytest.mark.parametrize("su", [0, -1])
+def test_chain_tcp_tx_shape(oracle, stream_mode, su):
     """TCP Tx shape (tcp/IpTcpProto_output.h:1251-1277): pseudo-header state + header node
     + up to 2 send-ring chunks (utils/TcpRingBufferUtils.h:51), 100k segments."""
+    stream_mode(su)
     rng = np.random.default_rng(9)
     ring = rng.integers(0, 256, size=1 << 22, dtype=np.uint8)
     hdrs = rng.integers(0, 256, size=100000 * 60, dtype=np.uint8)
@@ -458,6 +463,20 @@ def test_chain_tcp_tx_shape(oracle):
     assert np.array_equal(got, np.array(want, dtype=np.uint16))
 
 
+@pytest.mark.parametrize("su", [2, 4, 8, -1])
+def test_chain_bench_shape(su, stream_mode):
+    """bench.py's CHAIN layout (20-B header nodes at a 32-B stride + a contiguous payload ring
+    split in two chunks per chain): header and payload chunks each stream as one run."""
+    stream_mode(su)
+    sys.path.insert(0, ROOT)
+    import bench
+    spec = {"n": 50000, "seed": 77}
+    ch = bench.make_chains(spec, torch.device(DEV))
+    out = _np(A.chksum_batch_chain(ch["addr"], ch["len"], ch["index"], ch["states"],
+                                   final=True))
+    assert bench.chain_check(ch, out).startswith("bit-exact")
+
+
 # ---- frame-level batches: Tx fill / Rx verify (SURVEY 8(f) rows 2-3) ----------------------
 
 def _corrupt(buf, off, frac, seed):
@@ -470,8 +489,10 @@ def _corrupt(buf, off, frac, seed):
         buf[j] ^= np.uint8(1 << int(rng.integers(0, 8)))
 
 
+@pytest.mark.parametrize("su", [0, -1])
 @pytest.mark.parametrize("n,maxp", [(200000, 1460), (20000, 9000)])
-def test_tx_fill_matches_oracle(oracle, n, maxp):
+def test_tx_fill_matches_oracle(oracle, stream_mode, n, maxp, su):
+    stream_mode(su)
     buf, off = synth.frames_host(n, seed=11, max_payload=maxp)
     dbuf, doff = _d(buf), _d(off)
     st = _np(A.tx_fill(dbuf, doff))
@@ -483,8 +504,10 @@ def test_tx_fill_matches_oracle(oracle, n, maxp):
     assert bad.size == 0, bad[:10]
 
 
+@pytest.mark.parametrize("su", [0, -1])
 @pytest.mark.parametrize("n,maxp", [(200000, 1460), (20000, 9000)])
-def test_rx_verify_matches_oracle(oracle, n, maxp):
+def test_rx_verify_matches_oracle(oracle, stream_mode, n, maxp, su):
+    stream_mode(su)
     buf, off = synth.frames_host(n, seed=12, max_payload=maxp)
     oracle.tx_fill_batch(buf, off)                 # valid frames ...
     rng = np.random.default_rng(1)
@@ -516,10 +539,12 @@ def _edge_frames(seed, n):
     return frame_cases.pack(frame_cases.frames(seed, n))
 
 
+@pytest.mark.parametrize("su", [0, 2, -1])
 @pytest.mark.parametrize("shift", [0, 1, 7, 13])
-def test_rx_verify_edge_frames(oracle, shift):
+def test_rx_verify_edge_frames(oracle, stream_mode, shift, su):
     """tests/golden/frame_cases.py: every verdict, IPv4 options, padding, zero-sum L4 data,
     one mutation in 40 % of frames; the whole batch starts `shift` bytes into a buffer."""
+    stream_mode(su)
     buf, off = _edge_frames(20251015 + shift, 3000)
     big = np.zeros(buf.size + shift, dtype=np.uint8)
     big[shift:] = buf
@@ -529,8 +554,10 @@ def test_rx_verify_edge_frames(oracle, shift):
     assert np.all(np.bincount(want, minlength=9) > 0)
 
 
+@pytest.mark.parametrize("su", [0, 2, -1])
 @pytest.mark.parametrize("shift", [0, 3])
-def test_tx_fill_edge_frames(oracle, shift):
+def test_tx_fill_edge_frames(oracle, stream_mode, shift, su):
+    stream_mode(su)
     buf, off = _edge_frames(7 + shift, 3000)
     big = np.zeros(buf.size + shift, dtype=np.uint8)
     big[shift:] = buf

@@ -41,12 +41,17 @@ def main():
     ap.add_argument("--variants", default=None,
                     help='"U,P,NT,WPC[,SU];..." or, for RX/TX, "F,WPC[,SU];..." (0 = automatic; '
                          'SU = stream-mode windows 2/4/8, -1 = stream mode off)')
+    ap.add_argument("--lib", default=None,
+                    help="load this build of libaipstack_chksum.so instead (experiments)")
     args = ap.parse_args()
 
     import torch
 
+    if args.lib:  # before the package loads the library
+        os.environ["AIPSTACK_AMD_LIB"] = os.path.abspath(args.lib)
     import aipstack_amd as A
     from aipstack_amd import _lib, synth
+    print(f"library: {_lib.LIB_PATH}", file=sys.stderr)
     lib = _lib.load()
 
     dev = torch.device("cuda", 0)
