@@ -58,6 +58,8 @@ __device__ __forceinline__ void store_be16(uint64_t addr, uint32_t v) {
     *reinterpret_cast<u16_any_align *>(addr) = (uint16_t)bswap16(v);
 #elif AIPSTACK_TX_STORE_MODE == 1
     __builtin_nontemporal_store((uint16_t)bswap16(v), reinterpret_cast<u16_any_align *>(addr));
+#else
+    asm volatile("" ::"v"(v), "v"(addr));  // keep the value live, store nothing
 #endif
 }
 
