@@ -63,6 +63,22 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+class stdout_to_stderr:
+    """Point file descriptor 1 at stderr for the duration (C/C++ library chatter included;
+    C stdio buffers are flushed before fd 1 is restored)."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self._saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        ctypes.CDLL(None).fflush(None)
+        os.dup2(self._saved, 1)
+        os.close(self._saved)
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -293,8 +309,12 @@ def main():
     from aipstack_amd import synth
 
     if world > 1:
-        # control plane only (barriers + max of times); no data-path collective
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        # control plane only (barriers + max of times); no data-path collective. Gloo's C++
+        # side prints "[Gloo] Rank r is connected to ..." on stdout: keep stdout for the one
+        # JSON line.
+        with stdout_to_stderr():
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+            dist.barrier()
     # AIPSTACK_BENCH_FORCE_DEVICE: rehearsal of the multi-rank flow on a 1-GPU box (every
     # rank on that device). Never set by the driver; ranks then own their LOCAL_RANK GPU.
     device = int(os.environ.get("AIPSTACK_BENCH_FORCE_DEVICE", local_rank))
