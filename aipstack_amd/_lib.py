@@ -31,6 +31,8 @@ SIGNATURES = {
     "aipstack_chksum_batch_chain": (_c_int, [_c_vp, _c_vp, _c_vp, _c_vp, _c_u64, _c_vp, _c_u32, _c_vp]),
     "aipstack_chksum_rx_verify": (_c_int, [_c_vp, _c_vp, _c_u64, _c_vp, _c_vp]),
     "aipstack_chksum_tx_fill": (_c_int, [_c_vp, _c_vp, _c_u64, _c_vp, _c_vp]),
+    "aipstack_chksum_tx_fill_workspace_bytes": (_c_u64, [_c_u64]),
+    "aipstack_chksum_tx_fill_split": (_c_int, [_c_vp, _c_vp, _c_u64, _c_vp, _c_vp, _c_u64, _c_vp]),
     "aipstack_chksum_strerror": (ctypes.c_char_p, [_c_int]),
     "aipstack_chksum_last_hip_error": (_c_int, []),
     "aipstack_chksum_device_check": (_c_int, [_c_int]),

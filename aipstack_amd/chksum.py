@@ -444,16 +444,34 @@ def rx_verify(frames, offsets, *, out=None, stream=None):
     return out
 
 
-def tx_fill(frames, offsets, *, out=None, stream=None):
+def tx_fill(frames, offsets, *, out=None, stream=None, split=True, workspace=None):
     """Tx fill on the GPU, IN PLACE: writes the IPv4 header checksum and the TCP / UDP /
-    ICMP checksum of every frame; returns one status per frame (AIPSTACK_RX_* codes)."""
+    ICMP checksum of every frame; returns one status per frame (AIPSTACK_RX_* codes).
+
+    ``split=True`` (default) runs the two-pass ``aipstack_chksum_tx_fill_split`` with a
+    workspace of 8 bytes per frame (``workspace``: a device tensor of at least that many
+    bytes, else one is taken from torch's allocator); ``split=False`` the one-pass
+    ``aipstack_chksum_tx_fill``. Both write the same bytes."""
     _require_device(frames, "frames")
     _require_device(offsets, "offsets")
     n = offsets.numel() - 1
     out = _u8_out(out, max(n, 0), frames)
-    _check(_lib.load().aipstack_chksum_tx_fill(frames.data_ptr(), offsets.data_ptr(), n,
-                                               out.data_ptr(), _stream_handle(stream)),
-           "aipstack_chksum_tx_fill")
+    lib = _lib.load()
+    if not split:
+        _check(lib.aipstack_chksum_tx_fill(frames.data_ptr(), offsets.data_ptr(), n,
+                                           out.data_ptr(), _stream_handle(stream)),
+               "aipstack_chksum_tx_fill")
+        return out
+    need = int(lib.aipstack_chksum_tx_fill_workspace_bytes(max(n, 0)))
+    if workspace is None:
+        workspace = _torch().empty(max(need, 8), dtype=_torch().uint8, device=frames.device)
+    else:
+        _require_device(workspace, "workspace")
+    ws_bytes = workspace.numel() * workspace.element_size()
+    _check(lib.aipstack_chksum_tx_fill_split(frames.data_ptr(), offsets.data_ptr(), n,
+                                             out.data_ptr(), workspace.data_ptr(), ws_bytes,
+                                             _stream_handle(stream)),
+           "aipstack_chksum_tx_fill_split")
     return out
 
 

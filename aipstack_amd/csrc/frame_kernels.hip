@@ -63,6 +63,40 @@ __device__ __forceinline__ void store_be16(uint64_t addr, uint32_t v) {
 #endif
 }
 
+// Split Tx fill's per-frame field record: IPv4 header checksum (bits 0-15), L4 checksum
+// (16-31), L4 field offset from the frame start (32-39), write the IPv4 field (bit 40),
+// write the L4 field (bit 41), the frame's status (48-55).
+__device__ __forceinline__ uint64_t tx_record(uint32_t hchk, uint32_t chk, int fld, bool ip,
+                                              bool l4, int status) {
+    return (uint64_t)(hchk & 0xFFFFu) | (uint64_t)(chk & 0xFFFFu) << 16 |
+           (uint64_t)(uint32_t)fld << 32 | (uint64_t)ip << 40 | (uint64_t)l4 << 41 |
+           (uint64_t)(uint8_t)status << 48;
+}
+
+// Second pass of split Tx fill: one frame per thread, the field stores of every frame
+// after the whole read pass (stream-ordered behind frame_kernel<TX, ..., SPLIT>), and the
+// status bytes.
+__global__ __launch_bounds__(kBlock) void tx_scatter_kernel(uint64_t base,
+                                                            const uint64_t *__restrict__ offsets,
+                                                            const uint64_t *__restrict__ records,
+                                                            uint8_t *__restrict__ status,
+                                                            uint64_t n) {
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        const uint64_t rec = records[i];
+        status[i] = (uint8_t)(rec >> 48);
+        const uint64_t S = base + offsets[i];
+        if ((rec >> 40) & 1u)
+            store_be16(S + 24, (uint32_t)rec);
+        if ((rec >> 41) & 1u)
+            store_be16(S + ((rec >> 32) & 0xFFu), (uint32_t)(rec >> 16));
+    }
+}
+
+#ifndef AIPSTACK_TX_RECORD_MODE  // experiments only (tools/build_variant.sh): 1 = nontemporal
+#define AIPSTACK_TX_RECORD_MODE 0   // record stores; 2 = none, 3/4/5 = 4/2/1 bytes (wrong output)
+#endif
+
 // What the header pass decides for one frame (lane j <-> frame j of the chunk).
 struct FrameLane {
     uint64_t l4s;       // first byte the L4 checksum covers (its parity orients the sum)
@@ -245,10 +279,15 @@ __device__ __forceinline__ FrameLane parse_lane(const u32x4 (&seg)[kHdrSegs], ui
 #ifndef AIPSTACK_FRAME_PREFETCH
 #define AIPSTACK_FRAME_PREFETCH(SU) ((SU) / 2)
 #endif
-template <bool TX, int U, int P, bool NT, int SU>
+// SPLIT (Tx only): instead of storing the two fields in place, lane j writes frame j's
+// field record (tx_record) to a workspace, coalesced; tx_scatter_kernel stores them after
+// the whole read pass. Measured (profiles/r01g/tx_store_probe.jsonl): 2-byte stores
+// interleaved with the read stream cost ~5x what the same stores cost as their own pass.
+template <bool TX, int U, int P, bool NT, int SU, bool SPLIT>
 __global__ __launch_bounds__(kBlock, 4) void frame_kernel(CsrDesc desc, uint64_t n,
                                                        uint32_t chunks_per_wave,
-                                                       uint8_t *__restrict__ status) {
+                                                       uint8_t *__restrict__ status,
+                                                       uint64_t *__restrict__ records) {
     const int lane = threadIdx.x & (kWave - 1);
     const uint32_t wave_in_block = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerBlock + wave_in_block;
@@ -329,23 +368,41 @@ __global__ __launch_bounds__(kBlock, 4) void frame_kernel(CsrDesc desc, uint64_t
         uint32_t chk = (~fold16((uint32_t)m + (uint32_t)(m >> 32))) & 0xFFFFu;
         int v = fl.pre;
         if (TX) {
-            if (fl.ip_ok)
-                store_be16(S + 24, fl.hchk);
-            if (fl.l4) {
-                if (fl.udp && chk == 0) chk = 0xFFFFu;              // udp/IpUdpProto.h:176-178
-                store_be16(S + (uint64_t)fl.fld, chk);
+            if (fl.udp && chk == 0) chk = 0xFFFFu;                  // udp/IpUdpProto.h:176-178
+            if constexpr (SPLIT) {
+                const uint64_t rec = tx_record(fl.hchk, chk, fl.fld, fl.ip_ok, fl.l4, v);
+                if (lane < cnt) {
+#if AIPSTACK_TX_RECORD_MODE == 0
+                    records[p0 + lane] = rec;
+#elif AIPSTACK_TX_RECORD_MODE == 1  // experiments (wrong output from 3 on): nontemporal,
+                    __builtin_nontemporal_store(rec, records + p0 + lane);
+#elif AIPSTACK_TX_RECORD_MODE == 3  // 4-, 2-, 1-byte records, none
+                    reinterpret_cast<uint32_t *>(records)[p0 + lane] = (uint32_t)rec;
+#elif AIPSTACK_TX_RECORD_MODE == 4
+                    reinterpret_cast<uint16_t *>(records)[p0 + lane] = (uint16_t)rec;
+#elif AIPSTACK_TX_RECORD_MODE == 5
+                    reinterpret_cast<uint8_t *>(records)[p0 + lane] = (uint8_t)rec;
+#else
+                    asm volatile("" ::"v"(rec));
+#endif
+                }
+            } else {
+                if (fl.ip_ok)
+                    store_be16(S + 24, fl.hchk);
+                if (fl.l4)
+                    store_be16(S + (uint64_t)fl.fld, chk);
             }
         } else if (fl.l4) {
             v = chk == 0 ? AIPSTACK_RX_ACCEPT : AIPSTACK_RX_DROP_L4_CHKSUM;
         }
-        if (lane < cnt)
+        if (!SPLIT && lane < cnt)  // split Tx: the status travels in the record
             status[p0 + lane] = (uint8_t)v;
     }
 }
 
-template <bool TX>
+template <bool TX, bool SPLIT = false>
 int launch_frames(const void *d_base, const uint64_t *d_offsets, uint64_t n, uint8_t *d_status,
-                  hipStream_t stream) {
+                  uint64_t *d_records, hipStream_t stream) {
     const uint64_t nchunks = (n + kWave - 1) / kWave;
     const int cus = device_cu_count();
     if (cus <= 0) return AIPSTACK_CHKSUM_EHIP;
@@ -359,8 +416,8 @@ int launch_frames(const void *d_base, const uint64_t *d_offsets, uint64_t n, uin
     CsrDesc desc{(uint64_t)(uintptr_t)d_base, d_offsets};
     const int su = tuning_stream_windows(8);  // measured: 8 > 4 > off > 2 (RX and TX)
 #define AIPSTACK_LAUNCH_FRAMES(P, SU)                                                          \
-    hipLaunchKernelGGL((frame_kernel<TX, 2, P, true, SU>), dim3((unsigned)blocks), dim3(kBlock), \
-                       0, stream, desc, n, (uint32_t)cpw, d_status)
+    hipLaunchKernelGGL((frame_kernel<TX, 2, P, true, SU, SPLIT>), dim3((unsigned)blocks),        \
+                       dim3(kBlock), 0, stream, desc, n, (uint32_t)cpw, d_status, d_records)
 #define AIPSTACK_LAUNCH_FRAMES_SU(P)              \
     switch (su) {                                 \
         case 0: AIPSTACK_LAUNCH_FRAMES(P, 0); break; \
@@ -375,6 +432,13 @@ int launch_frames(const void *d_base, const uint64_t *d_offsets, uint64_t n, uin
     }
 #undef AIPSTACK_LAUNCH_FRAMES_SU
 #undef AIPSTACK_LAUNCH_FRAMES
+    if constexpr (SPLIT) {
+        const int st = check_hip(hipGetLastError());
+        if (st != AIPSTACK_CHKSUM_OK) return st;
+        const uint64_t sblocks = min((n + kBlock - 1) / kBlock, (uint64_t)cus * 64);
+        hipLaunchKernelGGL(tx_scatter_kernel, dim3((unsigned)sblocks), dim3(kBlock), 0, stream,
+                           desc.base, d_offsets, d_records, d_status, n);
+    }
     return check_hip(hipGetLastError());
 }
 
@@ -387,12 +451,28 @@ extern "C" int aipstack_chksum_rx_verify(const void *d_base, const uint64_t *d_o
                                          uint8_t *d_verdict, void *stream) {
     if (n == 0) return AIPSTACK_CHKSUM_OK;
     if (!d_base || !d_offsets || !d_verdict || n > (1ull << 40)) return AIPSTACK_CHKSUM_EINVAL;
-    return launch_frames<false>(d_base, d_offsets, n, d_verdict, (hipStream_t)stream);
+    return launch_frames<false>(d_base, d_offsets, n, d_verdict, nullptr, (hipStream_t)stream);
 }
 
 extern "C" int aipstack_chksum_tx_fill(void *d_base, const uint64_t *d_offsets, uint64_t n,
                                        uint8_t *d_status, void *stream) {
     if (n == 0) return AIPSTACK_CHKSUM_OK;
     if (!d_base || !d_offsets || !d_status || n > (1ull << 40)) return AIPSTACK_CHKSUM_EINVAL;
-    return launch_frames<true>(d_base, d_offsets, n, d_status, (hipStream_t)stream);
+    return launch_frames<true>(d_base, d_offsets, n, d_status, nullptr, (hipStream_t)stream);
+}
+
+extern "C" uint64_t aipstack_chksum_tx_fill_workspace_bytes(uint64_t n) {
+    return n * sizeof(uint64_t);
+}
+
+extern "C" int aipstack_chksum_tx_fill_split(void *d_base, const uint64_t *d_offsets, uint64_t n,
+                                             uint8_t *d_status, void *d_workspace,
+                                             uint64_t workspace_bytes, void *stream) {
+    if (n == 0) return AIPSTACK_CHKSUM_OK;
+    if (!d_base || !d_offsets || !d_status || !d_workspace || n > (1ull << 40) ||
+        workspace_bytes < aipstack_chksum_tx_fill_workspace_bytes(n) ||
+        ((uintptr_t)d_workspace & 7u) != 0)
+        return AIPSTACK_CHKSUM_EINVAL;
+    return launch_frames<true, true>(d_base, d_offsets, n, d_status,
+                                     static_cast<uint64_t *>(d_workspace), (hipStream_t)stream);
 }

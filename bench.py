@@ -96,6 +96,8 @@ def parse():
                         "(host-memory streaming engine; PCIe-inclusive). Prints its own line.")
     p.add_argument("--e2e-pageable", action="store_true",
                    help="with --e2e: do not page-lock the host batch (CPU copy to staging)")
+    p.add_argument("--tx-inplace", action="store_true",
+                   help="TX: the one-pass in-place fill (default: the two-pass split fill)")
     p.add_argument("--e2e-streams", type=int, default=4)
     p.add_argument("--e2e-chunk-mib", type=int, default=64)
     return p.parse_args()
@@ -337,6 +339,7 @@ def main():
         buf = torch.from_numpy(frames_host).to(dev)
         d_off = torch.from_numpy(spec["offsets"]).to(dev)
         status = torch.empty(n, dtype=torch.uint8, device=dev)
+        tx_ws = torch.empty(8 * n, dtype=torch.uint8, device=dev)  # split fill's records
     if layout == "chain":
         chain = make_chains(spec, dev)
         spec["total"] = chain["payload"]
@@ -363,7 +366,8 @@ def main():
             A.chksum_batch_chain(chain["addr"], chain["len"], chain["index"], chain["states"],
                                  out=out, final=True, stream=stream)
         else:  # tx: idempotent (the filled fields are excluded from their own sums)
-            A.tx_fill(buf, d_off, out=status, stream=stream)
+            A.tx_fill(buf, d_off, out=status, stream=stream, split=not args.tx_inplace,
+                      workspace=tx_ws)
 
     for _ in range(args.warmup):
         step()
@@ -453,6 +457,8 @@ def main():
             "payload_bytes_per_gpu": payload,
             "layout": layout,
             "parallelism": f"disjoint packet shards x{world}, no collective",
+            **({"tx_fill": "in-place, one pass" if args.tx_inplace else
+                "split: read pass + scatter pass (both timed)"} if layout == "tx" else {}),
         },
         "roofline": {
             "bound": "hbm",

@@ -128,6 +128,17 @@ int aipstack_chksum_rx_verify(const void *d_base, const uint64_t *d_offsets, uin
 int aipstack_chksum_tx_fill(void *d_base, const uint64_t *d_offsets, uint64_t n,
                             uint8_t *d_status, void *stream);
 
+/* Tx fill in two stream-ordered passes, same results as aipstack_chksum_tx_fill: a read pass
+ * computes every frame's fields into d_workspace (8 bytes per frame, 8-byte aligned, at
+ * least aipstack_chksum_tx_fill_workspace_bytes(n) bytes, owned by the caller and free
+ * again once the stream passes the call), then a scatter pass stores them into the frames.
+ * Faster on large batches: field stores interleaved with the read stream cost several
+ * times what they cost as a pass of their own. */
+uint64_t aipstack_chksum_tx_fill_workspace_bytes(uint64_t n);
+int aipstack_chksum_tx_fill_split(void *d_base, const uint64_t *d_offsets, uint64_t n,
+                                  uint8_t *d_status, void *d_workspace,
+                                  uint64_t workspace_bytes, void *stream);
+
 /* ---- 3. host-memory streaming engine ----------------------------------------------- */
 
 /* The reference's packet path starts and ends in host memory (TAP read()/write(),

@@ -76,6 +76,12 @@ def test_argument_validation_without_gpu():
     assert lib.aipstack_chksum_batch_strided(p, 1, 65536, 1, o, 0, None) == A.AIPSTACK_CHKSUM_EINVAL
     assert lib.aipstack_chksum_batch_csr(p, None, 1, o, 0, None) == A.AIPSTACK_CHKSUM_EINVAL
     assert lib.aipstack_chksum_batch_seeded_csr(p, p, None, 1, o, None) == A.AIPSTACK_CHKSUM_EINVAL
+    # split Tx fill: 8 workspace bytes per frame, 8-byte aligned, checked before any launch
+    assert lib.aipstack_chksum_tx_fill_workspace_bytes(1000) == 8000
+    assert lib.aipstack_chksum_tx_fill_split(p, p, 0, o, None, 0, None) == 0
+    assert lib.aipstack_chksum_tx_fill_split(p, p, 2, o, o, 15, None) == A.AIPSTACK_CHKSUM_EINVAL
+    assert lib.aipstack_chksum_tx_fill_split(p, p, 2, o, None, 16, None) == A.AIPSTACK_CHKSUM_EINVAL
+    assert lib.aipstack_chksum_tx_fill_split(p, p, 1, o, o + 1, 15, None) == A.AIPSTACK_CHKSUM_EINVAL
 
 
 def test_python_batch_api_requires_device_tensors():

@@ -489,13 +489,14 @@ def _corrupt(buf, off, frac, seed):
         buf[j] ^= np.uint8(1 << int(rng.integers(0, 8)))
 
 
+@pytest.mark.parametrize("split", [False, True])
 @pytest.mark.parametrize("su", [0, -1])
 @pytest.mark.parametrize("n,maxp", [(200000, 1460), (20000, 9000)])
-def test_tx_fill_matches_oracle(oracle, stream_mode, n, maxp, su):
+def test_tx_fill_matches_oracle(oracle, stream_mode, n, maxp, su, split):
     stream_mode(su)
     buf, off = synth.frames_host(n, seed=11, max_payload=maxp)
     dbuf, doff = _d(buf), _d(off)
-    st = _np(A.tx_fill(dbuf, doff))
+    st = _np(A.tx_fill(dbuf, doff, split=split))
     want_buf = buf.copy()
     want_st = oracle.tx_fill_batch(want_buf, off)
     assert np.array_equal(st, want_st)
@@ -522,6 +523,25 @@ def test_rx_verify_matches_oracle(oracle, stream_mode, n, maxp, su):
     assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
     kinds = set(np.unique(want).tolist())
     assert {0, 2, 3, 5, 6, 7, 8} <= kinds          # the verdicts this mix must reach
+
+
+def test_tx_fill_split_workspace_and_ragged_counts(oracle):
+    """Split Tx fill with a caller workspace (reused across calls, larger than needed, at
+    an 8-byte-aligned offset of a bigger tensor) at ragged frame counts; idempotent."""
+    import torch
+    ws = torch.empty(8 * 5000 + 64, dtype=torch.uint8, device="cuda")
+    for n in (1, 63, 64, 65, 4097):
+        buf, off = synth.frames_host(n, seed=100 + n)
+        dbuf, doff = _d(buf), _d(off)
+        st = _np(A.tx_fill(dbuf, doff, workspace=ws[8:]))
+        want = buf.copy()
+        want_st = oracle.tx_fill_batch(want, off)
+        assert np.array_equal(st, want_st)
+        assert np.array_equal(_np(dbuf), want)
+        st2 = _np(A.tx_fill(dbuf, doff, workspace=ws[8:]))  # fill is idempotent
+        assert np.array_equal(st2, want_st) and np.array_equal(_np(dbuf), want)
+    with pytest.raises(A.ChksumError):
+        A.tx_fill(dbuf, doff, workspace=ws[: 8 * n - 8])
 
 
 def test_fill_then_verify_on_gpu():
@@ -554,15 +574,16 @@ def test_rx_verify_edge_frames(oracle, stream_mode, shift, su):
     assert np.all(np.bincount(want, minlength=9) > 0)
 
 
+@pytest.mark.parametrize("split", [False, True])
 @pytest.mark.parametrize("su", [0, 2, -1])
 @pytest.mark.parametrize("shift", [0, 3])
-def test_tx_fill_edge_frames(oracle, stream_mode, shift, su):
+def test_tx_fill_edge_frames(oracle, stream_mode, shift, su, split):
     stream_mode(su)
     buf, off = _edge_frames(7 + shift, 3000)
     big = np.zeros(buf.size + shift, dtype=np.uint8)
     big[shift:] = buf
     dbig = _d(big)
-    st = _np(A.tx_fill(dbig, _d(off + np.uint64(shift))))
+    st = _np(A.tx_fill(dbig, _d(off + np.uint64(shift)), split=split))
     want = buf.copy()
     want_st = oracle.tx_fill_batch(want, off)
     assert np.array_equal(st, want_st)

@@ -41,6 +41,8 @@ def main():
     ap.add_argument("--variants", default=None,
                     help='"U,P,NT,WPC[,SU];..." or, for RX/TX, "F,WPC[,SU];..." (0 = automatic; '
                          'SU = stream-mode windows 2/4/8, -1 = stream mode off)')
+    ap.add_argument("--tx-inplace", action="store_true",
+                    help="TX: the one-pass in-place fill (default: split)")
     ap.add_argument("--lib", default=None,
                     help="load this build of libaipstack_chksum.so instead (experiments)")
     args = ap.parse_args()
@@ -99,11 +101,14 @@ def main():
     out = torch.empty(n, dtype=torch.uint8 if layout in ("rx", "tx") else torch.uint16,
                       device=dev)
 
+    tx_ws = torch.empty(8 * n, dtype=torch.uint8, device=dev) if layout == "tx" else None
+
     def run():
         if layout == "rx":
             A.rx_verify(buf, d_off, out=out, stream=stream)
         elif layout == "tx":
-            A.tx_fill(buf, d_off, out=out, stream=stream)
+            A.tx_fill(buf, d_off, out=out, stream=stream, split=not args.tx_inplace,
+                      workspace=tx_ws)
         elif layout == "strided":
             A.chksum_batch_strided(buf, plen, plen, n, out=out, stream=stream)
         else:
