@@ -20,32 +20,34 @@ import os
 import statistics
 import sys
 
-HOT_KERNELS = ("chksum_batch_kernel", "chksum_chain_kernel", "frame_kernel")
+HOT_KERNELS = ("chksum_batch_kernel", "chksum_chain_kernel", "frame_kernel",
+               "tx_scatter_kernel")  # split Tx fill: read pass + scatter pass, summed
 COUNTERS = ("FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_SALU", "SQ_INSTS_VALU", "SQ_WAVE_CYCLES",
             "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY")
 
 
 def per_dispatch(csv_path):
-    """{counter: [value per hot-kernel dispatch, in dispatch order]}"""
+    """{(hot kernel, counter): [value per dispatch of that kernel, in dispatch order]}"""
     acc = {}
     with open(csv_path) as f:
         for row in csv.DictReader(f):
-            if not any(k in row["Kernel_Name"] for k in HOT_KERNELS):
+            kern = next((k for k in HOT_KERNELS if k in row["Kernel_Name"]), None)
+            if kern is None:
                 continue
-            key = (int(row["Dispatch_Id"]), row["Counter_Name"])
+            key = (kern, int(row["Dispatch_Id"]), row["Counter_Name"])
             acc[key] = acc.get(key, 0.0) + float(row["Counter_Value"])
     out = {}
-    for (disp, name), v in sorted(acc.items()):
-        out.setdefault(name, []).append(v)
+    for (kern, disp, name), v in sorted(acc.items()):
+        out.setdefault((kern, name), []).append(v)
     return out
 
 
 def summarise(round_dir, cfg):
     vals = {}
     for path in glob.glob(os.path.join(round_dir, f"pmc_{cfg}", "*", "run_counter_collection.csv")):
-        for name, series in per_dispatch(path).items():
+        for (kern, name), series in per_dispatch(path).items():  # a step's kernels summed
             warm = series[1:] if len(series) > 1 else series
-            vals[name] = statistics.median(warm)
+            vals[name] = vals.get(name, 0.0) + statistics.median(warm)
     if "FETCH_SIZE" not in vals or "WRITE_SIZE" not in vals:
         return None
     hbm = int(round((2 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024))
