@@ -202,6 +202,24 @@ struct BatchChksum {
             reinterpret_cast<std::uint32_t const *>(d_states), n, d_out,
             final_chksum ? AIPSTACK_CHKSUM_FINAL : 0u, stream);
     }
+    // Raw Ethernet frames at CSR offsets: receive verdicts / send-side fill (AIPSTACK_RX_*).
+    static int rxVerify(void const *d_frames, std::uint64_t const *d_offsets, std::uint64_t n,
+                        std::uint8_t *d_verdict, void *stream = nullptr) {
+        return aipstack_chksum_rx_verify(d_frames, d_offsets, n, d_verdict, stream);
+    }
+    static int txFill(void *d_frames, std::uint64_t const *d_offsets, std::uint64_t n,
+                      std::uint8_t *d_status, void *stream = nullptr) {
+        return aipstack_chksum_tx_fill(d_frames, d_offsets, n, d_status, stream);
+    }
+    static std::uint64_t txFillWorkspaceBytes(std::uint64_t n) {
+        return aipstack_chksum_tx_fill_workspace_bytes(n);
+    }
+    static int txFillSplit(void *d_frames, std::uint64_t const *d_offsets, std::uint64_t n,
+                           std::uint8_t *d_status, void *d_workspace,
+                           std::uint64_t workspace_bytes, void *stream = nullptr) {
+        return aipstack_chksum_tx_fill_split(d_frames, d_offsets, n, d_status, d_workspace,
+                                             workspace_bytes, stream);
+    }
 };
 
 }  // namespace AIpStackAmd

@@ -14,6 +14,7 @@
 #include "aipstack_amd/chksum.h"
 #include "aipstack_amd/synth.h"
 #include "chksum_oracle.h"
+#include "frame_oracle.h"
 
 #define HIP_OK(x)                                                                  \
     do {                                                                           \
@@ -113,6 +114,56 @@ int main() {
     oracle_batch_seeded_csr(h.data(), off.data(), states.data(), n, want.data());
     for (uint64_t i = 0; i < n; i++)
         EXPECT(got[i] == want[i], "seeded i=%lu got %04x want %04x", (unsigned long)i, got[i], want[i]);
+
+    // ---- frames: Rx verify, Tx fill in one pass and split (caller workspace), vs the frame
+    // oracle (oracle/frame_oracle.c); the frames start 3 bytes into the device buffer
+    {
+        const uint64_t nf = 50000;
+        std::vector<uint64_t> foff(nf + 1);
+        const uint64_t fbytes = aipstack_synth_frames_host(nullptr, foff.data(), nf, 21, 1460);
+        std::vector<unsigned char> fh(fbytes + 3);
+        aipstack_synth_frames_host(fh.data() + 3, foff.data(), nf, 21, 1460);
+        std::vector<uint64_t> foff3(foff);
+        for (auto &o : foff3) o += 3;
+        unsigned char *dfr = nullptr;
+        uint64_t *dfoff = nullptr, *dws = nullptr;
+        uint8_t *dst = nullptr;
+        HIP_OK(hipMalloc(&dfr, fh.size()));
+        HIP_OK(hipMalloc(&dfoff, (nf + 1) * 8));
+        HIP_OK(hipMalloc(&dst, nf));
+        const uint64_t ws = aipstack_chksum_tx_fill_workspace_bytes(nf);
+        HIP_OK(hipMalloc(&dws, ws));
+        HIP_OK(hipMemcpy(dfoff, foff3.data(), (nf + 1) * 8, hipMemcpyHostToDevice));
+        std::vector<unsigned char> want_fr(fh), got_fr(fh.size());
+        std::vector<uint8_t> want_st(nf), got_st(nf);
+        oracle_tx_fill_batch(want_fr.data(), foff3.data(), nf, want_st.data());
+        for (int split = 0; split < 2; split++) {
+            HIP_OK(hipMemcpy(dfr, fh.data(), fh.size(), hipMemcpyHostToDevice));
+            st = split ? aipstack_chksum_tx_fill_split(dfr, dfoff, nf, dst, dws, ws, stream)
+                       : aipstack_chksum_tx_fill(dfr, dfoff, nf, dst, stream);
+            EXPECT(st == 0, "tx_fill (split %d) launch failed %d", split, st);
+            HIP_OK(hipMemcpyAsync(got_fr.data(), dfr, fh.size(), hipMemcpyDeviceToHost, stream));
+            HIP_OK(hipMemcpyAsync(got_st.data(), dst, nf, hipMemcpyDeviceToHost, stream));
+            HIP_OK(hipStreamSynchronize(stream));
+            EXPECT(got_fr == want_fr, "tx_fill (split %d): frame bytes differ from the oracle", split);
+            EXPECT(got_st == want_st, "tx_fill (split %d): statuses differ from the oracle", split);
+        }
+        // the filled frames verify; then flip one byte in every 7th frame
+        for (uint64_t i = 0; i < nf; i += 7) got_fr[foff3[i] + (foff3[i + 1] - foff3[i]) / 2] ^= 0x10;
+        HIP_OK(hipMemcpy(dfr, got_fr.data(), fh.size(), hipMemcpyHostToDevice));
+        st = aipstack_chksum_rx_verify(dfr, dfoff, nf, dst, stream);
+        EXPECT(st == 0, "rx_verify launch failed %d", st);
+        HIP_OK(hipMemcpyAsync(got_st.data(), dst, nf, hipMemcpyDeviceToHost, stream));
+        HIP_OK(hipStreamSynchronize(stream));
+        oracle_rx_verify_batch(got_fr.data(), foff3.data(), nf, want_st.data());
+        EXPECT(got_st == want_st, "rx_verify: verdicts differ from the oracle");
+        EXPECT(aipstack_chksum_tx_fill_split(dfr, dfoff, nf, dst, dws, ws - 8, stream) ==
+                   AIPSTACK_CHKSUM_EINVAL, "split fill: short workspace accepted");
+        HIP_OK(hipFree(dfr));
+        HIP_OK(hipFree(dfoff));
+        HIP_OK(hipFree(dst));
+        HIP_OK(hipFree(dws));
+    }
 
     // ---- argument errors are reported, not executed
     EXPECT(aipstack_chksum_batch_strided(nullptr, 1, 1, 1, dout, 0, stream) == AIPSTACK_CHKSUM_EINVAL, "null base");
