@@ -267,6 +267,19 @@ def _require_device(t, name: str) -> None:
         raise ValueError(f"{name} must be contiguous")
 
 
+def _require_offsets(offsets, name: str = "offsets") -> None:
+    """CSR offsets: a contiguous device tensor of 64-bit integers (the C-ABI reads uint64)."""
+    torch = _torch()
+    _require_device(offsets, name)
+    if offsets.dtype not in (torch.int64, torch.uint64):
+        raise ValueError(f"{name} must be an int64/uint64 device tensor")
+
+
+def _same_device(a, b, names: str) -> None:
+    if a.device != b.device:
+        raise ValueError(f"{names} must be on the same device")
+
+
 def _out_tensor(out, n: int, like):
     torch = _torch()
     if out is None:
@@ -274,6 +287,7 @@ def _out_tensor(out, n: int, like):
     _require_device(out, "out")
     if out.dtype not in (torch.uint16, torch.int16) or out.numel() < n:
         raise ValueError("out must be a uint16/int16 device tensor with >= n elements")
+    _same_device(out, like, "out and the input")
     return out
 
 
@@ -296,7 +310,8 @@ def chksum_batch_csr(buf, offsets, *, out=None, final: bool = False, stream=None
     """``out[i] = IpChksumInverted(buf[offsets[i]:offsets[i+1]])`` on the GPU. ``offsets``
     is a device int64/uint64 tensor of n+1 non-decreasing byte offsets."""
     _require_device(buf, "buf")
-    _require_device(offsets, "offsets")
+    _require_offsets(offsets)
+    _same_device(buf, offsets, "buf and offsets")
     n = offsets.numel() - 1
     if n < 0:
         raise ValueError("offsets must hold n+1 entries")
@@ -312,9 +327,13 @@ def chksum_batch_seeded_csr(buf, offsets, states, *, out=None, stream=None):
     """``out[i] = IpChksumAccumulator(State(states[i])).getChksum(IpBufRef(packet i))`` on
     the GPU (final checksum). ``states`` is a device int32/uint32 tensor of n states."""
     _require_device(buf, "buf")
-    _require_device(offsets, "offsets")
+    _require_offsets(offsets)
     _require_device(states, "states")
+    _same_device(buf, offsets, "buf and offsets")
+    _same_device(buf, states, "buf and states")
     n = offsets.numel() - 1
+    if n < 0:
+        raise ValueError("offsets must hold n+1 entries")
     if states.numel() < n or states.element_size() != 4:
         raise ValueError("states must hold n 32-bit entries")
     out = _out_tensor(out, n, buf)
@@ -368,11 +387,22 @@ class ChksumEngine:
                "aipstack_chksum_engine_unregister")
         self._registered = [a for a in self._registered if a is not arr]
 
+    @staticmethod
+    def _host_args(buf: np.ndarray, out, n: int) -> np.ndarray:
+        if not isinstance(buf, np.ndarray) or not buf.flags.c_contiguous:
+            raise ValueError("buf must be a C-contiguous numpy array")
+        if out is None:
+            return np.empty(max(n, 0), dtype=np.uint16)
+        if (not isinstance(out, np.ndarray) or out.dtype != np.uint16
+                or not out.flags.c_contiguous or not out.flags.writeable or out.size < n):
+            raise ValueError("out must be a writable C-contiguous uint16 array of >= n elements")
+        return out
+
     def strided(self, buf: np.ndarray, stride: int, length: int, n: int, *, out=None,
                 final: bool = False) -> np.ndarray:
         if n and (n - 1) * stride + length > buf.nbytes:
             raise ValueError("batch exceeds buf")
-        out = np.empty(n, dtype=np.uint16) if out is None else out
+        out = self._host_args(buf, out, n)
         _check(self._lib.aipstack_chksum_engine_host_strided(
             self._h, buf.ctypes.data, stride, length, n, out.ctypes.data,
             AIPSTACK_CHKSUM_FINAL if final else 0), "aipstack_chksum_engine_host_strided")
@@ -384,7 +414,7 @@ class ChksumEngine:
         n = o.size - 1
         if n > 0 and int(o[-1]) > buf.nbytes:
             raise ValueError("offsets exceed buf")
-        out = np.empty(max(n, 0), dtype=np.uint16) if out is None else out
+        out = self._host_args(buf, out, n)
         _check(self._lib.aipstack_chksum_engine_host_csr(
             self._h, buf.ctypes.data, o.ctypes.data, n, out.ctypes.data,
             AIPSTACK_CHKSUM_FINAL if final else 0), "aipstack_chksum_engine_host_csr")
@@ -428,6 +458,7 @@ def _u8_out(out, n, like):
     _require_device(out, "out")
     if out.element_size() != 1 or out.numel() < n:
         raise ValueError("out must be a uint8 device tensor with >= n elements")
+    _same_device(out, like, "out and frames")
     return out
 
 
@@ -435,7 +466,8 @@ def rx_verify(frames, offsets, *, out=None, stream=None):
     """Rx verify on the GPU: frame i = ``frames[offsets[i]:offsets[i+1]]`` (raw Ethernet);
     returns one AIPSTACK_RX_* verdict per frame (uint8 device tensor). Read-only."""
     _require_device(frames, "frames")
-    _require_device(offsets, "offsets")
+    _require_offsets(offsets)
+    _same_device(frames, offsets, "frames and offsets")
     n = offsets.numel() - 1
     out = _u8_out(out, max(n, 0), frames)
     _check(_lib.load().aipstack_chksum_rx_verify(frames.data_ptr(), offsets.data_ptr(), n,
@@ -453,7 +485,8 @@ def tx_fill(frames, offsets, *, out=None, stream=None, split=True, workspace=Non
     bytes, else one is taken from torch's allocator); ``split=False`` the one-pass
     ``aipstack_chksum_tx_fill``. Both write the same bytes."""
     _require_device(frames, "frames")
-    _require_device(offsets, "offsets")
+    _require_offsets(offsets)
+    _same_device(frames, offsets, "frames and offsets")
     n = offsets.numel() - 1
     out = _u8_out(out, max(n, 0), frames)
     lib = _lib.load()
@@ -462,16 +495,23 @@ def tx_fill(frames, offsets, *, out=None, stream=None, split=True, workspace=Non
                                            out.data_ptr(), _stream_handle(stream)),
                "aipstack_chksum_tx_fill")
         return out
+    torch = _torch()
     need = int(lib.aipstack_chksum_tx_fill_workspace_bytes(max(n, 0)))
     if workspace is None:
-        workspace = _torch().empty(max(need, 8), dtype=_torch().uint8, device=frames.device)
+        workspace = torch.empty(max(need, 8), dtype=torch.uint8, device=frames.device)
     else:
         _require_device(workspace, "workspace")
+        _same_device(frames, workspace, "frames and workspace")
     ws_bytes = workspace.numel() * workspace.element_size()
+    launch_stream = torch.cuda.current_stream(frames.device) if stream is None else stream
     _check(lib.aipstack_chksum_tx_fill_split(frames.data_ptr(), offsets.data_ptr(), n,
                                              out.data_ptr(), workspace.data_ptr(), ws_bytes,
-                                             _stream_handle(stream)),
+                                             _stream_handle(launch_stream)),
            "aipstack_chksum_tx_fill_split")
+    # The caching allocator must not hand the workspace out again before both passes on
+    # the launch stream are done with it (it may not be torch's current stream).
+    if hasattr(launch_stream, "cuda_stream"):
+        workspace.record_stream(launch_stream)
     return out
 
 

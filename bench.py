@@ -38,6 +38,8 @@ CONFIGS = {
     # name: (layout, packets per GPU, packet bytes (strided) / None (mixed))
     "A": ("strided", 1 << 20, 1500),
     "B": ("strided", 256 << 10, 9000),
+    # config A's packets in 2048-B ring slots (stride != len: the per-packet wave mode)
+    "A2K": ("strided", 1 << 20, 1500),
     "C": ("csr", 2 << 20, None),
     # SURVEY 8(f) rows 2-3 (not BASELINE metric lines): raw Ethernet frames
     "RX": ("rx", 1 << 20, None),
@@ -45,9 +47,12 @@ CONFIGS = {
     # chained + seeded (TCP Tx shape)
     "CHAIN": ("chain", 1 << 20, None),
 }
+SLOT_STRIDE = {"A2K": 2048}  # strided configs whose packets do not lie back to back
 WORKLOAD_NAMES = {
     "A": "1M x 1500B Ethernet-MTU packets per GPU, IP checksum (BASELINE configs[1]; x8 = configs[4])",
     "B": "256K x 9000B jumbo packets per GPU, IP checksum (BASELINE configs[2])",
+    "A2K": "1M x 1500B packets per GPU in 2048B ring slots (stride != length: one packet per "
+           "wavefront), IP checksum",
     "C": "2M mixed 64-1500B packets per GPU incl. odd lengths/starts, CSR (BASELINE configs[3])",
     "RX": "1M raw Ethernet frames per GPU (TCP/UDP/ICMP/other/ARP/fragments, 0-1460B payload), "
           "Rx verify: IPv4 header + L4 checksum verdicts",
@@ -116,8 +121,11 @@ def shard_spec(config, rank, world, n=None):
     n = n_default if n is None else n
     spec = {"layout": layout, "n": n, "plen": plen, "first_packet": rank * n}
     if layout == "strided":
-        spec["total"] = n * plen
-        spec["byte_offset"] = rank * n * plen
+        stride = SLOT_STRIDE.get(config, plen)
+        spec["stride"] = stride
+        spec["total"] = n * stride      # buffer bytes (slot gaps hold bytes no packet covers)
+        spec["payload"] = n * plen
+        spec["byte_offset"] = rank * n * stride
         spec["offsets"] = None
     elif layout in ("rx", "tx", "chain"):
         # each rank synthesises its own frames / chains (seed per rank): they are independent
@@ -221,11 +229,12 @@ def chain_check(chain, got):
 def cpu_baseline(spec):
     """Reference scalar path on the host; bounded sample = this rank's whole batch."""
     layout, n, plen, off_host = spec["layout"], spec["n"], spec["plen"], spec["offsets"]
-    total = spec["total"]
+    total = spec.get("payload", spec["total"])
+    stride = spec.get("stride", plen)
     host = host_shard(spec)
     out = np.empty(n, dtype=np.uint16)
     ref_path = os.path.join(ROOT, "oracle", "_ref", "libref_chksum.so")
-    cores_all = min(16, os.cpu_count() or 1)
+    cores_all = _affinity_cores()  # every core this process may run on
     if os.path.exists(ref_path):
         kind = "reference"
         lib = ctypes.CDLL(ref_path)
@@ -242,7 +251,7 @@ def cpu_baseline(spec):
                 o = off_host.astype(np.uint64)
                 return lib.ref_time_batch_csr(threads, reps, host.ctypes.data, o.ctypes.data, n,
                                               out.ctypes.data)
-            return lib.ref_time_batch_strided(threads, reps, host.ctypes.data, plen, plen, n,
+            return lib.ref_time_batch_strided(threads, reps, host.ctypes.data, stride, plen, n,
                                               out.ctypes.data)
     else:  # the C restatement (oracle/), single thread
         kind = "port"
@@ -261,7 +270,7 @@ def cpu_baseline(spec):
                 if layout == "csr":
                     lib.oracle_batch_csr(host.ctypes.data, o.ctypes.data, n, out.ctypes.data, 0)
                 else:
-                    lib.oracle_batch_strided(host.ctypes.data, plen, plen, n, out.ctypes.data, 0)
+                    lib.oracle_batch_strided(host.ctypes.data, stride, plen, n, out.ctypes.data, 0)
                 ts.append(time.perf_counter() - t0)
             return float(np.median(ts[1:]))
     t1 = timed(1, CPU_REPS)
@@ -270,16 +279,28 @@ def cpu_baseline(spec):
         "unit": "GiB/s",
         "cores": 1,
         "kind": kind,
-        "sample": f"this rank's whole batch ({n} packets, {total} B) in host memory, "
+        "sample": f"this rank's whole batch ({n} packets, {total} B of packets) in host memory, "
                   f"median of {CPU_REPS} passes after 1 warm-up, 1 thread"
                   + (" (reference Chksum.h:77-99 compiled -O2 from /root/reference)"
                      if kind == "reference" else " (oracle/chksum_oracle.c port)"),
     }
     if cores_all > 1:
         tn = timed(cores_all, 5)
-        res["all_cores"] = {"value": round(total / tn / 2**30, 3), "cores": cores_all}
+        res["all_cores"] = {"value": round(total / tn / 2**30, 3), "cores": cores_all,
+                            "threads": cores_all,
+                            "sample": "same batch, disjoint packet ranges per std::thread, "
+                                      "median of 5 passes"}
     res["cpu_model"] = _cpu_model()
+    res["nproc"] = os.cpu_count()
+    res["affinity_cores"] = _affinity_cores()
     return res, out
+
+
+def _affinity_cores():
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
 
 
 def _cpu_model():
@@ -346,6 +367,7 @@ def main():
     off_host = spec["offsets"]
     byte_offset = spec["byte_offset"]
     total = spec["total"]
+    stride = spec.get("stride", plen)
     if layout in ("strided", "csr"):
         buf = torch.empty(total, dtype=torch.uint8, device=dev)
         synth.fill_device(buf, synth.SEED_DATA, byte_offset)
@@ -357,7 +379,7 @@ def main():
 
     def step():
         if layout == "strided":
-            A.chksum_batch_strided(buf, plen, plen, n, out=out, stream=stream)
+            A.chksum_batch_strided(buf, stride, plen, n, out=out, stream=stream)
         elif layout == "csr":
             A.chksum_batch_csr(buf, d_off, out=out, stream=stream)
         elif layout == "rx":
@@ -410,7 +432,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     max_elapsed = float(t.item())
 
-    payload = total
+    payload = spec.get("payload", total)
     alg = algorithmic_bytes(layout, n, payload)
 
     # ---- parity of this run's output against the oracle / reference (rank 0 sample)
@@ -423,8 +445,10 @@ def main():
         if not args.no_parity:
             parity = chain_check(chain, out.cpu().numpy())
     elif rank == 0:
+        # rank 0 times the CPU baseline on its own shard at every world size (after the
+        # timed region; the other ranks wait at the final barrier)
         host_out = out.cpu().numpy()
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline:
             cpu, want = cpu_baseline(spec)
             if not args.no_parity:
                 parity = "bit-exact" if np.array_equal(host_out, want) else "MISMATCH"
@@ -451,6 +475,7 @@ def main():
             "workload": WORKLOAD_NAMES[args.config],
             "config": args.config,
             "packets_per_gpu": n,
+            **({"slot_stride": stride} if layout == "strided" and stride != plen else {}),
             "packet_bytes": plen if plen else {"csr": "64-1500 (mixed)",
                                                 "chain": "20 + 1460 in 3 chunks"}.get(
                                                     layout, "60-1514 (frames)"),
@@ -490,7 +515,8 @@ def e2e(args, rank, world, local_rank, layout, n, plen):
     import aipstack_amd as A
     from aipstack_amd import synth
     spec = shard_spec(args.config, rank, world)
-    off, total = spec["offsets"], spec["total"]
+    off, total = spec["offsets"], spec.get("payload", spec["total"])
+    stride = spec.get("stride", plen)
     host = host_shard(spec)
     out = np.empty(n, dtype=np.uint16)
     eng = A.ChksumEngine(int(os.environ.get("AIPSTACK_BENCH_FORCE_DEVICE", local_rank)),
@@ -501,7 +527,7 @@ def e2e(args, rank, world, local_rank, layout, n, plen):
 
     def step():
         if layout == "strided":
-            eng.strided(host, plen, plen, n, out=out)
+            eng.strided(host, stride, plen, n, out=out)
         else:
             eng.csr(host, off, out=out)
 
@@ -516,18 +542,15 @@ def e2e(args, rank, world, local_rank, layout, n, plen):
     if world > 1:
         dist.barrier()
     import torch
-    # Diagnostic, AFTER the timed region (not part of `value`): per-launch event pairs,
-    # to expose outliers / clock ramps that the bracketed average smooths over.
+    # Diagnostic, AFTER the timed region (not part of `value`): wall time of each call
+    # (every engine call is synchronous: H2D, kernels and D2H of the whole batch).
     per_launch = []
     if args.per_launch:
-        pairs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                 for _ in range(args.steps)]
-        for a, b in pairs:
-            a.record(stream)
+        for _ in range(args.steps):
+            c0 = time.perf_counter()
             step()
-            b.record(stream)
-        torch.cuda.synchronize()
-        per_launch = sorted(a.elapsed_time(b) * 1e3 for a, b in pairs)
+            per_launch.append((time.perf_counter() - c0) * 1e6)
+        per_launch.sort()
 
     t = torch.tensor([elapsed], dtype=torch.float64)
     if world > 1:
@@ -540,7 +563,7 @@ def e2e(args, rank, world, local_rank, layout, n, plen):
         if layout == "strided":
             lib.oracle_batch_strided.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
                                                  ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32]
-            lib.oracle_batch_strided(host.ctypes.data, plen, plen, n, want.ctypes.data, 0)
+            lib.oracle_batch_strided(host.ctypes.data, stride, plen, n, want.ctypes.data, 0)
         else:
             lib.oracle_batch_csr.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                              ctypes.c_void_p, ctypes.c_uint32]
@@ -559,6 +582,9 @@ def e2e(args, rank, world, local_rank, layout, n, plen):
                        "host_memory": "pageable (CPU copy into pinned staging)"
                        if args.e2e_pageable else "registered (hipHostRegister, DMA direct)",
                        "streams": args.e2e_streams, "chunk_MiB": args.e2e_chunk_mib},
+            **({"per_call_us": {"min": round(per_launch[0], 1),
+                                "median": round(per_launch[len(per_launch) // 2], 1),
+                                "max": round(per_launch[-1], 1)}} if per_launch else {}),
             "parity": parity}), flush=True)
     eng.close()
     if world > 1:
@@ -588,7 +614,7 @@ def oracle_check(spec, got):
     if spec["layout"] == "strided":
         lib.oracle_batch_strided.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
                                              ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32]
-        lib.oracle_batch_strided(host.ctypes.data, spec["plen"], spec["plen"], n,
+        lib.oracle_batch_strided(host.ctypes.data, spec["stride"], spec["plen"], n,
                                  want.ctypes.data, 0)
     else:
         lib.oracle_batch_csr.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,

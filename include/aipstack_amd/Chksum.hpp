@@ -24,6 +24,13 @@
 
 namespace AIpStackAmd {
 
+// meta/BasicMetaUtils.h:39-42: the tag type the reference's addWord overloads take
+// (IpChksumAccumulator::addWord(WrapType<std::uint16_t>, ...), Chksum.h:191, 213).
+template <typename TType>
+struct WrapType {
+    using Type = TType;
+};
+
 // Chksum.h:122-125
 inline std::uint16_t IpChksum(char const *data, std::size_t len) {
     return std::uint16_t(~IpChksumInverted(data, len));
@@ -36,7 +43,7 @@ struct IpBufNode {
     IpBufNode const *next = nullptr;
 };
 
-// Buf.h:118-251 (the subset the checksum path uses)
+// Buf.h:118-251 (the members the checksum path and its callers use)
 struct IpBufRef {
     IpBufNode const *node = nullptr;
     std::size_t offset = 0;
@@ -46,6 +53,11 @@ struct IpBufRef {
     std::size_t getChunkLength() const {
         std::size_t rem = node->len - offset;
         return tot_len < rem ? tot_len : rem;
+    }
+    // Buf.h:186-191: at least `amount` bytes in the first chunk (the Rx paths' header
+    // checks, e.g. ip/IpStack.h:939, udp/IpUdpProto.h:473).
+    bool hasHeader(std::size_t amount) const {
+        return amount <= tot_len && amount <= node->len - offset;
     }
     IpBufRef hideHeader(std::size_t amount) const {
         return IpBufRef{node, offset + amount, tot_len - amount};
@@ -96,23 +108,29 @@ public:
     enum class State : std::uint32_t {};
 
     IpChksumAccumulator() : m_sum(0) {}
-    explicit IpChksumAccumulator(State state) : m_sum(std::uint32_t(state)) {}
+    // Chksum.h:171: implicit, as in the reference (`IpChksumAccumulator chksum = state;`).
+    IpChksumAccumulator(State state) : m_sum(std::uint32_t(state)) {}
 
     State getState() const { return State(m_sum); }
 
-    void addWord16(std::uint16_t word) { m_sum += word; }
+    // Chksum.h:191-217: the reference's tag-dispatched word adds.
+    void addWord(WrapType<std::uint16_t>, std::uint16_t word) { m_sum += word; }
+    void addWord(WrapType<std::uint32_t>, std::uint32_t word) {
+        addWord(WrapType<std::uint16_t>(), std::uint16_t(word >> 16));
+        addWord(WrapType<std::uint16_t>(), std::uint16_t(word));
+    }
     void addWordOctets(std::uint8_t hi, std::uint8_t lo) {
-        addWord16(std::uint16_t((std::uint16_t(hi) << 8) | lo));
+        addWord(WrapType<std::uint16_t>(), std::uint16_t((std::uint16_t(hi) << 8) | lo));
     }
-    void addWord32(std::uint32_t word) {
-        addWord16(std::uint16_t(word >> 16));
-        addWord16(std::uint16_t(word));
-    }
+    // Chksum.h:225-235 (num_bytes must be even, as the reference asserts at :227)
     void addEvenBytes(char const *ptr, std::size_t num_bytes) {
         unsigned char const *p = reinterpret_cast<unsigned char const *>(ptr);
         for (std::size_t i = 0; i + 1 < num_bytes; i += 2)
-            addWord16(std::uint16_t((std::uint16_t(p[i]) << 8) | p[i + 1]));
+            addWord(WrapType<std::uint16_t>(), std::uint16_t((std::uint16_t(p[i]) << 8) | p[i + 1]));
     }
+    // Shorthands for the two addWord overloads (not in the reference).
+    void addWord16(std::uint16_t word) { addWord(WrapType<std::uint16_t>(), word); }
+    void addWord32(std::uint32_t word) { addWord(WrapType<std::uint32_t>(), word); }
 
     std::uint16_t getChksum() {
         fold();

@@ -115,7 +115,12 @@ int aipstack_chksum_batch_chain(const uint64_t *d_chunk_addr, const uint32_t *d_
 #define AIPSTACK_RX_ACCEPT_OTHER       8 /* IPv4 header OK; protocol other than TCP/UDP/ICMP */
 
 /* Rx verify: frame i = bytes [d_offsets[i], d_offsets[i+1]) of d_base (an Ethernet frame,
- * as the TAP driver delivers it); d_verdict[i] = one of AIPSTACK_RX_*. Read-only. */
+ * as the TAP driver delivers it); d_verdict[i] = one of AIPSTACK_RX_*. Read-only.
+ * Frame offsets (here and in the Tx fills) are non-decreasing (n+1 entries) and each frame
+ * is at most 65535 bytes, so that 64 consecutive frames span at most 4 MiB: the kernels
+ * read a 64-frame chunk's header bytes through one range-checked window over that span.
+ * Offsets outside this contract give unspecified verdicts (never accesses outside the
+ * chunk's span). */
 int aipstack_chksum_rx_verify(const void *d_base, const uint64_t *d_offsets, uint64_t n,
                               uint8_t *d_verdict, void *stream);
 

@@ -129,3 +129,10 @@ double ref_time_batch_csr(int threads, int reps, const char *base,
 }
 
 } // extern "C"
+
+// The reference stack's checksum call sequences (tests/cpp/call_sites.inc, shared text with
+// tests/cpp/hpp_shim.cpp), compiled against the reference's AIpStack:: types as ref_cs_*.
+using AIpStack::IpChksum;
+using AIpStack::WrapType;
+#define CS_NAME(x) ref_cs_##x
+#include "call_sites.inc"

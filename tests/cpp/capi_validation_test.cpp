@@ -1,0 +1,106 @@
+// Host test program: the C-ABI's argument validation (include/aipstack_amd/chksum.h) --
+// every entry point rejects null pointers, oversize arguments and bad handles with
+// AIPSTACK_CHKSUM_EINVAL before touching a device, accepts n == 0 as a no-op, and the
+// host-memory engine fails cleanly (ENODEV / EHIP) where no gfx950 device is visible.
+// Built twice: plain (make -C tests/cpp) and under AddressSanitizer + UBSan together with
+// the whole library's host code (make -C tests/cpp asan). Runs on a host without a GPU;
+// with one, the device-dependent expectations switch to success.
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "aipstack_amd/chksum.h"
+
+#define CHECK(cond)                                                                  \
+    do {                                                                             \
+        if (!(cond)) {                                                               \
+            std::fprintf(stderr, "CHECK failed %s:%d: %s\n", __FILE__, __LINE__, #cond); \
+            std::abort();                                                            \
+        }                                                                            \
+    } while (0)
+
+int main() {
+    const int EINVAL_ = AIPSTACK_CHKSUM_EINVAL;
+    char dummy[64] = {0};
+    std::uint64_t off[2] = {0, 8};
+    std::uint16_t out[4];
+    std::uint8_t st[4];
+    std::uint32_t states[4] = {0};
+    std::uint32_t lens[4] = {1, 1, 1, 1};
+    std::uint64_t addrs[4] = {0};
+
+    // n == 0 is a no-op whatever the pointers
+    CHECK(aipstack_chksum_batch_strided(nullptr, 0, 0, 0, nullptr, 0, nullptr) == 0);
+    CHECK(aipstack_chksum_batch_csr(nullptr, nullptr, 0, nullptr, 0, nullptr) == 0);
+    CHECK(aipstack_chksum_batch_seeded_csr(nullptr, nullptr, nullptr, 0, nullptr, nullptr) == 0);
+    CHECK(aipstack_chksum_batch_chain(nullptr, nullptr, nullptr, nullptr, 0, nullptr, 0, nullptr) == 0);
+    CHECK(aipstack_chksum_rx_verify(nullptr, nullptr, 0, nullptr, nullptr) == 0);
+    CHECK(aipstack_chksum_tx_fill(nullptr, nullptr, 0, nullptr, nullptr) == 0);
+    CHECK(aipstack_chksum_tx_fill_split(nullptr, nullptr, 0, nullptr, nullptr, 0, nullptr) == 0);
+
+    // null pointers / bad sizes
+    CHECK(aipstack_chksum_batch_strided(nullptr, 1, 1, 1, out, 0, nullptr) == EINVAL_);
+    CHECK(aipstack_chksum_batch_strided(dummy, 1, 1, 1, nullptr, 0, nullptr) == EINVAL_);
+    CHECK(aipstack_chksum_batch_strided(dummy, 1, 65536, 1, out, 0, nullptr) == EINVAL_);
+    CHECK(aipstack_chksum_batch_strided(dummy, 1, 1, (1ull << 40) + 1, out, 0, nullptr) == EINVAL_);
+    CHECK(aipstack_chksum_batch_csr(nullptr, off, 1, out, 0, nullptr) == EINVAL_);
+    CHECK(aipstack_chksum_batch_csr(dummy, nullptr, 1, out, 0, nullptr) == EINVAL_);
+    CHECK(aipstack_chksum_batch_csr(dummy, off, 1, nullptr, 0, nullptr) == EINVAL_);
+    CHECK(aipstack_chksum_batch_seeded_csr(dummy, off, nullptr, 1, out, nullptr) == EINVAL_);
+    CHECK(aipstack_chksum_batch_chain(nullptr, lens, off, states, 1, out, 0, nullptr) == EINVAL_);
+    CHECK(aipstack_chksum_batch_chain(addrs, nullptr, off, states, 1, out, 0, nullptr) == EINVAL_);
+    CHECK(aipstack_chksum_batch_chain(addrs, lens, nullptr, states, 1, out, 0, nullptr) == EINVAL_);
+    CHECK(aipstack_chksum_batch_chain(addrs, lens, off, states, 1, nullptr, 0, nullptr) == EINVAL_);
+    CHECK(aipstack_chksum_rx_verify(dummy, off, 1, nullptr, nullptr) == EINVAL_);
+    CHECK(aipstack_chksum_tx_fill(dummy, nullptr, 1, st, nullptr) == EINVAL_);
+    // split fill: workspace missing, too small, misaligned
+    CHECK(aipstack_chksum_tx_fill_workspace_bytes(3) >= 24);
+    CHECK(aipstack_chksum_tx_fill_split(dummy, off, 1, st, nullptr, 64, nullptr) == EINVAL_);
+    CHECK(aipstack_chksum_tx_fill_split(dummy, off, 4, st, dummy, 8, nullptr) == EINVAL_);
+    CHECK(aipstack_chksum_tx_fill_split(dummy, off, 1, st, dummy + 1, 63, nullptr) == EINVAL_);
+
+    // tunables
+    CHECK(aipstack_chksum_tune(nullptr, 1) == EINVAL_);
+    CHECK(aipstack_chksum_tune("no_such_key", 1) == EINVAL_);
+    CHECK(aipstack_chksum_tune("stream", 0) == 0);
+
+    // engine: argument checks come before any device work
+    aipstack_chksum_engine *e = nullptr;
+    CHECK(aipstack_chksum_engine_create(0, 0, 0, &e) == EINVAL_ && e == nullptr);
+    CHECK(aipstack_chksum_engine_create(0, 0, 17, &e) == EINVAL_);
+    CHECK(aipstack_chksum_engine_create(0, 0, 2, nullptr) == EINVAL_);
+    CHECK(aipstack_chksum_engine_create(-1, 0, 2, &e) == AIPSTACK_CHKSUM_ENODEV && e == nullptr);
+    CHECK(aipstack_chksum_engine_register(nullptr, dummy, 64) == EINVAL_);
+    CHECK(aipstack_chksum_engine_unregister(nullptr, dummy) == EINVAL_);
+    CHECK(aipstack_chksum_engine_host_strided(nullptr, dummy, 1, 1, 1, out, 0) == EINVAL_);
+    CHECK(aipstack_chksum_engine_host_csr(nullptr, dummy, off, 1, out, 0) == EINVAL_);
+    aipstack_chksum_engine_destroy(nullptr);  // no-op
+
+    const int dev = aipstack_chksum_device_check(0);
+    CHECK(dev == 0 || dev == AIPSTACK_CHKSUM_ENODEV || dev == AIPSTACK_CHKSUM_EHIP);
+    const int ec = aipstack_chksum_engine_create(0, 0, 2, &e);
+    if (dev == 0) {
+        CHECK(ec == 0 && e != nullptr);
+        // engine-level contract checks (host side, before any copy)
+        std::uint64_t bad_off[3] = {0, 8, 4};  // decreasing
+        CHECK(aipstack_chksum_engine_host_csr(e, dummy, bad_off, 2, out, 0) == EINVAL_);
+        std::uint64_t big_off[2] = {0, 65536};  // > 65535 bytes
+        std::vector<char> big(65536, 0);
+        CHECK(aipstack_chksum_engine_host_csr(e, big.data(), big_off, 1, out, 0) == EINVAL_);
+        CHECK(aipstack_chksum_engine_host_strided(e, dummy, 1, 65536, 1, out, 0) == EINVAL_);
+        CHECK(aipstack_chksum_engine_register(e, nullptr, 64) == EINVAL_);
+        CHECK(aipstack_chksum_engine_register(e, dummy, 0) == EINVAL_);
+        CHECK(aipstack_chksum_engine_unregister(e, dummy) == EINVAL_);  // never registered
+        aipstack_chksum_engine_destroy(e);
+    } else {
+        CHECK(ec == dev && e == nullptr);
+    }
+
+    // diagnostics
+    for (int s : {0, -1, -2, -3, -99}) CHECK(aipstack_chksum_strerror(s) != nullptr);
+    CHECK(aipstack_chksum_abi_version() == AIPSTACK_CHKSUM_ABI_VERSION);
+    std::printf("capi_validation_test: OK (device %s)\n", dev == 0 ? "present" : "absent");
+    return 0;
+}

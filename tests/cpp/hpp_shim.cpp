@@ -1,5 +1,7 @@
 // Test shim: exposes the C++ header surface (include/aipstack_amd/Chksum.hpp) through
-// extern "C" so the Python tests can check it against the reference's golden vectors.
+// extern "C" so the Python tests can check it against the reference's golden vectors:
+// the accumulator/chain entry points below, and the reference stack's call sequences of
+// call_sites.inc (hpp_cs_*), the same text the reference wrapper compiles as ref_cs_*.
 #include <cstddef>
 #include <cstdint>
 #include <vector>
@@ -23,8 +25,8 @@ extern "C" std::uint16_t hpp_accumulate(const std::uint16_t *w16, std::size_t n1
                                         const char *hdr, std::size_t hdr_len, char *payload,
                                         std::size_t payload_len, std::uint32_t *state_out) {
     IpChksumAccumulator acc;
-    for (std::size_t i = 0; i < n16; i++) acc.addWord16(w16[i]);
-    for (std::size_t i = 0; i < n32; i++) acc.addWord32(w32[i]);
+    for (std::size_t i = 0; i < n16; i++) acc.addWord(WrapType<std::uint16_t>(), w16[i]);
+    for (std::size_t i = 0; i < n32; i++) acc.addWord(WrapType<std::uint32_t>(), w32[i]);
     acc.addEvenBytes(hdr, hdr_len);
     if (state_out) *state_out = std::uint32_t(acc.getState());
     IpBufNode node{payload, payload_len, nullptr};
@@ -32,3 +34,6 @@ extern "C" std::uint16_t hpp_accumulate(const std::uint16_t *w16, std::size_t n1
 }
 
 extern "C" std::uint16_t hpp_chksum(const char *p, std::size_t n) { return IpChksum(p, n); }
+
+#define CS_NAME(x) hpp_cs_##x
+#include "call_sites.inc"

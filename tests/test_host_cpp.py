@@ -1,0 +1,125 @@
+"""The C++ side of the boundary, on the CPU:
+
+* the reference's OWN tests/ip_chksum_test.cpp, compiled in place with
+  -DAIPSTACK_EXTERNAL_CHKSUM and linked to libaipstack_chksum.so (oracle/_ref/
+  ip_chksum_test_external; only where the reference was present at build time);
+* the repo's counterpart tests/cpp/ip_chksum_test.cpp on Chksum.hpp;
+* the reference stack's checksum call sequences (tests/cpp/call_sites.inc: TCP/UDP Rx and
+  Tx, IPv4 header Tx/Rx, ICMP) compiled against Chksum.hpp, checked against the answers
+  the same text gives when compiled against the reference (tests/golden/
+  call_site_cases.json), through ctypes and as a standalone program;
+* the C-ABI's argument validation (tests/cpp/capi_validation_test.cpp);
+* all of the above again under AddressSanitizer + UBSan (make -C tests/cpp asan; the
+  reference's nix build uses both, default.nix:5-6).
+"""
+import ctypes
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, ROOT
+
+import call_sites
+
+CPP = os.path.join(ROOT, "tests", "cpp")
+BUILD = os.path.join(CPP, "build")
+REF_EXT = os.path.join(ROOT, "oracle", "_ref", "ip_chksum_test_external")
+REF_LIB = os.path.join(ROOT, "oracle", "_ref", "libref_chksum.so")
+ASAN_ENV = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1",
+                UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+
+
+def _built(*targets):
+    missing = [t for t in targets if not os.path.exists(os.path.join(BUILD, t))]
+    if missing:
+        goals = ["asan"] if any(t.startswith("asan/") for t in missing) else []
+        subprocess.run(["make", "-j8", "-C", CPP, "all", *goals], check=True,
+                       stdout=subprocess.DEVNULL)
+    return [os.path.join(BUILD, t) for t in targets]
+
+
+def _run(cmd, env=None, timeout=300):
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, (cmd, r.returncode, r.stdout[-2000:], r.stderr[-4000:])
+    return r.stdout
+
+
+@pytest.fixture(scope="module")
+def cases():
+    with open(os.path.join(GOLDEN, "call_site_cases.json")) as f:
+        return json.load(f)["cases"]
+
+
+@pytest.mark.skipif(not os.path.exists(REF_EXT),
+                    reason="reference test not built here (no /root/reference at build time)")
+def test_reference_ip_chksum_test_on_our_hook():
+    """/root/reference/tests/ip_chksum_test.cpp, unmodified, linked to our IpChksumInverted
+    (Chksum.h:50-51): the 0x00FF chain known answer + 10 M random chain-vs-flat splits."""
+    _run([REF_EXT], timeout=600)
+
+
+def test_repo_ip_chksum_test():
+    (exe,) = _built("ip_chksum_test")
+    assert "OK" in _run([exe])
+
+
+def test_call_sites_golden_ctypes(cases, golden):
+    lib = ctypes.CDLL(_built("libhpp_shim.so")[0])
+    blob = golden["blob"]
+    bad = [c for c in cases if call_sites.evaluate(lib, "hpp", c, blob) != c["want"]]
+    assert not bad, bad[:3]
+    sites = {c["site"] for c in cases}
+    assert sites == set(call_sites.SITES)
+
+
+@pytest.mark.skipif(not os.path.exists(REF_LIB), reason="reference library not built here")
+def test_call_sites_live_vs_reference(golden):
+    """Fresh inputs (another seed) through both compilations of call_sites.inc."""
+    ref = ctypes.CDLL(REF_LIB)
+    hpp = ctypes.CDLL(_built("libhpp_shim.so")[0])
+    blob = golden["blob"]
+    for c in call_sites.make_cases(blob, seed=777):
+        c.pop("expect", None)
+        assert call_sites.evaluate(hpp, "hpp", c, blob) == call_sites.evaluate(ref, "ref", c, blob), c
+
+
+def _write_case_files(tmp_path, cases, blob):
+    blob_path = tmp_path / "blob.bin"
+    blob.tofile(blob_path)
+    lines = []
+    for c in cases:
+        want = c["want"] if isinstance(c["want"], list) else [c["want"]]
+        ch = " ".join(f"{o} {l}" for o, l in c["chunks"])
+        lines.append(" ".join(map(str, [c["site"], len(c["args"]), *c["args"],
+                                        c["hdr"] or "-", len(c["chunks"])]))
+                     + (" " + ch if ch else "")
+                     + " " + " ".join(map(str, [c["offset"], c["tot_len"], len(want), *want])))
+    case_path = tmp_path / "cases.txt"
+    case_path.write_text("\n".join(lines) + "\n")
+    return str(blob_path), str(case_path)
+
+
+def test_call_sites_program(tmp_path, cases, golden):
+    (exe,) = _built("call_sites_test")
+    b, c = _write_case_files(tmp_path, cases, golden["blob"])
+    assert f"{len(cases)} cases, 0 mismatches" in _run([exe, b, c])
+
+
+def test_capi_validation():
+    (exe,) = _built("capi_validation_test")
+    assert "OK" in _run([exe])
+
+
+@pytest.mark.parametrize("prog", ["ip_chksum_test", "call_sites_test", "capi_validation_test"])
+def test_asan_ubsan(prog, tmp_path, cases, golden):
+    (exe,) = _built(f"asan/{prog}")
+    args = [exe]
+    if prog == "call_sites_test":
+        args += list(_write_case_files(tmp_path, cases, golden["blob"]))
+    elif prog == "ip_chksum_test":
+        args.append("300000")
+    out = _run(args, env=ASAN_ENV, timeout=600)
+    assert "OK" in out or "0 mismatches" in out
