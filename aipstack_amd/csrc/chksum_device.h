@@ -687,66 +687,173 @@ struct StreamRun {
     }
 };
 
-// Minimum / maximum over the 64 lanes (DPP row scan + row broadcasts), wave-uniform.
-#define AIPSTACK_WAVE_REDUCE(name, op, ident)                                                \
-    __device__ __forceinline__ int name(int v) {                                             \
-        v = op(v, __builtin_amdgcn_update_dpp((int)(ident), v, 0x111, 0xF, 0xF, false));     \
-        v = op(v, __builtin_amdgcn_update_dpp((int)(ident), v, 0x112, 0xF, 0xF, false));     \
-        v = op(v, __builtin_amdgcn_update_dpp((int)(ident), v, 0x114, 0xF, 0xF, false));     \
-        v = op(v, __builtin_amdgcn_update_dpp((int)(ident), v, 0x118, 0xF, 0xF, false));     \
-        v = op(v, __builtin_amdgcn_update_dpp((int)(ident), v, 0x142, 0xA, 0xF, false));     \
-        v = op(v, __builtin_amdgcn_update_dpp((int)(ident), v, 0x143, 0xC, 0xF, false));     \
-        return __builtin_amdgcn_readlane(v, 63);                                             \
-    }
-AIPSTACK_WAVE_REDUCE(wave_min_i32, min, 0x7FFFFFFF)
-AIPSTACK_WAVE_REDUCE(wave_max_i32, max, 0x80000000u)
-#undef AIPSTACK_WAVE_REDUCE
+// Inclusive max-scan over the 64 lanes (-1 = unset).
+__device__ __forceinline__ int wave_max_scan(int v) {
+#define AIPSTACK_MAXSCAN(ctrl, rowmask) \
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, ctrl, rowmask, 0xF, false));
+    AIPSTACK_MAXSCAN(0x111, 0xF)
+    AIPSTACK_MAXSCAN(0x112, 0xF)
+    AIPSTACK_MAXSCAN(0x114, 0xF)
+    AIPSTACK_MAXSCAN(0x118, 0xF)
+    AIPSTACK_MAXSCAN(0x142, 0xA)
+    AIPSTACK_MAXSCAN(0x143, 0xC)
+#undef AIPSTACK_MAXSCAN
+    return v;
+}
 
-// Stream runs for chunks that lie close together in memory but not back to back (the
-// chain kernel: header nodes in one area, payload chunks in another). The candidates
-// (lanes in `cand`, chunk [a, a + l), l <= kStreamMaxLen) are tried as one run over
-// their address hull; a sparse hull (more than 2x their bytes + 2 KiB) is split once at
-// its middle and each half tried. A dense set's chunk sums are H(a + l) - H(a) over its
-// run: exact halves-sums, as the per-chunk path gives. Returns the lanes done, whose
-// sums are written to `sums`.
+// ---------------------------------------------------------------------------------
+// Gathered stream: up to 64 chunks anywhere in memory (lane j: chunk [a_j, a_j + l_j),
+// l_j <= 65535, empty chunks allowed), read as ONE stream of 16-byte segments that
+// skips everything between them. The segments holding chunk j's bytes, in order, get
+// the compact indices [cs_j, cs_j + ns_j) (cs = exclusive scan of the counts); window w
+// is compact indices [64w, 64w + 64), and lane k loads index 64w + k from the chunk that
+// owns it, at gbase_owner + 16 * index. Over that compact byte stream the prefixes work
+// exactly as in StreamRun: chunk j is the bytes [16 cs_j + (a_j & 15), that + l_j), so
+// its exact halves-sum is H(end) - H(start), the head and tail bytes outside it masked
+// at the two boundaries. A segment shared by two chunks is loaded once for each (the
+// second time from L2); bytes outside every chunk's segments are never read, so chunks
+// may sit in separate allocations (a 16-byte segment around a mapped byte is mapped).
+//
+// Owners: per group of U windows each chunk marks the lane where it starts (one LDS
+// write per lane, non-starting lanes write a trash slot), then a max-scan per window.
+// Software-pipelined: group g + 1's owners and loads are issued before group g is
+// consumed, so the wave keeps U windows in flight while it scans.
+// ---------------------------------------------------------------------------------
+constexpr int kGatherSlots = kWave + 1;  // per window: 64 lanes + a trash slot
+
 template <int U, bool NT>
-__device__ __forceinline__ uint64_t stream_dense_chunks(uint64_t a, uint32_t l, int lane,
-                                                        uint64_t cand, uint32_t &sums,
-                                                        uint32_t voff) {
-    if (!cand) return 0;
-    // addresses relative to the first candidate; chunks over 2^30 bytes away never stream
-    const int first = (int)__builtin_ctzll(cand);
-    const uint64_t base =
-        ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(a >> 32), first) << 32) |
-        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)a, first);
-    const int64_t rel = (int64_t)(a - base);
-    cand &= __builtin_amdgcn_ballot_w64(rel > -(1ll << 30) && rel < (1ll << 30));
-    const int rs = (int)rel, re = (int)rel + (int)l;
-    uint64_t done = 0, half0 = 0, half1 = 0;
-    for (int t = 0; t < 3; ++t) {  // the whole set, then its two halves
-        const uint64_t m = t == 0 ? cand : (t == 1 ? half0 : half1);
-        if (!m) continue;
-        const bool in = ((m >> lane) & 1u) != 0;
-        const int lo = wave_min_i32(in ? rs : 0x7FFFFFFF);
-        const int hi = wave_max_i32(in ? re : (int)0x80000000u);
-        const uint32_t tot = wave_sum(in ? l : 0u);  // <= 64 * 2^17
-        if ((uint32_t)(hi - lo) <= 2u * tot + 2048u) {
-            const uint64_t X1 = base + (uint64_t)(int64_t)hi;
-            StreamRun<U, NT> run;
-            run.begin((base + (uint64_t)(int64_t)lo) & ~(uint64_t)15, X1, voff);
-            const uint64_t bs[2] = {in ? a : X1, in ? a + l : X1};
-            uint32_t h[2], hx;
-            run.prefixes(bs, h, hx, voff);
-            if (in) sums = h[1] - h[0];
-            done |= m;
-            if (t == 0) break;
-        } else if (t == 0) {
-            const int mid = lo + (int)((uint32_t)(hi - lo) >> 1);
-            half0 = m & __builtin_amdgcn_ballot_w64(rs < mid);
-            half1 = m & ~half0;
+struct GatherRun {
+    uint32_t T;           // segments in the compact stream
+    uint32_t gb_lo, gb_hi;
+    uint32_t mark_slot;   // this lane's mark slot for the group its chunk starts in
+    uint32_t start_win;   // window its chunk starts in (~0: empty chunk)
+    int cur;              // owner of the previous window's last lane (wave-uniform)
+
+    __device__ __forceinline__ void init(uint64_t a, uint32_t l, uint32_t ns, uint32_t cs,
+                                         uint32_t total) {
+        T = total;
+        const uint64_t gbase = (a & ~(uint64_t)15) - 16ull * cs;
+        gb_lo = (uint32_t)gbase;
+        gb_hi = (uint32_t)(gbase >> 32);
+        start_win = ns ? (cs >> 6) : ~0u;
+        mark_slot = cs & 63u;
+        cur = 0;
+    }
+
+    // Owners of windows [w, w + U) and their loads into v (lanes past T load the stream's
+    // last segment again and count it as 0: every address stays inside a chunk).
+    __device__ __forceinline__ void issue(uint32_t w, int lane, uint32_t (*mark)[kGatherSlots],
+                                          u32x4 (&v)[U]) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) mark[u][lane] = 0u;
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t du = start_win - w;  // < U: starts in this group
+        uint32_t *slot = du < (uint32_t)U ? &mark[du][mark_slot] : &mark[0][kWave];
+        *slot = (uint32_t)lane + 1u;
+        __builtin_amdgcn_wave_barrier();
+        uint32_t m[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) m[u] = mark[u][lane];
+        __builtin_amdgcn_wave_barrier();
+        // inclusive max-scan (0 = no chunk starts at or before this lane in the window)
+#define AIPSTACK_GMAX(ctrl, rowmask)                                                         \
+    _Pragma("unroll") for (int u = 0; u < U; ++u)                                           \
+        m[u] = max(m[u], (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m[u], ctrl, rowmask, 0xF, \
+                                                               false));
+        AIPSTACK_GMAX(0x111, 0xF)
+        AIPSTACK_GMAX(0x112, 0xF)
+        AIPSTACK_GMAX(0x114, 0xF)
+        AIPSTACK_GMAX(0x118, 0xF)
+        AIPSTACK_GMAX(0x142, 0xA)
+        AIPSTACK_GMAX(0x143, 0xC)
+#undef AIPSTACK_GMAX
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int owner = m[u] ? (int)m[u] - 1 : cur;
+            cur = __builtin_amdgcn_readlane(owner, 63);
+            const uint32_t c0 = (w + (uint32_t)u) * (uint32_t)kWave + (uint32_t)lane;
+            const uint32_t c = min(c0, T - 1u);
+            const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(owner << 2, (int)gb_lo);
+            const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(owner << 2, (int)gb_hi);
+            const uint64_t addr = (((uint64_t)hi << 32) | lo) + 16ull * c;
+            typedef __attribute__((address_space(1))) const u32x4 gseg;
+            const gseg *p = (const gseg *)(addr);
+            if constexpr (NT)
+                v[u] = __builtin_nontemporal_load(p);
+            else
+                v[u] = *p;
         }
     }
-    return done;
+};
+
+template <int U, bool NT>
+__device__ __forceinline__ uint32_t sum_gathered_chunks(uint64_t a, uint32_t l, int lane,
+                                                        uint32_t (*mark)[kGatherSlots]) {
+    const uint32_t rs = (uint32_t)a & 15u;
+    const uint32_t ns = l ? (rs + l + 15u) >> 4 : 0u;
+    const uint32_t ns_incl = wave_incl_scan(ns);
+    const uint32_t cs = ns_incl - ns;
+    const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)ns_incl, 63);
+    if (T == 0) return 0;
+    const uint32_t nwin = (T + (uint32_t)kWave - 1u) >> 6;
+    GatherRun<U, NT> run;
+    run.init(a, l, ns, cs, T);
+    // this lane's two boundaries in the compact byte stream (empty chunk: both at 0)
+    const uint32_t bnd[2] = {ns ? 16u * cs + rs : 0u, ns ? 16u * cs + rs + l : 0u};
+    uint32_t bwin[2], below[2][4], h[2] = {0u, 0u};
+    int bsrc[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        bwin[k] = bnd[k] >> 10;
+        bsrc[k] = (int)(((bnd[k] >> 4) & 63u) << 2);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) below[k][d] = dword_keep(0, (int)(bnd[k] & 15u) - 4 * d);
+    }
+    uint32_t carry = 0;  // H at the current window's start, mod 2^32
+    auto consume = [&](uint32_t w, const u32x4 (&v)[U]) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t wu = w + (uint32_t)u;
+            const uint32_t c0 = wu * (uint32_t)kWave + (uint32_t)lane;
+            uint32_t s = halves(v[u][0], halves(v[u][1], halves(v[u][2], halves(v[u][3], 0u))));
+            s = c0 < T ? s : 0u;  // lanes past the stream re-read its last segment
+            const uint32_t incl = wave_incl_scan(s);
+            const uint32_t excl = incl - s;
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                if (__builtin_amdgcn_ballot_w64(bwin[k] == wu)) {
+                    uint32_t part = (uint32_t)__builtin_amdgcn_ds_bpermute(bsrc[k], (int)excl);
+#pragma unroll
+                    for (int d = 0; d < 4; ++d)
+                        part = halves(
+                            (uint32_t)__builtin_amdgcn_ds_bpermute(bsrc[k], (int)v[u][d]) &
+                                below[k][d],
+                            part);
+                    if (bwin[k] == wu) h[k] = carry + part;
+                }
+            }
+            carry += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        }
+    };
+    // two register sets, alternating: group g+1 in flight while group g is consumed. The
+    // next group is issued unconditionally (past the end every lane re-reads the last
+    // segment), so the loads stay straight-line and each wait is counted (vmcnt(N)).
+    // The loop runs whole pairs of groups (a group past the end sums zeros and moves no
+    // boundary): one exit, so the waits stay counted across the back edge.
+    u32x4 va[U], vb[U];
+    run.issue(0, lane, mark, va);
+    const uint32_t npairs = (nwin + 2u * U - 1u) / (2u * U);
+    for (uint32_t i = 0, w = 0; i < npairs; ++i, w += 2u * U) {
+        run.issue(w + U, lane, mark, vb);
+        consume(w, va);
+        run.issue(w + 2u * U, lane, mark, va);
+        consume(w + U, vb);
+    }
+    // a boundary at compact index T when T is a multiple of 64: past the last window
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+        if (bwin[k] >= nwin) h[k] = carry;
+    return h[1] - h[0];
 }
 
 // Stream mode for one chunk (stream_ok). Lane j < cnt holds packet j = [S, E); returns

@@ -129,36 +129,24 @@ __global__ __launch_bounds__(kBlock) void chksum_batch_kernel(Desc desc, uint64_
 // chunk <-> lane: coalesced loads of the chunk table; the chunk's chain from the chain
 // starts marked in LDS and a max-scan; its logical-position parity from a ballot of odd
 // lengths (prefix popcounts) plus the parity carried in from the previous 64 chunks; the
-// chunk sums one per wave, P in flight (sum_lane_packets, as the CSR batch); then each
-// oriented chunk sum is added into its chain's LDS accumulator.
+// 64 chunk sums from one gathered stream over just their bytes (sum_gathered_chunks,
+// chksum_device.h); then each oriented chunk sum is added into its chain's 64-bit LDS
+// accumulator, exact for any number of chunks per chain.
 // ---------------------------------------------------------------------------------
-
-// Inclusive max-scan over the wave of non-decreasing-where-set values (-1 = unset).
-__device__ __forceinline__ int wave_max_scan(int v) {
-#define AIPSTACK_MAXSCAN(ctrl, rowmask) \
-    v = max(v, __builtin_amdgcn_update_dpp(-1, v, ctrl, rowmask, 0xF, false));
-    AIPSTACK_MAXSCAN(0x111, 0xF)
-    AIPSTACK_MAXSCAN(0x112, 0xF)
-    AIPSTACK_MAXSCAN(0x114, 0xF)
-    AIPSTACK_MAXSCAN(0x118, 0xF)
-    AIPSTACK_MAXSCAN(0x142, 0xA)
-    AIPSTACK_MAXSCAN(0x143, 0xC)
-#undef AIPSTACK_MAXSCAN
-    return v;
-}
 
 __device__ __forceinline__ uint32_t parity_below(uint64_t mask, uint32_t s) {  // s in 0..64
     const uint64_t below = s == 0 ? 0ull : (~0ull >> (64u - s));
     return (uint32_t)__builtin_popcountll(mask & below) & 1u;
 }
 
-template <int U, int P, bool NT, int SU>
+template <bool NT, int SU>
 __global__ __launch_bounds__(kBlock) void chksum_chain_kernel(
     const uint64_t *__restrict__ chunk_addr, const uint32_t *__restrict__ chunk_len,
     const uint64_t *__restrict__ index, const uint32_t *__restrict__ states, uint64_t n,
     uint32_t chunks_per_wave, uint16_t *__restrict__ out, uint32_t flags) {
-    __shared__ uint32_t lds_acc[kWavesPerBlock][kWave];  // per-chain sum of chunk sums
+    __shared__ uint64_t lds_acc[kWavesPerBlock][kWave];  // per-chain sum of chunk sums
     __shared__ int lds_mark[kWavesPerBlock][kWave];      // chain starting at chunk lane
+    __shared__ uint32_t lds_gmark[kWavesPerBlock][SU][kGatherSlots];  // gathered stream owners
     const int lane = threadIdx.x & (kWave - 1);
     const uint32_t wave_in_block = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerBlock + wave_in_block;
@@ -166,9 +154,7 @@ __global__ __launch_bounds__(kBlock) void chksum_chain_kernel(
     uint64_t c = wave * chunks_per_wave;
     const uint64_t c_end = min(c + chunks_per_wave, ngroups);
     const bool final_flag = (flags & AIPSTACK_CHKSUM_FINAL) != 0;
-    const uint32_t voff = (uint32_t)lane * 16u;
-    const uint32_t not_lane0 = lane == 0 ? 0u : ~0u;
-    uint32_t *acc = lds_acc[wave_in_block];
+    uint64_t *acc = lds_acc[wave_in_block];
     int *mark = lds_mark[wave_in_block];
     CsrDesc idx_desc{0, index};  // the chain index walks like CSR offsets
 
@@ -214,25 +200,14 @@ __global__ __launch_bounds__(kBlock) void chksum_chain_kernel(
             const uint32_t s = before ? 0u : scs - kr;
             uint32_t q = parity_below(odd, (uint32_t)lane) ^ parity_below(odd, s);
             if (before) q ^= carry_par;
-            // chunk sums: stream runs over sets of chunks that lie close together, the
-            // rest one chunk per wave (P in flight; small ones four per instruction)
-            uint32_t sums = 0;
-            uint64_t todo = __builtin_amdgcn_ballot_w64(valid && l != 0);
-            if constexpr (SU > 0)
-                todo &= ~stream_dense_chunks<SU, NT>(
-                    a, l, lane, todo & __builtin_amdgcn_ballot_w64(l <= kStreamMaxLen), sums,
-                    voff);
-            if (todo) {
-                const LaneMeta meta = lane_meta(a, a + (uint64_t)l);
-                NoMaskHook hook;
-                sums |= sum_lane_packets<U, P, AIPSTACK_ROWS_CHAIN, NT>(meta, todo, lane, voff,
-                                                                       not_lane0, hook);
-            }
+            // the 64 chunk sums: one gathered stream over just the chunks' bytes
+            const uint32_t sums =
+                sum_gathered_chunks<SU, NT>(a, valid ? l : 0u, lane, lds_gmark[wave_in_block]);
             uint32_t r = fold16(sums);
             if ((uint32_t)(a & 1) == q)
                 r = bswap16(r);
             if (valid && r != 0)
-                __hip_atomic_fetch_add(&acc[cid], r, __ATOMIC_RELAXED,
+                __hip_atomic_fetch_add(&acc[cid], (uint64_t)r, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_WORKGROUP);
             // carry to the next 64 chunks
             const int last = (int)min((uint64_t)(kWave - 1), K1 - kb - 1);
@@ -240,10 +215,13 @@ __global__ __launch_bounds__(kBlock) void chksum_chain_kernel(
             carry_par = __builtin_amdgcn_readlane(q ^ (l & 1u), last);
         }
         __builtin_amdgcn_wave_barrier();
-        const uint32_t sum = acc[lane];  // <= chunks * 0xFFFF
+        const uint64_t sum = acc[lane];  // <= chunks * 0xFFFF: exact for any chunk count
         __builtin_amdgcn_wave_barrier();
+        // fold to 16 bits keeping the residue mod 0xFFFF and zero-ness (2^32 = 1)
+        uint64_t s33 = (sum & 0xFFFFFFFFull) + (sum >> 32);
+        const uint32_t s32 = (uint32_t)s33 + (uint32_t)(s33 >> 32);
         // m_sum = state (+) chain sum with end-around carry; getChksum folds and inverts.
-        const uint64_t t = (uint64_t)state + fold16(sum);
+        const uint64_t t = (uint64_t)state + fold16(s32);
         uint32_t r = fold16((uint32_t)t + (uint32_t)(t >> 32));
         r = final_flag ? (~r & 0xFFFFu) : r;
         if (lane < cnt)
@@ -384,7 +362,7 @@ int launch(const Desc &desc, uint64_t n, uint32_t max_len, uint16_t *d_out, uint
     return AIPSTACK_CHKSUM_EINVAL;
 }
 
-template <int U, int P, bool NT, int SU>
+template <bool NT, int SU>
 int launch_chain(const uint64_t *d_addr, const uint32_t *d_len, const uint64_t *d_index,
                  const uint32_t *d_states, uint64_t n, uint16_t *d_out, uint32_t flags,
                  hipStream_t stream) {
@@ -397,7 +375,7 @@ int launch_chain(const uint64_t *d_addr, const uint32_t *d_len, const uint64_t *
     const uint64_t waves = (nchunks + cpw - 1) / cpw;
     const uint64_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
     if (blocks > 0x7FFFFFFFull || cpw > 0xFFFFFFFFull) return AIPSTACK_CHKSUM_EINVAL;
-    hipLaunchKernelGGL((chksum_chain_kernel<U, P, NT, SU>), dim3((unsigned)blocks), dim3(kBlock), 0,
+    hipLaunchKernelGGL((chksum_chain_kernel<NT, SU>), dim3((unsigned)blocks), dim3(kBlock), 0,
                        stream, d_addr, d_len, d_index, d_states, n, (uint32_t)cpw, d_out, flags);
     return check_hip(hipGetLastError());
 }
@@ -481,13 +459,13 @@ extern "C" int aipstack_chksum_batch_chain(const uint64_t *d_chunk_addr,
     if (n == 0) return AIPSTACK_CHKSUM_OK;
     if (!d_chunk_addr || !d_chunk_len || !d_chunk_index || !d_out) return AIPSTACK_CHKSUM_EINVAL;
     if (n > (1ull << 40)) return AIPSTACK_CHKSUM_EINVAL;
-    // Chains are mostly short pieces (headers, ring-buffer halves): U = 2 covers 2 KiB.
-#define AIPSTACK_LAUNCH_CHAIN(NT, SU)                                                          \
-    return launch_chain<2, 4, NT, SU>(d_chunk_addr, d_chunk_len, d_chunk_index, d_states, n, \
-                                      d_out, flags, (hipStream_t)stream)
-    if (!tuning().nontemporal.load(std::memory_order_relaxed)) AIPSTACK_LAUNCH_CHAIN(false, 0);
+    // SU: gathered-stream windows issued together ("stream" tunable; off is not an option
+    // here: every chunk is summed by the gathered stream)
+#define AIPSTACK_LAUNCH_CHAIN(NT, SU)                                                       \
+    return launch_chain<NT, SU>(d_chunk_addr, d_chunk_len, d_chunk_index, d_states, n,     \
+                                d_out, flags, (hipStream_t)stream)
+    if (!tuning().nontemporal.load(std::memory_order_relaxed)) AIPSTACK_LAUNCH_CHAIN(false, 4);
     switch (tuning_stream_windows(4)) {
-        case 0: AIPSTACK_LAUNCH_CHAIN(true, 0);
         case 2: AIPSTACK_LAUNCH_CHAIN(true, 2);
         case 8: AIPSTACK_LAUNCH_CHAIN(true, 8);
         default: AIPSTACK_LAUNCH_CHAIN(true, 4);

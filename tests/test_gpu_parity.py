@@ -328,6 +328,32 @@ def test_cpp_capi_program():
     assert "OK" in r.stdout
 
 
+def test_bench_two_ranks_one_gpu():
+    """The multi-GPU bench path (one process per GPU, disjoint packet shards, gloo for the
+    control plane only) rehearsed with 2 ranks on device 0 (AIPSTACK_BENCH_FORCE_DEVICE):
+    torchrun launches bench.py --gpus 2 as the driver does; exactly one JSON line comes
+    back, with n_gpus 2, rank 0's shard bit-exact and its CPU baseline present."""
+    import json
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, AIPSTACK_BENCH_FORCE_DEVICE="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
+           "--steps", "5", "--warmup", "2", "--cpu-reps", "2"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 5 and d["scaling"] == "weak"
+    assert d["parity"] == "bit-exact"
+    cpu = d["cpu_baseline"]
+    assert cpu is not None and cpu["value"] > 0 and cpu["cores"] == 1
+    assert cpu["affinity_cores"] >= 1
+
+
 # ---- host-memory streaming engine (SURVEY 8(f) row 4) ------------------------------------
 
 @pytest.mark.parametrize("register", [False, True])
@@ -475,6 +501,85 @@ def test_chain_bench_shape(su, stream_mode):
     out = _np(A.chksum_batch_chain(ch["addr"], ch["len"], ch["index"], ch["states"],
                                    final=True))
     assert bench.chain_check(ch, out).startswith("bit-exact")
+
+
+def _chain_batch(chains, addr_of):
+    """chains: list of (state, [(buffer id, offset, length), ...]); addr_of(buffer id, offset)
+    gives the device address. Returns the chunk table as device tensors."""
+    addrs, lens, idx, states = [], [], [0], []
+    for st, chunks in chains:
+        for b, o, l in chunks:
+            if l:
+                addrs.append(addr_of(b, o))
+                lens.append(l)
+        idx.append(len(addrs))
+        states.append(st)
+    return (_d(np.array(addrs, dtype=np.uint64).view(np.int64)),
+            _d(np.array(lens, dtype=np.uint32).view(np.int32)),
+            _d(np.array(idx, dtype=np.uint64).view(np.int64)),
+            _d(np.array(states, dtype=np.uint32).view(np.int32)))
+
+
+def test_chain_many_chunks_exact(oracle):
+    """Chains of 70,000 one-byte and two-byte 0xFF chunks (the per-chain sum of chunk sums
+    passes 2^32 in a 32-bit accumulator) and a 200,000-chunk mixed chain, next to short
+    ones, against the oracle's chain rule (Chksum.h:283-315: end-around carry per chunk)."""
+    rng = np.random.default_rng(70000)
+    host = rng.integers(0, 256, size=1 << 20, dtype=np.uint8)
+    host[:4096] = 0xFF
+    db = _d(host)
+    chains = [
+        (0, [(0, int(rng.integers(0, 4000)), 1) for _ in range(70000)]),
+        (0xFFFFFFFF, [(0, int(rng.integers(0, 4000)), 2) for _ in range(70000)]),
+        (0x12345, [(0, 7, 3)]),
+        (int(rng.integers(0, 2**32)),
+         [(0, int(rng.integers(0, (1 << 20) - 1600)), int(rng.choice([0, 1, 2, 3, 1459])))
+          for _ in range(200000)]),
+        (0, []),
+        (0, [(0, 1, 1)] * 65537),
+    ]
+    addr, ln, idx, st = _chain_batch(chains, lambda b, o: db.data_ptr() + o)
+    got = _np(A.chksum_batch_chain(addr, ln, idx, st, final=True))
+    # oracle.chain = IpChksumAccumulator(State).getChksum(chain) (the final form)
+    want = np.array([oracle.chain(s, host, [(o, l) for _, o, l in ch if l]) for s, ch in chains],
+                    dtype=np.uint16)
+    assert np.array_equal(got, want), (got, want)
+
+
+def test_chain_chunks_in_separate_allocations(oracle):
+    """Chunks spread over separately allocated device buffers and pinned host memory: only
+    the chunks' own 16-byte segments may be read (the address space between allocations
+    can be unmapped; a read there faults the GPU)."""
+    rng = np.random.default_rng(4242)
+    hosts = [rng.integers(0, 256, size=int(sz), dtype=np.uint8)
+             for sz in (4096, 100000, 33, 65536 + 17, 5000)]
+    devs = [_d(h) for h in hosts[:4]]
+    pinned = torch.from_numpy(hosts[4]).pin_memory()  # device-accessible host memory
+    ptrs = [t.data_ptr() for t in devs] + [pinned.data_ptr()]
+    chains = []
+    for i in range(3000):
+        chunks = []
+        for _ in range(int(rng.integers(1, 6))):
+            b = int(rng.integers(0, len(hosts)))
+            sz = hosts[b].size
+            l = int(rng.integers(0, min(sz, 1600) + 1))
+            if rng.random() < 0.2:
+                o = sz - l          # ends at the allocation's last byte
+            elif rng.random() < 0.2:
+                o = 0               # starts at its first byte
+            else:
+                o = int(rng.integers(0, sz - l + 1))
+            chunks.append((b, o, l))
+        chains.append((int(rng.integers(0, 2**32)), chunks))
+    addr, ln, idx, st = _chain_batch(chains, lambda b, o: ptrs[b] + o)
+    got = _np(A.chksum_batch_chain(addr, ln, idx, st, final=True))
+    torch.cuda.synchronize()
+    want = []
+    for state, chunks in chains:
+        flat = np.concatenate([hosts[b][o:o + l] for b, o, l in chunks] + [np.zeros(0, np.uint8)])
+        # chain == flat with the state seeded (reference property, tests/ip_chksum_test.cpp)
+        want.append(oracle.chain(state, flat, [(0, flat.size)] if flat.size else []))
+    assert np.array_equal(got, np.array(want, dtype=np.uint16))
 
 
 # ---- frame-level batches: Tx fill / Rx verify (SURVEY 8(f) rows 2-3) ----------------------

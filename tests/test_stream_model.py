@@ -142,3 +142,107 @@ def test_stream_model_halves_sum_is_exact_for_max_len():
     # 2^17 - 1 bytes of 0xFF: halves-sum = 65535 * 65535 + 0xFF < 2^32 (no wrap ambiguity)
     n = (1 << 17) - 1
     assert (n // 2) * 0xFFFF + 0xFF < 2 ** 32
+
+
+# ---- gathered stream (chksum_device.h: sum_gathered_chunks, the chain kernel) ----------
+
+def gathered_model(buf, a, l, U=4):
+    """sum_gathered_chunks for one 64-chunk group: lane j = chunk [a[j], a[j] + l[j]) of buf
+    (absolute offsets into buf). Returns each lane's halves-sum (mod 2^32)."""
+    k = len(a)
+    a = [int(x) for x in a] + [0] * (64 - k)
+    l = [int(x) for x in l] + [0] * (64 - k)
+    rs = [x & 15 for x in a]
+    ns = [((rs[j] + l[j] + 15) >> 4) if l[j] else 0 for j in range(64)]
+    incl = np.cumsum(ns)
+    cs = [int(incl[j] - ns[j]) for j in range(64)]
+    T = int(incl[63])
+    if T == 0:
+        return [0] * 64
+    nwin = (T + 63) >> 6
+    gbase = [(a[j] & ~15) - 16 * cs[j] for j in range(64)]
+    bnd = [[16 * cs[j] + rs[j], 16 * cs[j] + rs[j] + l[j]] if ns[j] else [0, 0]
+           for j in range(64)]
+    h = [[0, 0] for _ in range(64)]
+    cur, carry = 0, 0
+    for w0 in range(0, nwin, U):
+        for u in range(U):
+            w = w0 + u
+            mark = [-1] * 64
+            for j in range(64):
+                if ns[j] and (cs[j] >> 6) == w:
+                    mark[cs[j] & 63] = j
+            m = list(np.maximum.accumulate(mark))
+            m = [cur if x < 0 else int(x) for x in m]
+            cur = m[63]
+            raw = np.zeros(64 * 16, dtype=np.uint8)
+            for lane in range(64):
+                c = w * 64 + lane
+                if c < T:
+                    addr = gbase[m[lane]] + 16 * c
+                    raw[lane * 16:lane * 16 + 16] = buf[addr:addr + 16]
+            seg = raw.view("<u2").astype(np.uint64).reshape(64, 8).sum(axis=1)
+            inc = np.cumsum(seg)
+            exc = inc - seg
+            for j in range(64):
+                for kk in range(2):
+                    b = bnd[j][kk]
+                    if b >> 10 == w:
+                        o = (b >> 4) & 63
+                        part = int(exc[o]) + _below(raw[o * 16:o * 16 + 16], b & 15)
+                        h[j][kk] = (carry + part) & M32
+            carry = (carry + int(inc[63])) & M32
+    for j in range(64):
+        for kk in range(2):
+            if bnd[j][kk] >> 10 >= nwin:
+                h[j][kk] = carry
+    return [(h[j][1] - h[j][0]) & M32 for j in range(64)]
+
+
+@pytest.mark.parametrize("U", [2, 4])
+@pytest.mark.parametrize("case", ["headers_and_ring", "tiny", "sparse", "long", "shared_segments"])
+def test_gathered_model_matches_oracle(oracle, case, U):
+    rng = np.random.default_rng(hash(("g", case, U)) % 2**32)
+    buf = rng.integers(0, 256, size=1 << 20, dtype=np.uint8)
+    buf[300000:310000] = 0xFF
+    buf[310000:320000] = 0
+    n = 64 if case != "tiny" else int(rng.integers(1, 65))
+    if case == "headers_and_ring":   # 20-B headers at a 32-B stride, payload ring pieces
+        a, l = [], []
+        pay = 500000 + int(rng.integers(0, 16))
+        for i in range(n):
+            if i % 3 == 0:
+                a.append(1000 + 32 * i)
+                l.append(20)
+            else:
+                cut = int(rng.integers(1, 1460))
+                a.append(pay)
+                l.append(cut if i % 3 == 1 else 1460 - cut)
+                pay += l[-1]
+    elif case == "tiny":
+        a = [int(x) for x in rng.integers(0, 200000, n)]
+        l = [int(x) for x in rng.choice([0, 1, 2, 3, 15, 16, 17], n)]
+    elif case == "sparse":           # far apart, odd addresses, some 0xFF / zero chunks
+        a = [int(x) for x in rng.integers(0, 900000, n)]
+        l = [int(x) for x in rng.integers(0, 1600, n)]
+        a[5], l[5] = 300001, 999
+        a[6], l[6] = 310003, 1001
+    elif case == "long":             # chunks of up to 65535 bytes spanning many windows
+        a = [int(x) for x in rng.integers(0, 900000, n)]
+        l = [int(x) for x in rng.choice([0, 1, 65535, 9000, 17], n)]
+    else:                            # back-to-back chunks sharing 16-B segments
+        a, l = [], []
+        p = 777
+        for i in range(n):
+            ln = int(rng.integers(0, 40))
+            a.append(p)
+            l.append(ln)
+            p += ln
+    sums = gathered_model(buf, a, l, U)
+    for j in range(n):
+        s = sums[j]
+        r = (s & 0xFFFF) + (s >> 16)
+        r = (r & 0xFFFF) + (r >> 16)
+        if (a[j] & 1) == 0:
+            r = ((r & 0xFF) << 8) | (r >> 8)
+        assert r == oracle.inverted(buf, a[j], l[j]), (case, j, a[j], l[j])
