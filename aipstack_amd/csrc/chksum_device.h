@@ -388,9 +388,6 @@ constexpr uint32_t kRowSegs = 16;
 #ifndef AIPSTACK_ROWS_FRAMES
 #define AIPSTACK_ROWS_FRAMES 0
 #endif
-#ifndef AIPSTACK_ROWS_CHAIN
-#define AIPSTACK_ROWS_CHAIN 2
-#endif
 
 __device__ u32x4 g_zero_segment;  // a valid address for rows without a packet
 
@@ -702,48 +699,98 @@ __device__ __forceinline__ int wave_max_scan(int v) {
 }
 
 // ---------------------------------------------------------------------------------
-// Gathered stream: up to 64 chunks anywhere in memory (lane j: chunk [a_j, a_j + l_j),
-// l_j <= 65535, empty chunks allowed), read as ONE stream of 16-byte segments that
-// skips everything between them. The segments holding chunk j's bytes, in order, get
-// the compact indices [cs_j, cs_j + ns_j) (cs = exclusive scan of the counts); window w
-// is compact indices [64w, 64w + 64), and lane k loads index 64w + k from the chunk that
-// owns it, at gbase_owner + 16 * index. Over that compact byte stream the prefixes work
-// exactly as in StreamRun: chunk j is the bytes [16 cs_j + (a_j & 15), that + l_j), so
-// its exact halves-sum is H(end) - H(start), the head and tail bytes outside it masked
-// at the two boundaries. A segment shared by two chunks is loaded once for each (the
-// second time from L2); bytes outside every chunk's segments are never read, so chunks
-// may sit in separate allocations (a 16-byte segment around a mapped byte is mapped).
+// Compact streams: byte runs that are NOT back to back in memory (the chain kernel's chunks,
+// anywhere in memory) read as one stream of just their 16-byte segments.
+// The segments of run j, in order, get the compact indices [cs_j, cs_j + ns_j); window w
+// is compact indices [64w, 64w + 64) and lane k loads index 64w + k from wherever the
+// Loader says it lives. Over that compact byte stream the prefixes work exactly as in
+// StreamRun: run j is the compact bytes [16 cs_j + (a_j & 15), that + l_j), so its exact
+// halves-sum is H(end) - H(start), the head and tail bytes outside it masked at the two
+// boundaries. Bytes outside every run's segments are never read.
 //
-// Owners: per group of U windows each chunk marks the lane where it starts (one LDS
-// write per lane, non-starting lanes write a trash slot), then a max-scan per window.
-// Software-pipelined: group g + 1's owners and loads are issued before group g is
-// consumed, so the wave keeps U windows in flight while it scans.
+// compact_sums() is software-pipelined: group g + 1's loads (U windows) are issued before
+// group g is consumed. The loop always runs whole pairs of groups and the next group is
+// issued unconditionally (a window past the stream sums zeros and moves no boundary), so
+// the loads stay straight-line and every wait is counted (vmcnt(N)), also across the back
+// edge. A Loader provides issue(w, v): windows [w, w + U) into v, lanes past the stream's
+// T segments loading anything readable (their sums are dropped here).
 // ---------------------------------------------------------------------------------
+template <int U, class Loader>
+__device__ __forceinline__ uint32_t compact_sums(uint32_t T, uint32_t b0, uint32_t b1,
+                                                 int lane, Loader &ld) {
+    const uint32_t nwin = (T + (uint32_t)kWave - 1u) >> 6;
+    const uint32_t bnd[2] = {b0, b1};
+    uint32_t bwin[2], below[2][4], h[2] = {0u, 0u};
+    int bsrc[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        bwin[k] = bnd[k] >> 10;
+        bsrc[k] = (int)(((bnd[k] >> 4) & 63u) << 2);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) below[k][d] = dword_keep(0, (int)(bnd[k] & 15u) - 4 * d);
+    }
+    uint32_t carry = 0;  // H at the current window's start, mod 2^32
+    auto consume = [&](uint32_t w, const u32x4 (&v)[U]) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t wu = w + (uint32_t)u;
+            const uint32_t c0 = wu * (uint32_t)kWave + (uint32_t)lane;
+            uint32_t s = halves(v[u][0], halves(v[u][1], halves(v[u][2], halves(v[u][3], 0u))));
+            s = c0 < T ? s : 0u;
+            const uint32_t incl = wave_incl_scan(s);
+            const uint32_t excl = incl - s;
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                if (__builtin_amdgcn_ballot_w64(bwin[k] == wu)) {
+                    uint32_t part = (uint32_t)__builtin_amdgcn_ds_bpermute(bsrc[k], (int)excl);
+#pragma unroll
+                    for (int d = 0; d < 4; ++d)
+                        part = halves(
+                            (uint32_t)__builtin_amdgcn_ds_bpermute(bsrc[k], (int)v[u][d]) &
+                                below[k][d],
+                            part);
+                    if (bwin[k] == wu) h[k] = carry + part;
+                }
+            }
+            carry += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        }
+    };
+    u32x4 va[U], vb[U];
+    ld.issue(0, va);
+    const uint32_t npairs = (nwin + 2u * U - 1u) / (2u * U);
+    for (uint32_t i = 0, w = 0; i < npairs; ++i, w += 2u * U) {
+        ld.issue(w + U, vb);
+        consume(w, va);
+        ld.issue(w + 2u * U, va);
+        consume(w + U, vb);
+    }
+    // a boundary at compact index T when T is a multiple of 64: past the last window
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+        if (bwin[k] >= nwin) h[k] = carry;
+    return h[1] - h[0];
+}
+
+// Loader for up to 64 chunks anywhere in memory (lane j: chunk [a_j, a_j + l_j)), the
+// chain kernel's: lane k finds the chunk owning its compact index per window (each chunk
+// marks the lane where it starts in LDS -- one write per lane per group, lanes that start
+// nothing write a trash slot -- then a max-scan) and loads from that chunk's address with
+// a global load. Lanes past the stream re-read its last segment: every address stays
+// inside a chunk, so chunks may sit in separate allocations (a 16-byte segment around a
+// mapped byte is mapped).
 constexpr int kGatherSlots = kWave + 1;  // per window: 64 lanes + a trash slot
 
 template <int U, bool NT>
-struct GatherRun {
-    uint32_t T;           // segments in the compact stream
-    uint32_t gb_lo, gb_hi;
-    uint32_t mark_slot;   // this lane's mark slot for the group its chunk starts in
-    uint32_t start_win;   // window its chunk starts in (~0: empty chunk)
-    int cur;              // owner of the previous window's last lane (wave-uniform)
+struct ChunkLoader {
+    uint32_t T;
+    uint32_t gb_lo, gb_hi;  // this lane's chunk: segment c (compact) is at gbase + 16 c
+    uint32_t mark_slot;     // the lane its chunk starts at, within its window
+    uint32_t start_win;     // the window its chunk starts in (~0: empty chunk)
+    int cur;                // owner of the previous window's last lane (wave-uniform)
+    int lane;
+    uint32_t (*mark)[kGatherSlots];
 
-    __device__ __forceinline__ void init(uint64_t a, uint32_t l, uint32_t ns, uint32_t cs,
-                                         uint32_t total) {
-        T = total;
-        const uint64_t gbase = (a & ~(uint64_t)15) - 16ull * cs;
-        gb_lo = (uint32_t)gbase;
-        gb_hi = (uint32_t)(gbase >> 32);
-        start_win = ns ? (cs >> 6) : ~0u;
-        mark_slot = cs & 63u;
-        cur = 0;
-    }
-
-    // Owners of windows [w, w + U) and their loads into v (lanes past T load the stream's
-    // last segment again and count it as 0: every address stays inside a chunk).
-    __device__ __forceinline__ void issue(uint32_t w, int lane, uint32_t (*mark)[kGatherSlots],
-                                          u32x4 (&v)[U]) {
+    __device__ __forceinline__ void issue(uint32_t w, u32x4 (&v)[U]) {
 #pragma unroll
         for (int u = 0; u < U; ++u) mark[u][lane] = 0u;
         __builtin_amdgcn_wave_barrier();
@@ -786,6 +833,9 @@ struct GatherRun {
     }
 };
 
+// The chain kernel's 64 chunk sums (lane j: chunk [a_j, a_j + l_j), l_j <= 65535, empty
+// allowed; `mark`: this wave's LDS scratch, U windows of kGatherSlots). Returns lane j's
+// exact halves-sum of its chunk.
 template <int U, bool NT>
 __device__ __forceinline__ uint32_t sum_gathered_chunks(uint64_t a, uint32_t l, int lane,
                                                         uint32_t (*mark)[kGatherSlots]) {
@@ -795,65 +845,19 @@ __device__ __forceinline__ uint32_t sum_gathered_chunks(uint64_t a, uint32_t l, 
     const uint32_t cs = ns_incl - ns;
     const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)ns_incl, 63);
     if (T == 0) return 0;
-    const uint32_t nwin = (T + (uint32_t)kWave - 1u) >> 6;
-    GatherRun<U, NT> run;
-    run.init(a, l, ns, cs, T);
+    ChunkLoader<U, NT> ld;
+    ld.T = T;
+    const uint64_t gbase = (a & ~(uint64_t)15) - 16ull * cs;
+    ld.gb_lo = (uint32_t)gbase;
+    ld.gb_hi = (uint32_t)(gbase >> 32);
+    ld.start_win = ns ? (cs >> 6) : ~0u;
+    ld.mark_slot = cs & 63u;
+    ld.cur = 0;
+    ld.lane = lane;
+    ld.mark = mark;
     // this lane's two boundaries in the compact byte stream (empty chunk: both at 0)
-    const uint32_t bnd[2] = {ns ? 16u * cs + rs : 0u, ns ? 16u * cs + rs + l : 0u};
-    uint32_t bwin[2], below[2][4], h[2] = {0u, 0u};
-    int bsrc[2];
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        bwin[k] = bnd[k] >> 10;
-        bsrc[k] = (int)(((bnd[k] >> 4) & 63u) << 2);
-#pragma unroll
-        for (int d = 0; d < 4; ++d) below[k][d] = dword_keep(0, (int)(bnd[k] & 15u) - 4 * d);
-    }
-    uint32_t carry = 0;  // H at the current window's start, mod 2^32
-    auto consume = [&](uint32_t w, const u32x4 (&v)[U]) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t wu = w + (uint32_t)u;
-            const uint32_t c0 = wu * (uint32_t)kWave + (uint32_t)lane;
-            uint32_t s = halves(v[u][0], halves(v[u][1], halves(v[u][2], halves(v[u][3], 0u))));
-            s = c0 < T ? s : 0u;  // lanes past the stream re-read its last segment
-            const uint32_t incl = wave_incl_scan(s);
-            const uint32_t excl = incl - s;
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                if (__builtin_amdgcn_ballot_w64(bwin[k] == wu)) {
-                    uint32_t part = (uint32_t)__builtin_amdgcn_ds_bpermute(bsrc[k], (int)excl);
-#pragma unroll
-                    for (int d = 0; d < 4; ++d)
-                        part = halves(
-                            (uint32_t)__builtin_amdgcn_ds_bpermute(bsrc[k], (int)v[u][d]) &
-                                below[k][d],
-                            part);
-                    if (bwin[k] == wu) h[k] = carry + part;
-                }
-            }
-            carry += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-        }
-    };
-    // two register sets, alternating: group g+1 in flight while group g is consumed. The
-    // next group is issued unconditionally (past the end every lane re-reads the last
-    // segment), so the loads stay straight-line and each wait is counted (vmcnt(N)).
-    // The loop runs whole pairs of groups (a group past the end sums zeros and moves no
-    // boundary): one exit, so the waits stay counted across the back edge.
-    u32x4 va[U], vb[U];
-    run.issue(0, lane, mark, va);
-    const uint32_t npairs = (nwin + 2u * U - 1u) / (2u * U);
-    for (uint32_t i = 0, w = 0; i < npairs; ++i, w += 2u * U) {
-        run.issue(w + U, lane, mark, vb);
-        consume(w, va);
-        run.issue(w + 2u * U, lane, mark, va);
-        consume(w + U, vb);
-    }
-    // a boundary at compact index T when T is a multiple of 64: past the last window
-#pragma unroll
-    for (int k = 0; k < 2; ++k)
-        if (bwin[k] >= nwin) h[k] = carry;
-    return h[1] - h[0];
+    const uint32_t b0 = ns ? 16u * cs + rs : 0u;
+    return compact_sums<U>(T, b0, ns ? b0 + l : 0u, lane, ld);
 }
 
 // Stream mode for one chunk (stream_ok). Lane j < cnt holds packet j = [S, E); returns

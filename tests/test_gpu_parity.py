@@ -152,6 +152,44 @@ def test_lengths(oracle, plen):
     assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("plen", [2, 15, 16, 17, 31, 100, 1499, 1500, 2047, 9000, 65535])
+def test_slotted_packets(oracle, plen):
+    """Packets in fixed slots (stride % 16 == 0, stride != len: one packet per wavefront),
+    at every start offset within a 16-byte segment."""
+    rng = np.random.default_rng(plen)
+    for base in (0, 1, 7, 8, 15):
+        for extra in (0, 16, 512):
+            stride = ((base % 16 + plen + 15) // 16) * 16 + extra
+            if stride == plen:
+                stride += 16
+            for n in (1, 63, 64, 65, 1000 if plen < 10000 else 100):
+                buf = torch.empty(n * stride + 64, dtype=torch.uint8, device=DEV)
+                synth.fill_device(buf, int(rng.integers(0, 1 << 30)))
+                got = _np(A.chksum_batch_strided(buf, stride, plen, n, byte_offset=base))
+                want = oracle.batch_strided(_np(buf), stride, plen, n, base_off=base)
+                assert np.array_equal(got, want), (plen, stride, base, n,
+                                                   np.nonzero(got != want)[0][:8])
+
+
+def test_slotted_full_size_ring_slots(oracle):
+    """bench.py's A2K: 1M x 1500-byte packets in 2048-byte slots, all 0x00 / all 0xFF
+    slots mixed in; FINAL flag."""
+    n, plen, stride = 1 << 20, 1500, 2048
+    buf = torch.empty(n * stride, dtype=torch.uint8, device=DEV)
+    synth.fill_device(buf, synth.SEED_DATA)
+    v = buf.view(n, stride)
+    v[::97, :plen] = 0
+    v[5::101, :plen] = 0xFF
+    got = _np(A.chksum_batch_strided(buf, stride, plen, n))
+    want = oracle.batch_strided(_np(buf), stride, plen, n)
+    assert np.array_equal(got, want), np.count_nonzero(got != want)
+    i = np.arange(n)
+    assert np.all(got[(i % 97 == 0) & (i % 101 != 5)] == 0)      # all-zero packets
+    assert np.all(got[i % 101 == 5] == 0xFFFF)                     # all-0xFF, even length
+    fin = _np(A.chksum_batch_strided(buf, stride, plen, n, final=True))
+    assert np.array_equal(fin, ~want)
+
+
 def _tune(key, value):
     from aipstack_amd import _lib
     assert _lib.load().aipstack_chksum_tune(key.encode(), value) == A.AIPSTACK_CHKSUM_OK

@@ -26,6 +26,7 @@ sys.path.insert(0, ROOT)
 DEFAULT_VARIANTS = {
     "A": "0,0,1,0;0,0,1,0,-1;0,0,1,0,2;0,0,1,0,8;0,0,1,32;0,0,1,128;0,0,1,256;0,0,1,32,8",
     "B": "0,0,1,0;0,0,1,0,-1;0,0,1,0,2;0,0,1,0,8;0,0,1,32;0,0,1,128;0,0,1,256;0,0,1,32,8",
+    "A2K": "0,0,1,0;0,0,1,0,4;0,0,1,0,8;0,0,1,0,-1;0,4,1,0,-1;0,8,1,0,-1;0,0,1,32;0,0,1,128",
     "C": "0,0,1,0;0,0,1,0,-1;0,0,1,0,2;0,0,1,0,8;0,0,1,64;0,0,1,256;0,0,1,64,8;"
          "0,0,1,32;0,0,1,32,8;0,0,1,32,2",
     "RX": "0,0;0,0,-1;0,0,2;0,0,8;2,0;4,64;4,256;2,64,2;2,256,2",
@@ -35,7 +36,7 @@ DEFAULT_VARIANTS = {
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", default="A", choices=["A", "B", "C", "RX", "TX"])
+    ap.add_argument("--config", default="A", choices=["A", "B", "C", "A2K", "RX", "TX"])
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--reps", type=int, default=5, help="launches per variant per round")
     ap.add_argument("--variants", default=None,
@@ -58,8 +59,11 @@ def main():
 
     dev = torch.device("cuda", 0)
     stream = torch.cuda.current_stream()
+    stride = None
     if args.config == "A":
         n, plen, layout = 1 << 20, 1500, "strided"
+    elif args.config == "A2K":  # MTU packets in 2048-byte ring slots
+        n, plen, layout, stride = 1 << 20, 1500, "strided", 2048
     elif args.config == "B":
         n, plen, layout = 256 << 10, 9000, "strided"
     elif args.config == "C":
@@ -86,8 +90,9 @@ def main():
         d_off = torch.from_numpy(off).to(dev)
         alg = total + 8 * (n + 1) + n + (4 * n if layout == "tx" else 0)
     elif layout == "strided":
+        stride = stride or plen
         total = n * plen
-        buf = torch.empty(total, dtype=torch.uint8, device=dev)
+        buf = torch.empty(n * stride, dtype=torch.uint8, device=dev)
         synth.fill_device(buf, synth.SEED_DATA)
         alg = total + 2 * n
     else:
@@ -110,7 +115,7 @@ def main():
             A.tx_fill(buf, d_off, out=out, stream=stream, split=not args.tx_inplace,
                       workspace=tx_ws)
         elif layout == "strided":
-            A.chksum_batch_strided(buf, plen, plen, n, out=out, stream=stream)
+            A.chksum_batch_strided(buf, stride, plen, n, out=out, stream=stream)
         else:
             A.chksum_batch_csr(buf, d_off, out=out, stream=stream)
 
@@ -149,7 +154,7 @@ def main():
     elif layout == "strided":
         orc.oracle_batch_strided.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
                                              ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32]
-        orc.oracle_batch_strided(host.ctypes.data, plen, plen, m, want.ctypes.data, 0)
+        orc.oracle_batch_strided(host.ctypes.data, stride, plen, m, want.ctypes.data, 0)
     else:
         orc.oracle_batch_csr.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                          ctypes.c_void_p, ctypes.c_uint32]
