@@ -257,6 +257,7 @@ struct Tuning {
         env("AIPSTACK_CHKSUM_NT", nontemporal);
         env("AIPSTACK_CHKSUM_FRAMES", frames);
         env("AIPSTACK_CHKSUM_STREAM", stream);
+
     }
 };
 

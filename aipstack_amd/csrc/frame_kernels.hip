@@ -63,19 +63,34 @@ __device__ __forceinline__ void store_be16(uint64_t addr, uint32_t v) {
 #endif
 }
 
-// Split Tx fill's per-frame field record: IPv4 header checksum (bits 0-15), L4 checksum
-// (16-31), L4 field offset from the frame start (32-39), write the IPv4 field (bit 40),
-// write the L4 field (bit 41), the frame's status (48-55).
-__device__ __forceinline__ uint64_t tx_record(uint32_t hchk, uint32_t chk, int fld, bool ip,
-                                              bool l4, int status) {
-    return (uint64_t)(hchk & 0xFFFFu) | (uint64_t)(chk & 0xFFFFu) << 16 |
-           (uint64_t)(uint32_t)fld << 32 | (uint64_t)ip << 40 | (uint64_t)l4 << 41 |
-           (uint64_t)(uint8_t)status << 48;
+// One frame's result, as the finish step produces it (lane j <-> frame j of the chunk):
+//   w0 = IPv4 header checksum (bits 0-15) | L4 checksum (16-31)
+//   w1 = L4 field offset from the frame start (0-7) | write the IPv4 field (8) | write the
+//        L4 field (9) | status / verdict (16-23)
+// Also the split Tx fill's workspace record (w0 | w1 << 32), scattered by tx_scatter_kernel.
+struct FrameOut {
+    uint64_t S;  // frame start (absolute address)
+    uint32_t w0, w1;
+};
+
+__device__ __forceinline__ uint32_t frame_w1(int fld, bool ip, bool l4, int status) {
+    return (uint32_t)(fld & 0xFF) | (uint32_t)ip << 8 | (uint32_t)l4 << 9 |
+           (uint32_t)(uint8_t)status << 16;
 }
 
-// Second pass of split Tx fill: one frame per thread, the field stores of every frame
-// after the whole read pass (stream-ordered behind frame_kernel<TX, ..., SPLIT>), and the
-// status bytes.
+// The stores of one frame: its status byte, and for Tx the two checksum fields in place.
+template <bool TX>
+__device__ __forceinline__ void store_frame(uint64_t S, uint32_t w0, uint32_t w1,
+                                            uint8_t *__restrict__ status, uint64_t i) {
+    status[i] = (uint8_t)(w1 >> 16);
+    if constexpr (TX) {
+        if (w1 & 0x100u) store_be16(S + 24, w0);
+        if (w1 & 0x200u) store_be16(S + (w1 & 0xFFu), w0 >> 16);
+    }
+}
+
+// Second pass of the split Tx fill: one frame per thread, the stores of every frame after
+// the whole read pass (stream-ordered behind frame_kernel<TX, ..., SPLIT>).
 __global__ __launch_bounds__(kBlock) void tx_scatter_kernel(uint64_t base,
                                                             const uint64_t *__restrict__ offsets,
                                                             const uint64_t *__restrict__ records,
@@ -84,18 +99,9 @@ __global__ __launch_bounds__(kBlock) void tx_scatter_kernel(uint64_t base,
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
     for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
         const uint64_t rec = records[i];
-        status[i] = (uint8_t)(rec >> 48);
-        const uint64_t S = base + offsets[i];
-        if ((rec >> 40) & 1u)
-            store_be16(S + 24, (uint32_t)rec);
-        if ((rec >> 41) & 1u)
-            store_be16(S + ((rec >> 32) & 0xFFu), (uint32_t)(rec >> 16));
+        store_frame<true>(base + offsets[i], (uint32_t)rec, (uint32_t)(rec >> 32), status, i);
     }
 }
-
-#ifndef AIPSTACK_TX_RECORD_MODE  // experiments only (tools/build_variant.sh): 1 = nontemporal
-#define AIPSTACK_TX_RECORD_MODE 0   // record stores; 2 = none, 3/4/5 = 4/2/1 bytes (wrong output)
-#endif
 
 // What the header pass decides for one frame (lane j <-> frame j of the chunk).
 struct FrameLane {
@@ -261,15 +267,15 @@ __device__ __forceinline__ FrameLane parse_lane(const u32x4 (&seg)[kHdrSegs], ui
     return r;
 }
 
-// Rx verify / Tx fill of n frames at CSR offsets. A wave walks 64-frame chunks:
+// Rx verify / Tx fill of one 64-frame chunk (CSR offsets), lane j <-> frame j:
 //   (B) lane j loads frame j's first 112 aligned bytes (one buffer descriptor per chunk)
 //       and parses its headers (parse_lane): the L4 byte range, pseudo-header words and
 //       the verdict when no L4 sum is needed;
 //   (C) the frames that need an L4 sum are summed one per wave, P in flight, exactly as
 //       the CSR checksum batch sums packets (PacketLoad over the L4 range); for Tx the
 //       checksum field is masked out of the sum;
-//   (D) lane j finishes frame j: verdict (one coalesced 64-byte store), and for Tx the
-//       IPv4 header and L4 checksums written in place.
+//   (D) lane j finishes frame j: the verdict, and for Tx the IPv4 header and L4 checksums.
+// Returns lane j's FrameOut; the caller stores it (store_frame) now or later.
 //
 // Stream mode (SU > 0, chunks whose frames lie back to back): (C) is replaced by stream
 // prefixes over the chunk's frames (chksum_device.h): each frame's L4 sum is
@@ -279,10 +285,93 @@ __device__ __forceinline__ FrameLane parse_lane(const u32x4 (&seg)[kHdrSegs], ui
 #ifndef AIPSTACK_FRAME_PREFETCH
 #define AIPSTACK_FRAME_PREFETCH(SU) ((SU) / 2)
 #endif
-// SPLIT (Tx only): instead of storing the two fields in place, lane j writes frame j's
-// field record (tx_record) to a workspace, coalesced; tx_scatter_kernel stores them after
-// the whole read pass. Measured (profiles/r01g/tx_store_probe.jsonl): 2-byte stores
-// interleaved with the read stream cost ~5x what the same stores cost as their own pass.
+template <bool TX, int U, int P, bool NT, int SU>
+__device__ __forceinline__ FrameOut process_chunk(const CsrDesc &desc, uint64_t p0, uint64_t n,
+                                                  int lane, uint32_t voff, uint32_t not_lane0,
+                                                  int &cnt_out) {
+    const auto chunk = desc.begin_chunk(p0, n, lane);
+    const int cnt = (int)min((uint64_t)kWave, n - p0);
+    cnt_out = cnt;
+    uint64_t S, E;
+    desc.lane_bounds(chunk, lane, S, E);
+    const uint64_t l64 = E - S;
+    const int len = (lane >= cnt || l64 >= (1ull << 31)) ? 0 : (int)l64;  // 0: NOT_IP4
+    // (B) headers: aligned segments [A0_j, A0_j + 112) through one range-checked
+    // descriptor over the chunk's aligned span (never past the 16-byte blocks holding
+    // the chunk's bytes; slots past it read 0). A span beyond what 64 frames of at most
+    // 65535 bytes can cover (offsets outside the contract, chksum.h) reads nothing.
+    const uint64_t base = (__builtin_amdgcn_readfirstlane((uint32_t)S) & ~15u) |
+                          ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(S >> 32)) << 32);
+    const uint64_t span = ((desc.base + chunk.end_off + 15u) & ~(uint64_t)15) - base;
+    const uint32_t hrec = __builtin_amdgcn_readfirstlane(
+        span > (uint64_t)kWave * 65536u + 16u ? 0u : (uint32_t)span);  // uniform: SGPR descriptor
+    const __amdgpu_buffer_rsrc_t hrsrc = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void *>(base), (short)0, hrec, 0x00020000);
+    const uint32_t hoff = (uint32_t)((S & ~(uint64_t)15) - base);
+    // this lane's blocks: A0 up to the first 32-byte boundary past the header bytes
+    // (A0 % 32 + 15 + 97 + 31 < 160, so at most 128 bytes = kHdrSegs segments)
+    const uint32_t a0_32 = (uint32_t)S & 16u;
+    const uint32_t hb_end = ((a0_32 + ((uint32_t)S & 15u) + kHdrNeed + 31u) & ~31u) - a0_32;
+    u32x4 seg[kHdrSegs];
+#pragma unroll
+    for (int i = 0; i < kHdrSegs; ++i)  // past hb_end: out of range, reads 0, no traffic
+        seg[i] = load_segment<false>(hrsrc, 16u * i < hb_end ? hoff + 16u * i : 0xFFFFFFF0u, 0u);
+    FrameLane fl;
+    uint32_t r;
+    bool streamed = false;
+    if constexpr (SU > 0) {
+        if (stream_ok(S, E, lane, cnt)) {
+            // (C') stream prefixes at each frame's L4 start and end. The first windows'
+            // loads go out now, behind the header loads, and arrive during the parse.
+            const int lastl = cnt - 1;
+            const uint64_t X1 =
+                ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(E >> 32), lastl)
+                 << 32) |
+                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)E, lastl);
+            StreamRun<SU, NT, AIPSTACK_FRAME_PREFETCH(SU)> run;
+            run.begin(base, X1, voff);
+            fl = parse_lane<TX, true>(seg, S, len, hb_end);
+            // frames without an L4 sum (and lanes past the batch) put both at X1
+            const bool use = lane < cnt && fl.l4;
+            const uint64_t bs[2] = {use ? fl.l4s : X1, use ? fl.l4e : X1};
+            uint32_t h[2], hx;
+            run.prefixes(bs, h, hx, voff);
+            r = fold16(h[1] - h[0] - fl.fhalf);  // exact halves-sum, < 2^32
+            streamed = true;
+        }
+    }
+    if (!streamed) {
+        fl = parse_lane<TX, false>(seg, S, len, hb_end);
+        const bool need = fl.ce != fl.cs;
+        const LaneMeta meta = lane_meta(fl.cs, fl.ce);
+        // (C) the remaining L4 bytes, one frame per wave, P frames' loads in flight
+        NoMaskHook hook;
+        const uint32_t sums = sum_lane_packets<U, P, AIPSTACK_ROWS_FRAMES, NT>(
+            meta, __builtin_amdgcn_ballot_w64(need), lane, voff, not_lane0, hook);
+        // both parts (< 2^24 + 2^17), folded
+        r = fold16(sums + fold16(fl.part));
+    }
+    // (D) per-lane finish: oriented by the L4 start
+    if ((fl.l4s & 1u) == 0)  // L4 start even: little-endian pairing -> big-endian
+        r = bswap16(r);
+    const uint64_t m = (uint64_t)fl.words + r;
+    uint32_t chk = (~fold16((uint32_t)m + (uint32_t)(m >> 32))) & 0xFFFFu;
+    int v = fl.pre;
+    if (TX) {
+        if (fl.udp && chk == 0) chk = 0xFFFFu;                      // udp/IpUdpProto.h:176-178
+    } else if (fl.l4) {
+        v = chk == 0 ? AIPSTACK_RX_ACCEPT : AIPSTACK_RX_DROP_L4_CHKSUM;
+    }
+    FrameOut o;
+    o.S = S;
+    o.w0 = (fl.hchk & 0xFFFFu) | chk << 16;
+    o.w1 = frame_w1(fl.fld, TX && fl.ip_ok, TX && fl.l4, v);
+    return o;
+}
+
+// The classic kernel: a wave walks its chunks and stores each chunk's results right after
+// it. SPLIT (Tx only): lane j writes frame j's record (w0 | w1 << 32) to a workspace
+// instead, and tx_scatter_kernel stores the fields after the whole read pass.
 template <bool TX, int U, int P, bool NT, int SU, bool SPLIT>
 __global__ __launch_bounds__(kBlock, 4) void frame_kernel(CsrDesc desc, uint64_t n,
                                                        uint32_t chunks_per_wave,
@@ -296,107 +385,16 @@ __global__ __launch_bounds__(kBlock, 4) void frame_kernel(CsrDesc desc, uint64_t
     const uint64_t c_end = min(c + chunks_per_wave, nchunks);
     const uint32_t voff = (uint32_t)lane * 16u;
     const uint32_t not_lane0 = lane == 0 ? 0u : ~0u;
-
     for (; c < c_end; ++c) {
         const uint64_t p0 = c * kWave;
-        const auto chunk = desc.begin_chunk(p0, n, lane);
-        const int cnt = (int)min((uint64_t)kWave, n - p0);
-        uint64_t S, E;
-        desc.lane_bounds(chunk, lane, S, E);
-        const uint64_t l64 = E - S;
-        const int len = (lane >= cnt || l64 >= (1ull << 31)) ? 0 : (int)l64;  // 0: NOT_IP4
-        // (B) headers: aligned segments [A0_j, A0_j + 112) through one range-checked
-        // descriptor over the chunk's aligned span (never past the 16-byte blocks holding
-        // the chunk's bytes; slots past it read 0).
-        const uint64_t base = (__builtin_amdgcn_readfirstlane((uint32_t)S) & ~15u) |
-                              ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(S >> 32)) << 32);
-        const uint64_t span = ((desc.base + chunk.end_off + 15u) & ~(uint64_t)15) - base;
-        const uint32_t hrec = __builtin_amdgcn_readfirstlane(
-            span > 0xFFFFFF00ull ? 0xFFFFFF00u : (uint32_t)span);  // uniform: SGPR descriptor
-        const __amdgpu_buffer_rsrc_t hrsrc = __builtin_amdgcn_make_buffer_rsrc(
-            reinterpret_cast<void *>(base), (short)0, hrec, 0x00020000);
-        const uint32_t hoff = (uint32_t)((S & ~(uint64_t)15) - base);
-        // this lane's blocks: A0 up to the first 32-byte boundary past the header bytes
-        // (A0 % 32 + 15 + 97 + 31 < 160, so at most 128 bytes = kHdrSegs segments)
-        const uint32_t a0_32 = (uint32_t)S & 16u;
-        const uint32_t hb_end = ((a0_32 + ((uint32_t)S & 15u) + kHdrNeed + 31u) & ~31u) - a0_32;
-        u32x4 seg[kHdrSegs];
-#pragma unroll
-        for (int i = 0; i < kHdrSegs; ++i)  // past hb_end: out of range, reads 0, no traffic
-            seg[i] = load_segment<false>(hrsrc, 16u * i < hb_end ? hoff + 16u * i : 0xFFFFFFF0u, 0u);
-        FrameLane fl;
-        uint32_t r;
-        bool streamed = false;
-        if constexpr (SU > 0) {
-            if (stream_ok(S, E, lane, cnt)) {
-                // (C') stream prefixes at each frame's L4 start and end. The first windows'
-                // loads go out now, behind the header loads, and arrive during the parse.
-                const int lastl = cnt - 1;
-                const uint64_t X1 =
-                    ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(E >> 32), lastl)
-                     << 32) |
-                    (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)E, lastl);
-                StreamRun<SU, NT, AIPSTACK_FRAME_PREFETCH(SU)> run;
-                run.begin(base, X1, voff);
-                fl = parse_lane<TX, true>(seg, S, len, hb_end);
-                // frames without an L4 sum (and lanes past the batch) put both at X1
-                const bool use = lane < cnt && fl.l4;
-                const uint64_t bs[2] = {use ? fl.l4s : X1, use ? fl.l4e : X1};
-                uint32_t h[2], hx;
-                run.prefixes(bs, h, hx, voff);
-                r = fold16(h[1] - h[0] - fl.fhalf);  // exact halves-sum, < 2^32
-                streamed = true;
-            }
+        int cnt;
+        const FrameOut o = process_chunk<TX, U, P, NT, SU>(desc, p0, n, lane, voff, not_lane0, cnt);
+        if (lane < cnt) {
+            if constexpr (SPLIT)
+                records[p0 + lane] = (uint64_t)o.w0 | (uint64_t)o.w1 << 32;
+            else
+                store_frame<TX>(o.S, o.w0, o.w1, status, p0 + lane);
         }
-        if (!streamed) {
-            fl = parse_lane<TX, false>(seg, S, len, hb_end);
-            const bool need = fl.ce != fl.cs;
-            const LaneMeta meta = lane_meta(fl.cs, fl.ce);
-
-            // (C) the remaining L4 bytes, one frame per wave, P frames' loads in flight
-            NoMaskHook hook;
-            const uint32_t sums = sum_lane_packets<U, P, AIPSTACK_ROWS_FRAMES, NT>(
-                meta, __builtin_amdgcn_ballot_w64(need), lane, voff, not_lane0, hook);
-            // both parts (< 2^24 + 2^17), folded
-            r = fold16(sums + fold16(fl.part));
-        }
-
-        // (D) per-lane finish: oriented by the L4 start
-        if ((fl.l4s & 1u) == 0)  // L4 start even: little-endian pairing -> big-endian
-            r = bswap16(r);
-        const uint64_t m = (uint64_t)fl.words + r;
-        uint32_t chk = (~fold16((uint32_t)m + (uint32_t)(m >> 32))) & 0xFFFFu;
-        int v = fl.pre;
-        if (TX) {
-            if (fl.udp && chk == 0) chk = 0xFFFFu;                  // udp/IpUdpProto.h:176-178
-            if constexpr (SPLIT) {
-                const uint64_t rec = tx_record(fl.hchk, chk, fl.fld, fl.ip_ok, fl.l4, v);
-                if (lane < cnt) {
-#if AIPSTACK_TX_RECORD_MODE == 0
-                    records[p0 + lane] = rec;
-#elif AIPSTACK_TX_RECORD_MODE == 1  // experiments (wrong output from 3 on): nontemporal,
-                    __builtin_nontemporal_store(rec, records + p0 + lane);
-#elif AIPSTACK_TX_RECORD_MODE == 3  // 4-, 2-, 1-byte records, none
-                    reinterpret_cast<uint32_t *>(records)[p0 + lane] = (uint32_t)rec;
-#elif AIPSTACK_TX_RECORD_MODE == 4
-                    reinterpret_cast<uint16_t *>(records)[p0 + lane] = (uint16_t)rec;
-#elif AIPSTACK_TX_RECORD_MODE == 5
-                    reinterpret_cast<uint8_t *>(records)[p0 + lane] = (uint8_t)rec;
-#else
-                    asm volatile("" ::"v"(rec));
-#endif
-                }
-            } else {
-                if (fl.ip_ok)
-                    store_be16(S + 24, fl.hchk);
-                if (fl.l4)
-                    store_be16(S + (uint64_t)fl.fld, chk);
-            }
-        } else if (fl.l4) {
-            v = chk == 0 ? AIPSTACK_RX_ACCEPT : AIPSTACK_RX_DROP_L4_CHKSUM;
-        }
-        if (!SPLIT && lane < cnt)  // split Tx: the status travels in the record
-            status[p0 + lane] = (uint8_t)v;
     }
 }
 
@@ -406,6 +404,8 @@ int launch_frames(const void *d_base, const uint64_t *d_offsets, uint64_t n, uin
     const uint64_t nchunks = (n + kWave - 1) / kWave;
     const int cus = device_cu_count();
     if (cus <= 0) return AIPSTACK_CHKSUM_EHIP;
+    CsrDesc desc{(uint64_t)(uintptr_t)d_base, d_offsets};
+    const int su = tuning_stream_windows(8);  // measured: 8 > 4 > off > 2 (RX and TX)
     const int wpc = tuning_waves_per_cu();
     const uint64_t target_waves = (uint64_t)cus * (wpc > 0 ? wpc : 128);
     uint64_t cpw = (nchunks + target_waves - 1) / target_waves;
@@ -413,8 +413,6 @@ int launch_frames(const void *d_base, const uint64_t *d_offsets, uint64_t n, uin
     const uint64_t waves = (nchunks + cpw - 1) / cpw;
     const uint64_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
     if (blocks > 0x7FFFFFFFull || cpw > 0xFFFFFFFFull) return AIPSTACK_CHKSUM_EINVAL;
-    CsrDesc desc{(uint64_t)(uintptr_t)d_base, d_offsets};
-    const int su = tuning_stream_windows(8);  // measured: 8 > 4 > off > 2 (RX and TX)
 #define AIPSTACK_LAUNCH_FRAMES(P, SU)                                                          \
     hipLaunchKernelGGL((frame_kernel<TX, 2, P, true, SU, SPLIT>), dim3((unsigned)blocks),        \
                        dim3(kBlock), 0, stream, desc, n, (uint32_t)cpw, d_status, d_records)
