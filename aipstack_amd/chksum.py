@@ -347,7 +347,9 @@ def chksum_batch_seeded_csr(buf, offsets, states, *, out=None, stream=None):
 class ChksumEngine:
     """Host-memory streaming engine (C-ABI ``aipstack_chksum_engine_*``): checksums
     batches held in HOST memory (numpy arrays) and returns results in host memory,
-    pipelining H2D / kernel / D2H over ``nstreams`` HIP streams."""
+    pipelining H2D / kernel / D2H over ``nstreams`` HIP streams. ``strided`` / ``csr`` are
+    synchronous; ``submit_strided`` / ``submit_csr`` return a ticket at once and
+    ``poll`` / ``wait`` complete it, so the caller can prepare its next batch meanwhile."""
 
     def __init__(self, device: int = 0, chunk_bytes: int = 0, nstreams: int = 2):
         self._lib = _lib.load()
@@ -357,12 +359,14 @@ class ChksumEngine:
                "aipstack_chksum_engine_create")
         self._h = h
         self._registered = []
+        self._inflight = {}
 
     def close(self) -> None:
         if self._h:
-            self._lib.aipstack_chksum_engine_destroy(self._h)
+            self._lib.aipstack_chksum_engine_destroy(self._h)  # waits for every stream
             self._h = None
             self._registered = []
+            self._inflight = {}
 
     def __enter__(self):
         return self
@@ -407,6 +411,59 @@ class ChksumEngine:
             self._h, buf.ctypes.data, stride, length, n, out.ctypes.data,
             AIPSTACK_CHKSUM_FINAL if final else 0), "aipstack_chksum_engine_host_strided")
         return out
+
+    # ---- asynchronous batches: submit returns a ticket, poll / wait complete it --------
+
+    def submit_strided(self, buf: np.ndarray, stride: int, length: int, n: int, *, out=None,
+                       final: bool = False):
+        """Enqueue a strided batch; returns (ticket, out). `out` is filled when the batch
+        completes (wait / poll); a registered `buf` must not change until then."""
+        if n and (n - 1) * stride + length > buf.nbytes:
+            raise ValueError("batch exceeds buf")
+        out = self._host_args(buf, out, n)
+        t = ctypes.c_uint64(0)
+        st = self._lib.aipstack_chksum_engine_submit_strided(
+            self._h, buf.ctypes.data, stride, length, n, out.ctypes.data,
+            AIPSTACK_CHKSUM_FINAL if final else 0, ctypes.byref(t))
+        self._keep(t.value, buf, out)
+        _check(st, "aipstack_chksum_engine_submit_strided")
+        return t.value, out
+
+    def submit_csr(self, buf: np.ndarray, offsets: np.ndarray, *, out=None,
+                   final: bool = False):
+        """Enqueue a CSR batch; returns (ticket, out) (see submit_strided)."""
+        o = np.ascontiguousarray(offsets, dtype=np.uint64)
+        n = o.size - 1
+        if n > 0 and int(o[-1]) > buf.nbytes:
+            raise ValueError("offsets exceed buf")
+        out = self._host_args(buf, out, n)
+        t = ctypes.c_uint64(0)
+        st = self._lib.aipstack_chksum_engine_submit_csr(
+            self._h, buf.ctypes.data, o.ctypes.data, max(n, 0), out.ctypes.data,
+            AIPSTACK_CHKSUM_FINAL if final else 0, ctypes.byref(t))
+        self._keep(t.value, buf, out)
+        _check(st, "aipstack_chksum_engine_submit_csr")
+        return t.value, out
+
+    def _keep(self, ticket, *arrays):
+        # the buffers the GPU and the completion still use stay alive until completion
+        if ticket:
+            self._inflight[ticket] = arrays
+
+    def poll(self, ticket: int) -> bool:
+        """True once batch `ticket` is complete (its `out` filled); False while running."""
+        st = self._lib.aipstack_chksum_engine_poll(self._h, ticket)
+        if st == 1:
+            return False
+        self._inflight.pop(ticket, None)
+        _check(st, "aipstack_chksum_engine_poll")
+        return True
+
+    def wait(self, ticket: int) -> None:
+        """Block until batch `ticket` is complete."""
+        st = self._lib.aipstack_chksum_engine_wait(self._h, ticket)
+        self._inflight.pop(ticket, None)
+        _check(st, "aipstack_chksum_engine_wait")
 
     def csr(self, buf: np.ndarray, offsets: np.ndarray, *, out=None,
             final: bool = False) -> np.ndarray:

@@ -11,8 +11,14 @@
 // Host buffers that were registered with aipstack_chksum_engine_register() (page-locked
 // via hipHostRegister, as a TAP/socket ring would be once at start-up) are copied by DMA
 // straight from the caller's memory; other host memory is first copied on the CPU into
-// pinned staging (the slower "pageable" path). Each call is synchronous for the caller.
-
+// pinned staging (the slower "pageable" path).
+//
+// Batches are submitted (aipstack_chksum_engine_submit_*: enqueue and return a ticket) and
+// completed (_poll: non-blocking, _wait: blocking); the synchronous calls are submit +
+// wait. A receive loop can therefore read() the next frames into its ring while the GPU
+// works on the previous batch. Each slot (stream + staging) carries the ticket of the
+// batch piece it holds; a submit that needs a busy slot first completes that slot's piece
+// (back-pressure after nstreams pieces in flight).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -41,6 +47,7 @@ struct Slot {
     bool busy = false;
     uint16_t *user_out = nullptr;  // where h_out goes once the slot completes
     uint64_t count = 0;
+    uint64_t ticket = 0;           // batch this slot's piece belongs to
 };
 
 struct Region {
@@ -56,7 +63,11 @@ struct aipstack_chksum_engine {
     uint64_t chunk_packets = 0;
     std::vector<Slot> slots;
     std::vector<Region> registered;
-    std::mutex mu;  // one batch at a time per engine
+    size_t next_slot = 0;      // round robin over the slots, across batches
+    uint64_t next_ticket = 1;  // tickets are never 0
+    uint64_t failed_ticket = 0;  // most recent batch a completion error was seen for
+    int failed_status = 0;
+    std::mutex mu;  // serialises the calls on one engine
 };
 
 namespace {
@@ -83,30 +94,44 @@ void release(aipstack_chksum_engine *e) {
     for (const Region &r : e->registered) (void)hipHostUnregister(const_cast<char *>(r.p));
 }
 
-// Wait for slot s to finish and hand its results to the caller.
-int drain(Slot &s) {
+// Complete slot s: wait for it (blocking) or only if it is done (non-blocking: returns
+// 1 while it is still running), then hand its results to the caller. A HIP error is
+// recorded against the slot's ticket.
+int drain(aipstack_chksum_engine *e, Slot &s, bool blocking = true) {
     if (!s.busy) return AIPSTACK_CHKSUM_OK;
-    int st = check_hip(hipEventSynchronize(s.done));
-    if (st == AIPSTACK_CHKSUM_OK) std::memcpy(s.user_out, s.h_out, s.count * sizeof(uint16_t));
+    hipError_t r;
+    if (blocking) {
+        r = hipEventSynchronize(s.done);
+    } else {
+        r = hipEventQuery(s.done);
+        if (r == hipErrorNotReady) return 1;
+    }
+    const int st = check_hip(r);
+    if (st == AIPSTACK_CHKSUM_OK) {
+        std::memcpy(s.user_out, s.h_out, s.count * sizeof(uint16_t));
+    } else {
+        e->failed_ticket = s.ticket;
+        e->failed_status = st;
+    }
     s.busy = false;
     return st;
 }
 
-// Pipeline over chunks. next(i0, &i1, &src, &bytes, &dst_base_shift) describes chunk
-// [i0, i1) of packets and its byte range in host memory.
+// Enqueue one batch as chunks over the slots. chunker(i0, &i1, &src, &bytes) describes
+// chunk [i0, i1) of packets and its byte range in host memory; launch(slot, i0, i1)
+// enqueues its kernel. Returns the status of the enqueue; *ticket identifies the batch.
 template <class Chunker, class Launch>
-int pipeline(aipstack_chksum_engine *e, uint64_t n, uint16_t *h_out, Chunker chunker,
-             Launch launch) {
-    std::lock_guard<std::mutex> lock(e->mu);
+int enqueue(aipstack_chksum_engine *e, uint64_t n, uint16_t *h_out, Chunker chunker,
+            Launch launch, uint64_t *ticket) {
     if (hipSetDevice(e->device) != hipSuccess) return AIPSTACK_CHKSUM_ENODEV;
+    const uint64_t t = e->next_ticket++;
+    *ticket = t;
     int status = AIPSTACK_CHKSUM_OK;
     uint64_t i0 = 0;
-    size_t k = 0;
     while (i0 < n && status == AIPSTACK_CHKSUM_OK) {
-        Slot &s = e->slots[k % e->slots.size()];
-        ++k;
-        status = drain(s);
-        if (status != AIPSTACK_CHKSUM_OK) break;
+        Slot &s = e->slots[e->next_slot];
+        e->next_slot = (e->next_slot + 1) % e->slots.size();
+        (void)drain(e, s);  // an earlier piece (this batch's or an older one's) completes
         uint64_t i1 = 0;
         const char *src = nullptr;
         uint64_t bytes = 0;
@@ -128,13 +153,29 @@ int pipeline(aipstack_chksum_engine *e, uint64_t n, uint16_t *h_out, Chunker chu
         s.busy = status == AIPSTACK_CHKSUM_OK;
         s.user_out = h_out + i0;
         s.count = cnt;
+        s.ticket = t;
         i0 = i1;
     }
-    for (Slot &s : e->slots) {
-        const int st = drain(s);
-        if (status == AIPSTACK_CHKSUM_OK) status = st;
+    if (status != AIPSTACK_CHKSUM_OK) {
+        e->failed_ticket = t;
+        e->failed_status = status;
     }
     return status;
+}
+
+// Complete batch `ticket`: 0 = done (results in place), 1 = still running (non-blocking
+// only), < 0 = it failed.
+int complete(aipstack_chksum_engine *e, uint64_t ticket, bool blocking) {
+    if (ticket == 0 || ticket >= e->next_ticket) return AIPSTACK_CHKSUM_EINVAL;
+    if (hipSetDevice(e->device) != hipSuccess) return AIPSTACK_CHKSUM_ENODEV;
+    int pending = 0;
+    for (Slot &s : e->slots) {
+        if (!s.busy || s.ticket != ticket) continue;
+        const int st = drain(e, s, blocking);
+        if (st == 1) pending = 1;
+    }
+    if (e->failed_ticket == ticket) return e->failed_status;
+    return pending;
 }
 
 }  // namespace
@@ -178,7 +219,7 @@ extern "C" int aipstack_chksum_engine_create(int device, uint64_t chunk_bytes, i
 extern "C" void aipstack_chksum_engine_destroy(aipstack_chksum_engine *e) {
     if (!e) return;
     (void)hipSetDevice(e->device);
-    release(e);
+    release(e);  // waits for every stream: pieces still in flight finish, unreported
     delete e;
 }
 
@@ -206,11 +247,12 @@ extern "C" int aipstack_chksum_engine_unregister(aipstack_chksum_engine *e, void
     return AIPSTACK_CHKSUM_EINVAL;
 }
 
-extern "C" int aipstack_chksum_engine_host_strided(aipstack_chksum_engine *e, const void *h_base,
-                                                   uint64_t stride, uint32_t len, uint64_t n,
-                                                   uint16_t *h_out, uint32_t flags) {
-    if (!e || !h_base || !h_out || len > AIPSTACK_CHKSUM_MAX_LEN) return AIPSTACK_CHKSUM_EINVAL;
-    if (n == 0) return AIPSTACK_CHKSUM_OK;
+extern "C" int aipstack_chksum_engine_submit_strided(aipstack_chksum_engine *e,
+                                                     const void *h_base, uint64_t stride,
+                                                     uint32_t len, uint64_t n, uint16_t *h_out,
+                                                     uint32_t flags, uint64_t *ticket) {
+    if (!e || !h_base || !h_out || !ticket || len > AIPSTACK_CHKSUM_MAX_LEN)
+        return AIPSTACK_CHKSUM_EINVAL;
     // packets per chunk: the chunk's byte span (i1-i0-1)*stride + len must fit
     uint64_t per = stride ? (e->chunk_bytes - len) / stride + 1 : e->chunk_packets;
     per = std::min<uint64_t>(std::max<uint64_t>(per, 1), e->chunk_packets);
@@ -225,14 +267,15 @@ extern "C" int aipstack_chksum_engine_host_strided(aipstack_chksum_engine *e, co
         return aipstack_chksum_batch_strided(s.d_bytes, stride, len, i1 - i0, s.d_out, flags,
                                              s.stream);
     };
-    return pipeline(e, n, h_out, chunker, launch);
+    std::lock_guard<std::mutex> lock(e->mu);
+    return enqueue(e, n, h_out, chunker, launch, ticket);
 }
 
-extern "C" int aipstack_chksum_engine_host_csr(aipstack_chksum_engine *e, const void *h_base,
-                                               const uint64_t *h_offsets, uint64_t n,
-                                               uint16_t *h_out, uint32_t flags) {
-    if (!e || !h_base || !h_offsets || !h_out) return AIPSTACK_CHKSUM_EINVAL;
-    if (n == 0) return AIPSTACK_CHKSUM_OK;
+extern "C" int aipstack_chksum_engine_submit_csr(aipstack_chksum_engine *e, const void *h_base,
+                                                 const uint64_t *h_offsets, uint64_t n,
+                                                 uint16_t *h_out, uint32_t flags,
+                                                 uint64_t *ticket) {
+    if (!e || !h_base || !h_offsets || !h_out || !ticket) return AIPSTACK_CHKSUM_EINVAL;
     for (uint64_t i = 0; i < n; ++i)  // contract check: non-decreasing, each <= 65535
         if (h_offsets[i + 1] < h_offsets[i] || h_offsets[i + 1] - h_offsets[i] > AIPSTACK_CHKSUM_MAX_LEN)
             return AIPSTACK_CHKSUM_EINVAL;
@@ -258,5 +301,46 @@ extern "C" int aipstack_chksum_engine_host_csr(aipstack_chksum_engine *e, const 
         if (st != AIPSTACK_CHKSUM_OK) return st;
         return aipstack_chksum_batch_csr(s.d_bytes, s.d_off, cnt, s.d_out, flags, s.stream);
     };
-    return pipeline(e, n, h_out, chunker, launch);
+    std::lock_guard<std::mutex> lock(e->mu);
+    return enqueue(e, n, h_out, chunker, launch, ticket);
+}
+
+extern "C" int aipstack_chksum_engine_poll(aipstack_chksum_engine *e, uint64_t ticket) {
+    if (!e) return AIPSTACK_CHKSUM_EINVAL;
+    std::lock_guard<std::mutex> lock(e->mu);
+    return complete(e, ticket, false);
+}
+
+extern "C" int aipstack_chksum_engine_wait(aipstack_chksum_engine *e, uint64_t ticket) {
+    if (!e) return AIPSTACK_CHKSUM_EINVAL;
+    std::lock_guard<std::mutex> lock(e->mu);
+    return complete(e, ticket, true);
+}
+
+extern "C" int aipstack_chksum_engine_host_strided(aipstack_chksum_engine *e, const void *h_base,
+                                                   uint64_t stride, uint32_t len, uint64_t n,
+                                                   uint16_t *h_out, uint32_t flags) {
+    if (!e || !h_base || !h_out || len > AIPSTACK_CHKSUM_MAX_LEN) return AIPSTACK_CHKSUM_EINVAL;
+    if (n == 0) return AIPSTACK_CHKSUM_OK;
+    uint64_t t = 0;
+    const int st = aipstack_chksum_engine_submit_strided(e, h_base, stride, len, n, h_out, flags, &t);
+    if (st != AIPSTACK_CHKSUM_OK) {
+        if (t) (void)aipstack_chksum_engine_wait(e, t);  // pieces already in flight
+        return st;
+    }
+    return aipstack_chksum_engine_wait(e, t);
+}
+
+extern "C" int aipstack_chksum_engine_host_csr(aipstack_chksum_engine *e, const void *h_base,
+                                               const uint64_t *h_offsets, uint64_t n,
+                                               uint16_t *h_out, uint32_t flags) {
+    if (!e || !h_base || !h_offsets || !h_out) return AIPSTACK_CHKSUM_EINVAL;
+    if (n == 0) return AIPSTACK_CHKSUM_OK;
+    uint64_t t = 0;
+    const int st = aipstack_chksum_engine_submit_csr(e, h_base, h_offsets, n, h_out, flags, &t);
+    if (st != AIPSTACK_CHKSUM_OK) {
+        if (t) (void)aipstack_chksum_engine_wait(e, t);
+        return st;
+    }
+    return aipstack_chksum_engine_wait(e, t);
 }

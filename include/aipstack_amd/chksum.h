@@ -152,8 +152,10 @@ int aipstack_chksum_tx_fill_split(void *d_base, const uint64_t *d_offsets, uint6
  * D2H copies over `nstreams` HIP streams in chunks of at most `chunk_bytes` (0 = 64 MiB)
  * of whole packets. Host buffers registered with aipstack_chksum_engine_register()
  * (page-locked once, e.g. a receive ring) are DMA'd directly; other host memory is first
- * copied into the engine's pinned staging. Calls are synchronous; one batch at a time
- * per engine (calls on one engine from several threads are serialised). */
+ * copied into the engine's pinned staging. The host_* calls are synchronous; the submit_*
+ * calls enqueue a batch and return a ticket at once, so the caller can fill its next batch
+ * (e.g. read() frames into its ring) while the GPU works; _poll / _wait complete it. Calls
+ * on one engine from several threads are serialised. */
 typedef struct aipstack_chksum_engine aipstack_chksum_engine;
 
 int aipstack_chksum_engine_create(int device, uint64_t chunk_bytes, int nstreams,
@@ -173,6 +175,24 @@ int aipstack_chksum_engine_host_strided(aipstack_chksum_engine *engine, const vo
 int aipstack_chksum_engine_host_csr(aipstack_chksum_engine *engine, const void *h_base,
                                     const uint64_t *h_offsets, uint64_t n, uint16_t *h_out,
                                     uint32_t flags);
+
+/* Asynchronous form of the two calls above: enqueue the batch and return at once with
+ * *ticket set. h_out is written when the batch completes; a REGISTERED h_base must stay
+ * unchanged until then (it is DMA'd while the GPU runs), pageable input is copied before
+ * the call returns. At most nstreams chunks are in flight per engine: a submit that needs
+ * a busy stream first completes the piece on it. Returns _OK or a negative status (a
+ * failure part-way leaves the pieces already enqueued to _wait). */
+int aipstack_chksum_engine_submit_strided(aipstack_chksum_engine *engine, const void *h_base,
+                                          uint64_t stride, uint32_t len, uint64_t n,
+                                          uint16_t *h_out, uint32_t flags, uint64_t *ticket);
+int aipstack_chksum_engine_submit_csr(aipstack_chksum_engine *engine, const void *h_base,
+                                      const uint64_t *h_offsets, uint64_t n, uint16_t *h_out,
+                                      uint32_t flags, uint64_t *ticket);
+
+/* Completion of a submitted batch: 0 = done (h_out holds the results), 1 = still running
+ * (poll only), negative = it failed (or _EINVAL for an unknown ticket). _wait blocks. */
+int aipstack_chksum_engine_poll(aipstack_chksum_engine *engine, uint64_t ticket);
+int aipstack_chksum_engine_wait(aipstack_chksum_engine *engine, uint64_t ticket);
 
 /* ---- diagnostics ------------------------------------------------------------------ */
 

@@ -76,6 +76,11 @@ int main() {
     CHECK(aipstack_chksum_engine_unregister(nullptr, dummy) == EINVAL_);
     CHECK(aipstack_chksum_engine_host_strided(nullptr, dummy, 1, 1, 1, out, 0) == EINVAL_);
     CHECK(aipstack_chksum_engine_host_csr(nullptr, dummy, off, 1, out, 0) == EINVAL_);
+    std::uint64_t ticket = 0;
+    CHECK(aipstack_chksum_engine_submit_strided(nullptr, dummy, 1, 1, 1, out, 0, &ticket) == EINVAL_);
+    CHECK(aipstack_chksum_engine_submit_csr(nullptr, dummy, off, 1, out, 0, &ticket) == EINVAL_);
+    CHECK(aipstack_chksum_engine_poll(nullptr, 1) == EINVAL_);
+    CHECK(aipstack_chksum_engine_wait(nullptr, 1) == EINVAL_);
     aipstack_chksum_engine_destroy(nullptr);  // no-op
 
     const int dev = aipstack_chksum_device_check(0);
@@ -93,6 +98,19 @@ int main() {
         CHECK(aipstack_chksum_engine_register(e, nullptr, 64) == EINVAL_);
         CHECK(aipstack_chksum_engine_register(e, dummy, 0) == EINVAL_);
         CHECK(aipstack_chksum_engine_unregister(e, dummy) == EINVAL_);  // never registered
+        CHECK(aipstack_chksum_engine_submit_csr(e, dummy, bad_off, 2, out, 0, &ticket) == EINVAL_);
+        CHECK(aipstack_chksum_engine_submit_csr(e, dummy, off, 1, out, 0, nullptr) == EINVAL_);
+        CHECK(aipstack_chksum_engine_poll(e, 0) == EINVAL_);          // never a ticket
+        CHECK(aipstack_chksum_engine_wait(e, 1u << 30) == EINVAL_);   // not issued yet
+        // a real batch through submit + poll/wait
+        std::vector<char> pk(4 * 1500, 0x5A);
+        std::uint16_t res[4] = {0, 0, 0, 0};
+        CHECK(aipstack_chksum_engine_submit_strided(e, pk.data(), 1500, 1500, 4, res, 0, &ticket) == 0);
+        CHECK(ticket != 0);
+        while (aipstack_chksum_engine_poll(e, ticket) == 1) {
+        }
+        CHECK(aipstack_chksum_engine_wait(e, ticket) == 0);
+        for (std::uint16_t r : res) CHECK(r == IpChksumInverted(pk.data(), 1500));
         aipstack_chksum_engine_destroy(e);
     } else {
         CHECK(ec == dev && e == nullptr);

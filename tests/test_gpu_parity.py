@@ -419,6 +419,35 @@ def test_engine_host_csr(oracle, register):
         assert np.array_equal(got, oracle.batch_csr(buf, off))
 
 
+def test_engine_async_submit_poll_wait(oracle):
+    """Non-blocking engine: several batches in flight at once (registered and pageable,
+    strided and CSR), completed out of submission order by poll and wait; results as the
+    synchronous calls give."""
+    rng = np.random.default_rng(31)
+    a = rng.integers(0, 256, size=300 * 1500, dtype=np.uint8)      # registered, strided
+    b_buf, b_off = synth.mixed_batch(5000)                          # pageable, CSR
+    c = rng.integers(0, 256, size=4000 * 9000, dtype=np.uint8)      # pageable, big strided
+    with A.ChksumEngine(0, chunk_bytes=1 << 20, nstreams=3) as eng:
+        eng.register(a)
+        ta, oa = eng.submit_strided(a, 1500, 1500, 300)
+        tb, ob = eng.submit_csr(b_buf, b_off, final=True)
+        tc, oc = eng.submit_strided(c, 9000, 9000, 4000)
+        assert len({ta, tb, tc}) == 3
+        # the caller is free meanwhile; complete the last one first
+        eng.wait(tc)
+        spins = 0
+        while not eng.poll(tb):
+            spins += 1
+            assert spins < 10_000_000
+        eng.wait(ta)
+        assert eng.poll(ta)  # already complete: stays complete
+        assert np.array_equal(oa, oracle.batch_strided(a, 1500, 1500, 300))
+        assert np.array_equal(ob, oracle.batch_csr(b_buf, b_off, final=True))
+        assert np.array_equal(oc, oracle.batch_strided(c, 9000, 9000, 4000))
+        with pytest.raises(A.ChksumError):
+            eng.wait(10**9)  # never issued
+
+
 def test_engine_rejects_bad_offsets():
     buf = np.zeros(1 << 20, dtype=np.uint8)
     with A.ChksumEngine(0) as eng:
