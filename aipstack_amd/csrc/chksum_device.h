@@ -699,98 +699,60 @@ __device__ __forceinline__ int wave_max_scan(int v) {
 }
 
 // ---------------------------------------------------------------------------------
-// Compact streams: byte runs that are NOT back to back in memory (the chain kernel's chunks,
-// anywhere in memory) read as one stream of just their 16-byte segments.
-// The segments of run j, in order, get the compact indices [cs_j, cs_j + ns_j); window w
-// is compact indices [64w, 64w + 64) and lane k loads index 64w + k from wherever the
-// Loader says it lives. Over that compact byte stream the prefixes work exactly as in
-// StreamRun: run j is the compact bytes [16 cs_j + (a_j & 15), that + l_j), so its exact
-// halves-sum is H(end) - H(start), the head and tail bytes outside it masked at the two
-// boundaries. Bytes outside every run's segments are never read.
+// Gathered stream (the chain kernel): up to 64 chunks anywhere in memory (lane j: chunk
+// [a_j, a_j + l_j), l_j <= 65535, empty chunks allowed) read as ONE stream of just their
+// 16-byte segments. The segments of chunk j, in order, get the compact indices
+// [cs_j, cs_j + ns_j) (cs = exclusive scan of the counts); window w is compact indices
+// [64w, 64w + 64), and lane k loads index c = 64w + k from the chunk that owns it, at
+// gbase_owner + 16 c (gbase_j = (a_j & ~15) - 16 cs_j).
 //
-// compact_sums() is software-pipelined: group g + 1's loads (U windows) are issued before
-// group g is consumed. The loop always runs whole pairs of groups and the next group is
-// issued unconditionally (a window past the stream sums zeros and moves no boundary), so
-// the loads stay straight-line and every wait is counted (vmcnt(N)), also across the back
-// edge. A Loader provides issue(w, v): windows [w, w + U) into v, lanes past the stream's
-// T segments loading anything readable (their sums are dropped here).
+// Owners: per group of U windows each chunk marks, in LDS, the lane where it starts (one
+// write per lane; lanes that start nothing write a trash slot), then a max-scan per window.
+// The owner also tells the loading lane whether its segment is the chunk's first (bytes
+// below a_j & 15 are not the chunk's) or last (bytes from the chunk's end on are not), and
+// the lane masks those bytes off before it sums the segment ("cleaned" segments, mask table
+// in LDS). The cleaned segments of chunk j then hold exactly its bytes, so with
+// G_j = the prefix of cleaned halves-sums up to segment cs_j (a segment-aligned position: no
+// partial segment to fetch), chunk j's exact halves-sum is G_{j+1} - G_j: one boundary per
+// lane, evaluated with one ds_bpermute of the window's exclusive scan. A segment shared by
+// two chunks is loaded once for each (the second time from L2); bytes outside every chunk's
+// segments are never read, so chunks may sit in separate allocations (a 16-byte segment
+// around a mapped byte is mapped). Lanes past the stream re-read its last segment and count
+// 0, so every address stays inside a chunk.
+//
+// Software-pipelined: group g + 1's owners and loads are issued before group g is
+// consumed. The loop always runs whole pairs of groups and the next group is issued
+// unconditionally (a window past the stream sums zeros and holds no boundary), so the loads
+// stay straight-line and every wait is counted (vmcnt(N)), also across the back edge.
 // ---------------------------------------------------------------------------------
-template <int U, class Loader>
-__device__ __forceinline__ uint32_t compact_sums(uint32_t T, uint32_t b0, uint32_t b1,
-                                                 int lane, Loader &ld) {
-    const uint32_t nwin = (T + (uint32_t)kWave - 1u) >> 6;
-    const uint32_t bnd[2] = {b0, b1};
-    uint32_t bwin[2], below[2][4], h[2] = {0u, 0u};
-    int bsrc[2];
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        bwin[k] = bnd[k] >> 10;
-        bsrc[k] = (int)(((bnd[k] >> 4) & 63u) << 2);
-#pragma unroll
-        for (int d = 0; d < 4; ++d) below[k][d] = dword_keep(0, (int)(bnd[k] & 15u) - 4 * d);
-    }
-    uint32_t carry = 0;  // H at the current window's start, mod 2^32
-    auto consume = [&](uint32_t w, const u32x4 (&v)[U]) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t wu = w + (uint32_t)u;
-            const uint32_t c0 = wu * (uint32_t)kWave + (uint32_t)lane;
-            uint32_t s = halves(v[u][0], halves(v[u][1], halves(v[u][2], halves(v[u][3], 0u))));
-            s = c0 < T ? s : 0u;
-            const uint32_t incl = wave_incl_scan(s);
-            const uint32_t excl = incl - s;
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                if (__builtin_amdgcn_ballot_w64(bwin[k] == wu)) {
-                    uint32_t part = (uint32_t)__builtin_amdgcn_ds_bpermute(bsrc[k], (int)excl);
-#pragma unroll
-                    for (int d = 0; d < 4; ++d)
-                        part = halves(
-                            (uint32_t)__builtin_amdgcn_ds_bpermute(bsrc[k], (int)v[u][d]) &
-                                below[k][d],
-                            part);
-                    if (bwin[k] == wu) h[k] = carry + part;
-                }
-            }
-            carry += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-        }
-    };
-    u32x4 va[U], vb[U];
-    ld.issue(0, va);
-    const uint32_t npairs = (nwin + 2u * U - 1u) / (2u * U);
-    for (uint32_t i = 0, w = 0; i < npairs; ++i, w += 2u * U) {
-        ld.issue(w + U, vb);
-        consume(w, va);
-        ld.issue(w + 2u * U, va);
-        consume(w + U, vb);
-    }
-    // a boundary at compact index T when T is a multiple of 64: past the last window
-#pragma unroll
-    for (int k = 0; k < 2; ++k)
-        if (bwin[k] >= nwin) h[k] = carry;
-    return h[1] - h[0];
-}
-
-// Loader for up to 64 chunks anywhere in memory (lane j: chunk [a_j, a_j + l_j)), the
-// chain kernel's: lane k finds the chunk owning its compact index per window (each chunk
-// marks the lane where it starts in LDS -- one write per lane per group, lanes that start
-// nothing write a trash slot -- then a max-scan) and loads from that chunk's address with
-// a global load. Lanes past the stream re-read its last segment: every address stays
-// inside a chunk, so chunks may sit in separate allocations (a 16-byte segment around a
-// mapped byte is mapped).
 constexpr int kGatherSlots = kWave + 1;  // per window: 64 lanes + a trash slot
+
+// LDS table of byte masks: entry head * 16 + (tail - 1) keeps bytes [head, tail) of a
+// 16-byte segment (head 0..15, tail 1..16). Filled once per block by fill_keep_table().
+typedef u32x4 KeepTable[256];
+
+__device__ __forceinline__ void fill_keep_table(KeepTable &t) {
+    for (int i = (int)threadIdx.x; i < 256; i += (int)blockDim.x) {
+        const int head = i >> 4, tail = (i & 15) + 1;
+        t[i] = u32x4{dword_keep(head, tail), dword_keep(head - 4, tail - 4),
+                     dword_keep(head - 8, tail - 8), dword_keep(head - 12, tail - 12)};
+    }
+}
 
 template <int U, bool NT>
 struct ChunkLoader {
     uint32_t T;
     uint32_t gb_lo, gb_hi;  // this lane's chunk: segment c (compact) is at gbase + 16 c
+    uint32_t first_info;    // cs_j | (a_j & 15) << 24: first segment, head bytes to drop
+    uint32_t last_info;     // (cs_j + ns_j - 1) | tail << 24: last segment, bytes kept
     uint32_t mark_slot;     // the lane its chunk starts at, within its window
     uint32_t start_win;     // the window its chunk starts in (~0: empty chunk)
     int cur;                // owner of the previous window's last lane (wave-uniform)
     int lane;
     uint32_t (*mark)[kGatherSlots];
 
-    __device__ __forceinline__ void issue(uint32_t w, u32x4 (&v)[U]) {
+    // Windows [w, w + U): loads into v, and each lane's keep-table index into keep.
+    __device__ __forceinline__ void issue(uint32_t w, u32x4 (&v)[U], uint32_t (&keep)[U]) {
 #pragma unroll
         for (int u = 0; u < U; ++u) mark[u][lane] = 0u;
         __builtin_amdgcn_wave_barrier();
@@ -820,8 +782,14 @@ struct ChunkLoader {
             cur = __builtin_amdgcn_readlane(owner, 63);
             const uint32_t c0 = (w + (uint32_t)u) * (uint32_t)kWave + (uint32_t)lane;
             const uint32_t c = min(c0, T - 1u);
-            const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(owner << 2, (int)gb_lo);
-            const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(owner << 2, (int)gb_hi);
+            const int src = owner << 2;
+            const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)gb_lo);
+            const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)gb_hi);
+            const uint32_t fi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)first_info);
+            const uint32_t li = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)last_info);
+            const uint32_t head = c == (fi & 0xFFFFFFu) ? fi >> 24 : 0u;
+            const uint32_t tail = c == (li & 0xFFFFFFu) ? li >> 24 : 16u;
+            keep[u] = head * 16u + tail - 1u;
             const uint64_t addr = (((uint64_t)hi << 32) | lo) + 16ull * c;
             typedef __attribute__((address_space(1))) const u32x4 gseg;
             const gseg *p = (const gseg *)(addr);
@@ -833,31 +801,67 @@ struct ChunkLoader {
     }
 };
 
-// The chain kernel's 64 chunk sums (lane j: chunk [a_j, a_j + l_j), l_j <= 65535, empty
-// allowed; `mark`: this wave's LDS scratch, U windows of kGatherSlots). Returns lane j's
-// exact halves-sum of its chunk.
+// The chain kernel's 64 chunk sums. `mark`: this wave's LDS scratch (U windows of
+// kGatherSlots); `keep`: the block's mask table (fill_keep_table). Returns lane j's exact
+// halves-sum of its chunk.
 template <int U, bool NT>
 __device__ __forceinline__ uint32_t sum_gathered_chunks(uint64_t a, uint32_t l, int lane,
-                                                        uint32_t (*mark)[kGatherSlots]) {
+                                                        uint32_t (*mark)[kGatherSlots],
+                                                        const KeepTable &keep_table) {
     const uint32_t rs = (uint32_t)a & 15u;
     const uint32_t ns = l ? (rs + l + 15u) >> 4 : 0u;
     const uint32_t ns_incl = wave_incl_scan(ns);
     const uint32_t cs = ns_incl - ns;
     const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)ns_incl, 63);
     if (T == 0) return 0;
+    const uint32_t nwin = (T + (uint32_t)kWave - 1u) >> 6;
     ChunkLoader<U, NT> ld;
     ld.T = T;
     const uint64_t gbase = (a & ~(uint64_t)15) - 16ull * cs;
     ld.gb_lo = (uint32_t)gbase;
     ld.gb_hi = (uint32_t)(gbase >> 32);
+    ld.first_info = cs | rs << 24;
+    ld.last_info = (cs + ns - 1u) | ((((rs + l - 1u) & 15u) + 1u) << 24);
     ld.start_win = ns ? (cs >> 6) : ~0u;
     ld.mark_slot = cs & 63u;
     ld.cur = 0;
     ld.lane = lane;
     ld.mark = mark;
-    // this lane's two boundaries in the compact byte stream (empty chunk: both at 0)
-    const uint32_t b0 = ns ? 16u * cs + rs : 0u;
-    return compact_sums<U>(T, b0, ns ? b0 + l : 0u, lane, ld);
+    // this lane's boundary: G at segment cs (an empty chunk's cs is the next one's)
+    const uint32_t bwin = cs >> 6;
+    const int bsrc = (int)((cs & 63u) << 2);
+    uint32_t g = 0, carry = 0;  // carry: prefix at the current window's start, mod 2^32
+    auto consume = [&](uint32_t w, const u32x4 (&v)[U], const uint32_t (&keep)[U]) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t wu = w + (uint32_t)u;
+            const uint32_t c0 = wu * (uint32_t)kWave + (uint32_t)lane;
+            const u32x4 km = keep_table[keep[u]];
+            uint32_t s = halves(v[u][0] & km[0],
+                                halves(v[u][1] & km[1],
+                                       halves(v[u][2] & km[2], halves(v[u][3] & km[3], 0u))));
+            s = c0 < T ? s : 0u;  // lanes past the stream re-read its last segment
+            const uint32_t incl = wave_incl_scan(s);
+            if (__builtin_amdgcn_ballot_w64(bwin == wu)) {
+                const uint32_t part = (uint32_t)__builtin_amdgcn_ds_bpermute(bsrc, (int)(incl - s));
+                if (bwin == wu) g = carry + part;
+            }
+            carry += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        }
+    };
+    u32x4 va[U], vb[U];
+    uint32_t ka[U], kb[U];
+    ld.issue(0, va, ka);
+    const uint32_t npairs = (nwin + 2u * U - 1u) / (2u * U);
+    for (uint32_t i = 0, w = 0; i < npairs; ++i, w += 2u * U) {
+        ld.issue(w + U, vb, kb);
+        consume(w, va, ka);
+        ld.issue(w + 2u * U, va, ka);
+        consume(w + U, vb, kb);
+    }
+    if (bwin >= nwin) g = carry;  // cs == T on a multiple of 64: past the last window
+    // chunk j ends where chunk j + 1 starts (lane 63: at T, prefix = the final carry)
+    return from_next_lane(g, carry, lane) - g;
 }
 
 // Stream mode for one chunk (stream_ok). Lane j < cnt holds packet j = [S, E); returns

@@ -140,13 +140,16 @@ __device__ __forceinline__ uint32_t parity_below(uint64_t mask, uint32_t s) {  /
 }
 
 template <bool NT, int SU>
-__global__ __launch_bounds__(kBlock) void chksum_chain_kernel(
+__global__ __launch_bounds__(kBlock, 5) void chksum_chain_kernel(
     const uint64_t *__restrict__ chunk_addr, const uint32_t *__restrict__ chunk_len,
     const uint64_t *__restrict__ index, const uint32_t *__restrict__ states, uint64_t n,
     uint32_t chunks_per_wave, uint16_t *__restrict__ out, uint32_t flags) {
     __shared__ uint64_t lds_acc[kWavesPerBlock][kWave];  // per-chain sum of chunk sums
     __shared__ int lds_mark[kWavesPerBlock][kWave];      // chain starting at chunk lane
     __shared__ uint32_t lds_gmark[kWavesPerBlock][SU][kGatherSlots];  // gathered stream owners
+    __shared__ KeepTable lds_keep;                                    // its segment masks
+    fill_keep_table(lds_keep);
+    __syncthreads();
     const int lane = threadIdx.x & (kWave - 1);
     const uint32_t wave_in_block = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerBlock + wave_in_block;
@@ -202,7 +205,8 @@ __global__ __launch_bounds__(kBlock) void chksum_chain_kernel(
             if (before) q ^= carry_par;
             // the 64 chunk sums: one gathered stream over just the chunks' bytes
             const uint32_t sums =
-                sum_gathered_chunks<SU, NT>(a, valid ? l : 0u, lane, lds_gmark[wave_in_block]);
+                sum_gathered_chunks<SU, NT>(a, valid ? l : 0u, lane, lds_gmark[wave_in_block],
+                                            lds_keep);
             uint32_t r = fold16(sums);
             if ((uint32_t)(a & 1) == q)
                 r = bswap16(r);
@@ -460,16 +464,15 @@ extern "C" int aipstack_chksum_batch_chain(const uint64_t *d_chunk_addr,
     if (n == 0) return AIPSTACK_CHKSUM_OK;
     if (!d_chunk_addr || !d_chunk_len || !d_chunk_index || !d_out) return AIPSTACK_CHKSUM_EINVAL;
     if (n > (1ull << 40)) return AIPSTACK_CHKSUM_EINVAL;
-    // SU: gathered-stream windows issued together ("stream" tunable; off is not an option
-    // here: every chunk is summed by the gathered stream)
+    // SU: gathered-stream windows per group ("stream" tunable: 2 or 4; off and 8 map to
+    // 2 -- every chunk goes through the gathered stream, and 8 windows spill registers).
+    // Measured on CHAIN (profiles/r02/bench_CHAIN_cleaned_sweep.jsonl): 2 windows, 73 VGPRs,
+    // 6 waves per SIMD, 286-291 us; 4 windows, 96 VGPRs, 5 waves, 300-302 us.
 #define AIPSTACK_LAUNCH_CHAIN(NT, SU)                                                       \
     return launch_chain<NT, SU>(d_chunk_addr, d_chunk_len, d_chunk_index, d_states, n,     \
                                 d_out, flags, (hipStream_t)stream)
-    if (!tuning().nontemporal.load(std::memory_order_relaxed)) AIPSTACK_LAUNCH_CHAIN(false, 4);
-    switch (tuning_stream_windows(4)) {
-        case 2: AIPSTACK_LAUNCH_CHAIN(true, 2);
-        case 8: AIPSTACK_LAUNCH_CHAIN(true, 8);
-        default: AIPSTACK_LAUNCH_CHAIN(true, 4);
-    }
+    if (!tuning().nontemporal.load(std::memory_order_relaxed)) AIPSTACK_LAUNCH_CHAIN(false, 2);
+    if (tuning_stream_windows(2) == 4) AIPSTACK_LAUNCH_CHAIN(true, 4);
+    AIPSTACK_LAUNCH_CHAIN(true, 2);
 #undef AIPSTACK_LAUNCH_CHAIN
 }

@@ -148,7 +148,9 @@ def test_stream_model_halves_sum_is_exact_for_max_len():
 
 def gathered_model(buf, a, l, U=4):
     """sum_gathered_chunks for one 64-chunk group: lane j = chunk [a[j], a[j] + l[j]) of buf
-    (absolute offsets into buf). Returns each lane's halves-sum (mod 2^32)."""
+    (absolute offsets into buf). Cleaned segments (bytes outside the owner chunk masked by
+    the loading lane), one boundary per lane at its chunk's first segment; returns each
+    lane's halves-sum (mod 2^32)."""
     k = len(a)
     a = [int(x) for x in a] + [0] * (64 - k)
     l = [int(x) for x in l] + [0] * (64 - k)
@@ -161,42 +163,44 @@ def gathered_model(buf, a, l, U=4):
         return [0] * 64
     nwin = (T + 63) >> 6
     gbase = [(a[j] & ~15) - 16 * cs[j] for j in range(64)]
-    bnd = [[16 * cs[j] + rs[j], 16 * cs[j] + rs[j] + l[j]] if ns[j] else [0, 0]
-           for j in range(64)]
-    h = [[0, 0] for _ in range(64)]
+    first = [cs[j] for j in range(64)]
+    last = [cs[j] + ns[j] - 1 for j in range(64)]
+    tail_keep = [((rs[j] + l[j] - 1) & 15) + 1 for j in range(64)]
+    g = [0] * 64
     cur, carry = 0, 0
-    for w0 in range(0, nwin, U):
-        for u in range(U):
-            w = w0 + u
-            mark = [-1] * 64
-            for j in range(64):
-                if ns[j] and (cs[j] >> 6) == w:
-                    mark[cs[j] & 63] = j
-            m = list(np.maximum.accumulate(mark))
-            m = [cur if x < 0 else int(x) for x in m]
-            cur = m[63]
-            raw = np.zeros(64 * 16, dtype=np.uint8)
-            for lane in range(64):
-                c = w * 64 + lane
-                if c < T:
-                    addr = gbase[m[lane]] + 16 * c
-                    raw[lane * 16:lane * 16 + 16] = buf[addr:addr + 16]
-            seg = raw.view("<u2").astype(np.uint64).reshape(64, 8).sum(axis=1)
-            inc = np.cumsum(seg)
-            exc = inc - seg
-            for j in range(64):
-                for kk in range(2):
-                    b = bnd[j][kk]
-                    if b >> 10 == w:
-                        o = (b >> 4) & 63
-                        part = int(exc[o]) + _below(raw[o * 16:o * 16 + 16], b & 15)
-                        h[j][kk] = (carry + part) & M32
-            carry = (carry + int(inc[63])) & M32
+    npairs = (nwin + 2 * U - 1) // (2 * U)
+    for w in range(npairs * 2 * U):            # whole pairs of groups, as the kernel
+        mark = [-1] * 64
+        for j in range(64):
+            if ns[j] and (cs[j] >> 6) == w:
+                mark[cs[j] & 63] = j
+        m = list(np.maximum.accumulate(mark))
+        m = [cur if x < 0 else int(x) for x in m]
+        cur = m[63]
+        seg = np.zeros(64, dtype=np.uint64)
+        for lane in range(64):
+            c0 = w * 64 + lane
+            c = min(c0, T - 1)
+            o = m[lane]
+            head = rs[o] if c == first[o] else 0
+            tail = tail_keep[o] if c == last[o] else 16
+            raw = np.zeros(16, dtype=np.uint8)
+            addr = gbase[o] + 16 * c
+            raw[:] = buf[addr:addr + 16]
+            raw[:head] = 0
+            raw[tail:] = 0
+            if c0 < T:
+                seg[lane] = int(raw.view("<u2").astype(np.uint64).sum())
+        inc = np.cumsum(seg)
+        exc = inc - seg
+        for j in range(64):
+            if cs[j] >> 6 == w:
+                g[j] = (carry + int(exc[cs[j] & 63])) & M32
+        carry = (carry + int(inc[63])) & M32
     for j in range(64):
-        for kk in range(2):
-            if bnd[j][kk] >> 10 >= nwin:
-                h[j][kk] = carry
-    return [(h[j][1] - h[j][0]) & M32 for j in range(64)]
+        if cs[j] >> 6 >= nwin:
+            g[j] = carry
+    return [((g[j + 1] if j < 63 else carry) - g[j]) & M32 for j in range(64)]
 
 
 @pytest.mark.parametrize("U", [2, 4])
