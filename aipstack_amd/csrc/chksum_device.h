@@ -618,7 +618,11 @@ struct StreamRun {
         }
     }
 
-    template <int NB>
+    // h[k] = H(b[k]) for every b[k] in [A, X1], and hx = H(X1). ALIGNED: h[k] = H at the
+    // start of b[k]'s 16-byte segment instead (one ds_bpermute per boundary and window, no
+    // partial segment; the caller adds the bytes of that segment below b[k] from data it
+    // holds itself), except h[k] = hx for b[k] == X1.
+    template <int NB, bool ALIGNED = false>
     __device__ __forceinline__ void prefixes(const uint64_t (&b)[NB], uint32_t (&h)[NB],
                                              uint32_t &hx, uint32_t voff) {
         // each boundary: its window, owner lane (x4 for ds_bpermute), dword masks below it
@@ -631,7 +635,8 @@ struct StreamRun {
             bwin[k] = boff >> 10;
             bsrc[k] = (int)(((boff >> 4) & 63u) << 2);
 #pragma unroll
-            for (int d = 0; d < 4; ++d) below[k][d] = dword_keep(0, (int)(boff & 15u) - 4 * d);
+            for (int d = 0; d < 4; ++d)
+                below[k][d] = ALIGNED ? 0u : dword_keep(0, (int)(boff & 15u) - 4 * d);
             h[k] = 0;
         }
         // X1's segment (the last one; past X1 it holds bytes outside the run): window, lane
@@ -657,12 +662,14 @@ struct StreamRun {
                 for (int k = 0; k < NB; ++k) {
                     if (__builtin_amdgcn_ballot_w64(bwin[k] == wu)) {  // boundaries in window
                         uint32_t part = (uint32_t)__builtin_amdgcn_ds_bpermute(bsrc[k], (int)excl);
+                        if constexpr (!ALIGNED) {
 #pragma unroll
-                        for (int d = 0; d < 4; ++d)
-                            part = halves(
-                                (uint32_t)__builtin_amdgcn_ds_bpermute(bsrc[k], (int)v[u][d]) &
-                                    below[k][d],
-                                part);
+                            for (int d = 0; d < 4; ++d)
+                                part = halves((uint32_t)__builtin_amdgcn_ds_bpermute(
+                                                  bsrc[k], (int)v[u][d]) &
+                                                  below[k][d],
+                                              part);
+                        }
                         if (bwin[k] == wu) h[k] = carry + part;
                     }
                 }

@@ -103,6 +103,29 @@ __global__ __launch_bounds__(kBlock) void tx_scatter_kernel(uint64_t base,
     }
 }
 
+// Halves-sum (the stream's H metric: little-endian 16-bit halves at even absolute
+// addresses) of the bytes [0, o) of one aligned 16-byte segment.
+__device__ __forceinline__ uint32_t halves_below(const u32x4 &x, uint32_t o) {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) acc = halves(x[d] & dword_keep(0, (int)o - 4 * d), acc);
+    return acc;
+}
+
+// The same for the segment at byte `off` (< 128) of a lane's header blocks (aligned
+// segments from A0): the bytes of that segment below `off`. Branch-free 8-way select.
+__device__ __forceinline__ uint32_t seg_below(const u32x4 (&seg)[kHdrSegs], uint32_t off) {
+    const uint32_t si = off >> 4;
+    u32x4 x = seg[0];
+#pragma unroll
+    for (int i = 1; i < kHdrSegs; ++i) {
+        const uint32_t m = si == (uint32_t)i ? ~0u : 0u;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) x[d] = (x[d] & ~m) | (seg[i][d] & m);
+    }
+    return halves_below(x, off & 15u);
+}
+
 // What the header pass decides for one frame (lane j <-> frame j of the chunk).
 struct FrameLane {
     uint64_t l4s;       // first byte the L4 checksum covers (its parity orients the sum)
@@ -334,9 +357,36 @@ __device__ __forceinline__ FrameOut process_chunk(const CsrDesc &desc, uint64_t 
             // frames without an L4 sum (and lanes past the batch) put both at X1
             const bool use = lane < cnt && fl.l4;
             const uint64_t bs[2] = {use ? fl.l4s : X1, use ? fl.l4e : X1};
+            // The stream gives H at the start of each boundary's segment; the bytes of that
+            // segment below the boundary come from header registers, once per chunk:
+            //  - l4s lies in the frame's own header blocks (l4s - A0 <= 89 < hb_end);
+            //  - l4e is usually the frame's end = the next frame's start, whose segment is
+            //    the next lane's header block 0; or it lies in the own header blocks (a short
+            //    frame with padding); or it is X1 (H(X1) is exact); else (bytes after the IPv4
+            //    total length in a long frame) that one segment is loaded here.
+            const uint64_t A0 = S & ~(uint64_t)15;
+            u32x4 nb;
+#pragma unroll
+            for (int d = 0; d < 4; ++d) nb[d] = from_next_lane(seg[0][d], 0u, lane);
+            const uint32_t p0 = use ? seg_below(seg, (uint32_t)(fl.l4s - A0)) : 0u;
+            uint32_t p1 = 0;
+            const bool e_mid = use && fl.l4e != X1;
+            const uint32_t e_off = (uint32_t)(fl.l4e - A0);
+            if (e_mid) {
+                if (fl.l4e == E)
+                    p1 = halves_below(nb, (uint32_t)E & 15u);
+                else if (e_off < hb_end)
+                    p1 = seg_below(seg, e_off);
+            }
+            const bool far = e_mid && fl.l4e != E && e_off >= hb_end;
+            if (__builtin_amdgcn_ballot_w64(far)) {
+                const u32x4 fs = load_segment<false>(
+                    hrsrc, far ? (uint32_t)((fl.l4e & ~(uint64_t)15) - base) : 0xFFFFFFF0u, 0u);
+                if (far) p1 = halves_below(fs, (uint32_t)fl.l4e & 15u);
+            }
             uint32_t h[2], hx;
-            run.prefixes(bs, h, hx, voff);
-            r = fold16(h[1] - h[0] - fl.fhalf);  // exact halves-sum, < 2^32
+            run.template prefixes<2, true>(bs, h, hx, voff);
+            r = fold16((h[1] + p1) - (h[0] + p0) - fl.fhalf);  // exact halves-sum, < 2^32
             streamed = true;
         }
     }
@@ -372,8 +422,11 @@ __device__ __forceinline__ FrameOut process_chunk(const CsrDesc &desc, uint64_t 
 // The classic kernel: a wave walks its chunks and stores each chunk's results right after
 // it. SPLIT (Tx only): lane j writes frame j's record (w0 | w1 << 32) to a workspace
 // instead, and tx_scatter_kernel stores the fields after the whole read pass.
+#ifndef AIPSTACK_FRAME_WAVES_PER_SIMD  // occupancy the register budget is fitted to
+#define AIPSTACK_FRAME_WAVES_PER_SIMD 4
+#endif
 template <bool TX, int U, int P, bool NT, int SU, bool SPLIT>
-__global__ __launch_bounds__(kBlock, 4) void frame_kernel(CsrDesc desc, uint64_t n,
+__global__ __launch_bounds__(kBlock, AIPSTACK_FRAME_WAVES_PER_SIMD) void frame_kernel(CsrDesc desc, uint64_t n,
                                                        uint32_t chunks_per_wave,
                                                        uint8_t *__restrict__ status,
                                                        uint64_t *__restrict__ records) {

@@ -40,9 +40,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--reps", type=int, default=5, help="launches per variant per round")
     ap.add_argument("--variants", default=None,
-                    help='"U,P,NT,WPC[,SU];..." or, for RX/TX, "F,WPC[,SU[,DEFERRED]];..." (0 = '
-                         'automatic; SU = stream-mode windows 2/4/8, -1 = stream mode off; '
-                         'DEFERRED 1 = stores after a grid barrier, 0 = per chunk)')
+                    help='"U,P,NT,WPC[,SU];..." or, for RX/TX, "F,WPC[,SU];..." (0 = automatic; '
+                         'SU = stream-mode windows 2/4/8, -1 = stream mode off)')
     ap.add_argument("--tx-inplace", action="store_true",
                     help="TX: the one-pass in-place fill (default: split)")
     ap.add_argument("--lib", default=None,
@@ -125,8 +124,7 @@ def main():
         if layout in ("rx", "tx"):
             f = [int(x) for x in v.split(",")]
             variants.append({"frames": f[0], "waves_per_cu": f[1],
-                             "stream": f[2] if len(f) > 2 else 0,
-                             "deferred": f[3] if len(f) > 3 else 1})
+                             "stream": f[2] if len(f) > 2 else 0})
             continue
         f = [int(x) for x in v.split(",")]
         u, p, nt, wpc = f[:4]
