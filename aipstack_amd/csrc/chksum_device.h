@@ -587,6 +587,11 @@ __device__ __forceinline__ bool stream_ok(uint64_t S, uint64_t E, int lane, int 
 // them with other work (the frame kernels' header parse); prefixes() then gives
 // h[k] = H(b[k]) for every b[k] in [A, X1], and hx = H(X1). Windows past the run read
 // zeros (range check) and change nothing.
+struct NoStreamHook {
+    __device__ __forceinline__ void group(uint32_t) {}
+    __device__ __forceinline__ void window(const u32x4 &, uint32_t) {}
+};
+
 template <int U, bool NT, int PRE = U>
 struct StreamRun {
     uint64_t A, X1;
@@ -622,9 +627,11 @@ struct StreamRun {
     // start of b[k]'s 16-byte segment instead (one ds_bpermute per boundary and window, no
     // partial segment; the caller adds the bytes of that segment below b[k] from data it
     // holds itself), except h[k] = hx for b[k] == X1.
-    template <int NB, bool ALIGNED = false>
+    // hook.group(w) runs before the windows [w, w + U) are consumed, hook.window(v, w) once
+    // per window with its data (the frame kernels copy header segments out of the stream).
+    template <int NB, bool ALIGNED = false, class Hook = NoStreamHook>
     __device__ __forceinline__ void prefixes(const uint64_t (&b)[NB], uint32_t (&h)[NB],
-                                             uint32_t &hx, uint32_t voff) {
+                                             uint32_t &hx, uint32_t voff, Hook &&hook = Hook()) {
         // each boundary: its window, owner lane (x4 for ds_bpermute), dword masks below it
         uint32_t bwin[NB];
         int bsrc[NB];
@@ -651,6 +658,7 @@ struct StreamRun {
         uint32_t carry = 0;  // H(start of the current window), mod 2^32
         uint32_t x_hi = 0;   // halves of the last segment's bytes at or above X1
         for (uint32_t w = 0; w < nwin;) {
+            hook.group(w);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const uint32_t wu = w + (uint32_t)u;
@@ -680,6 +688,7 @@ struct StreamRun {
                     x_hi = (uint32_t)__builtin_amdgcn_readlane((int)hh, xlane);
                 }
                 carry += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+                hook.window(v[u], wu);
             }
             w += U;
             if (w < nwin) issue<0, U>(w, voff);

@@ -290,6 +290,73 @@ __device__ __forceinline__ FrameLane parse_lane(const u32x4 (&seg)[kHdrSegs], ui
     return r;
 }
 
+// Halves-sum of a whole 16-byte segment.
+__device__ __forceinline__ uint32_t seg_halves(const u32x4 &x) {
+    return halves(x[0], halves(x[1], halves(x[2], halves(x[3], 0u))));
+}
+
+// Halves-sum of the bytes [A0, A0 + off) of a lane's header blocks (off < 16 * kHdrSegs):
+// the whole segments below off's segment (per-segment sums hs) plus that segment's bytes.
+__device__ __forceinline__ uint32_t hdr_below(const u32x4 (&seg)[kHdrSegs],
+                                              const uint32_t (&hs)[kHdrSegs], uint32_t off) {
+    const uint32_t si = off >> 4;
+    uint32_t acc = seg_below(seg, off);
+#pragma unroll
+    for (int i = 0; i < kHdrSegs - 1; ++i) acc += (uint32_t)i < si ? hs[i] : 0u;
+    return acc;
+}
+
+// Gathered frame stream (stream mode, round 2): the chunk's header segments -- the union
+// over its frames of [A0_j, A0_j + hb_end_j), within the run -- are copied out of the stream
+// windows into a compact LDS array as they pass (a segment's slot = the union segments
+// before it), instead of being loaded per lane before the stream: a header line loaded up
+// front has left L2 by the time the stream reaches it, so it was fetched twice (RX 1.11x).
+// Which lanes of window w hold header segments is bit (w & 31) of word (w >> 5) of an LDS
+// bit table per lane slot, so runs of at most kGatherWindows windows take this path.
+constexpr uint32_t kGatherWindows = 128;
+#ifndef AIPSTACK_FRAME_GATHER_TX  // Tx keeps per-lane header loads
+#define AIPSTACK_FRAME_GATHER_TX 0
+#endif
+constexpr uint32_t kHdrSlots = kWave * kHdrSegs;  // at most 8 segments per frame
+
+struct FrameLds {
+    u32x4 bits[kWave];            // per lane slot: 128 window bits
+    u32x4 slots[kHdrSlots];    // the compact header segments
+};
+
+struct HeaderCapture {
+    const uint32_t *bits;  // this lane's 4 words
+    u32x4 *slots;
+    uint32_t word;         // the current group's word
+    uint32_t count;        // header segments before the current window (wave-uniform)
+    __device__ __forceinline__ void group(uint32_t w) { word = bits[(w >> 5) & 3u]; }
+    __device__ __forceinline__ void window(const u32x4 &v, uint32_t w) {
+        const bool hit = (word >> (w & 31u)) & 1u;
+        const uint64_t m = __builtin_amdgcn_ballot_w64(hit);
+        const uint32_t below =
+            __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        if (hit) slots[count + below] = v;
+        count += (uint32_t)__builtin_popcountll(m);
+    }
+};
+
+// H(l4s) - H(A0) from the header blocks: l4s - A0 = (S & 15) + 14 + IHL * 4 lies in
+// [34, 89], i.e. in segment 2..5 (any other offset only feeds lanes whose sum is unused).
+__device__ __forceinline__ uint32_t l4s_below(const u32x4 (&seg)[kHdrSegs], uint32_t off) {
+    const uint32_t si = off >> 4;
+    u32x4 x = seg[2];
+#pragma unroll
+    for (int i = 3; i <= 5; ++i) {
+        const uint32_t m = si == (uint32_t)i ? ~0u : 0u;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) x[d] = (x[d] & ~m) | (seg[i][d] & m);
+    }
+    uint32_t acc = halves_below(x, off & 15u) + seg_halves(seg[0]) + seg_halves(seg[1]);
+#pragma unroll
+    for (int i = 2; i <= 4; ++i) acc += (uint32_t)i < si ? seg_halves(seg[i]) : 0u;
+    return acc;
+}
+
 // Rx verify / Tx fill of one 64-frame chunk (CSR offsets), lane j <-> frame j:
 //   (B) lane j loads frame j's first 112 aligned bytes (one buffer descriptor per chunk)
 //       and parses its headers (parse_lane): the L4 byte range, pseudo-header words and
@@ -311,7 +378,7 @@ __device__ __forceinline__ FrameLane parse_lane(const u32x4 (&seg)[kHdrSegs], ui
 template <bool TX, int U, int P, bool NT, int SU>
 __device__ __forceinline__ FrameOut process_chunk(const CsrDesc &desc, uint64_t p0, uint64_t n,
                                                   int lane, uint32_t voff, uint32_t not_lane0,
-                                                  int &cnt_out) {
+                                                  FrameLds *lds, int &cnt_out) {
     const auto chunk = desc.begin_chunk(p0, n, lane);
     const int cnt = (int)min((uint64_t)kWave, n - p0);
     cnt_out = cnt;
@@ -336,21 +403,116 @@ __device__ __forceinline__ FrameOut process_chunk(const CsrDesc &desc, uint64_t 
     const uint32_t a0_32 = (uint32_t)S & 16u;
     const uint32_t hb_end = ((a0_32 + ((uint32_t)S & 15u) + kHdrNeed + 31u) & ~31u) - a0_32;
     u32x4 seg[kHdrSegs];
+    auto load_headers = [&]() {
 #pragma unroll
-    for (int i = 0; i < kHdrSegs; ++i)  // past hb_end: out of range, reads 0, no traffic
-        seg[i] = load_segment<false>(hrsrc, 16u * i < hb_end ? hoff + 16u * i : 0xFFFFFFF0u, 0u);
+        for (int i = 0; i < kHdrSegs; ++i)  // past hb_end: out of range, reads 0, no traffic
+            seg[i] = load_segment<false>(hrsrc, 16u * i < hb_end ? hoff + 16u * i : 0xFFFFFFF0u,
+                                         0u);
+    };
     FrameLane fl;
     uint32_t r;
-    bool streamed = false;
+    bool streamed = false, have_headers = false;
     if constexpr (SU > 0) {
-        if (stream_ok(S, E, lane, cnt)) {
-            // (C') stream prefixes at each frame's L4 start and end. The first windows'
-            // loads go out now, behind the header loads, and arrive during the parse.
-            const int lastl = cnt - 1;
-            const uint64_t X1 =
-                ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(E >> 32), lastl)
-                 << 32) |
-                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)E, lastl);
+      if (stream_ok(S, E, lane, cnt)) {
+        const int lastl = cnt - 1;
+        const uint64_t X1 =
+            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(E >> 32), lastl)
+             << 32) |
+            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)E, lastl);
+        const uint32_t nseg = ((uint32_t)(X1 - base) + 15u) >> 4;
+        if ((!TX || AIPSTACK_FRAME_GATHER_TX) && ((nseg + 63u) >> 6) <= kGatherWindows) {
+            // (B'+C') one pass: the stream gives H at every frame's aligned start A0_j and
+            // hands the header segments to LDS; the parse runs on them after the stream.
+            const uint64_t A0 = S & ~(uint64_t)15;
+            const bool act = lane < cnt;
+            const uint32_t r0 = act ? (uint32_t)((A0 - base) >> 4) : nseg;
+            const uint32_t r1 = min(r0 + (hb_end >> 4), nseg);
+            // the bit table: 8 atomic ORs per lane (its header segments)
+            {
+                uint32_t z;  // made here (a zero quad kept live across the loop was spilled)
+                asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+                lds->bits[lane] = u32x4{z, z, z, z};
+            }
+            __builtin_amdgcn_wave_barrier();
+            {
+                uint32_t *words = reinterpret_cast<uint32_t *>(lds->bits);
+#pragma unroll
+                for (int i = 0; i < kHdrSegs; ++i) {
+                    const uint32_t g = r0 + (uint32_t)i;
+                    if (g < r1)
+                        __hip_atomic_fetch_or(&words[4u * (g & 63u) + (g >> 11)],
+                                              1u << ((g >> 6) & 31u), __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_WAVEFRONT);
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            StreamRun<SU, NT> run;
+            run.begin(base, X1, voff);
+            // compact slot of r0: the union segments below it. Regions start and end in
+            // lane order, so region j adds [max(r0_j, r1_{j-1}), r1_j) to the union.
+            const uint32_t r1p = (uint32_t)__builtin_amdgcn_ds_bpermute(
+                ((lane + 63) & 63) << 2, (int)(lane == 63 ? 0u : r1));
+            const uint32_t uj = max(r0, r1p);
+            const uint32_t nw = r1 > uj ? r1 - uj : 0u;
+            const uint32_t cslot = (wave_incl_scan(nw) - nw) - (uj - r0);
+            const uint32_t nmine = r1 - r0;
+            HeaderCapture cap;
+            cap.bits = reinterpret_cast<const uint32_t *>(&lds->bits[lane]);
+            cap.slots = lds->slots;
+            cap.word = 0;
+            cap.count = 0;
+            const uint64_t bs[1] = {act ? A0 : X1};
+            uint32_t hA[1], hx;
+            run.template prefixes<1, true>(bs, hA, hx, voff, cap);
+            __builtin_amdgcn_wave_barrier();
+            // this lane's header blocks, and the next frame's first block (its start)
+#pragma unroll
+            for (int i = 0; i < kHdrSegs; ++i) {
+                const u32x4 x = lds->slots[min(cslot + (uint32_t)i, kHdrSlots - 1u)];
+                seg[i] = (uint32_t)i < nmine ? x : u32x4{0u, 0u, 0u, 0u};
+            }
+            const uint32_t cs_n = from_next_lane(cslot, 0u, lane);
+            const uint32_t nm_n = from_next_lane(nmine, 0u, lane);
+            const uint32_t hA_n = from_next_lane(hA[0], 0u, lane);
+            // H(E) - H(A0 of the next frame): its first block's bytes below E
+            const uint32_t pn =
+                nm_n ? halves_below(lds->slots[min(cs_n, kHdrSlots - 1u)], (uint32_t)E & 15u) : 0u;
+            fl = parse_lane<TX, true>(seg, S, len, hb_end);
+            const bool use = act && fl.l4;
+            // H(l4s): l4s lies in the own header blocks (l4s - A0 <= 89 < hb_end)
+            const uint32_t h_s = hA[0] + l4s_below(seg, (uint32_t)(fl.l4s - A0));
+            // H(l4e): X1 (exact), or the next frame's start (its A0 plus the bytes below it
+            // in its first block), or inside the own header blocks (a short frame with
+            // padding); else (bytes after the IPv4 total length in a long frame) the chunk
+            // takes the per-frame path below.
+            const uint32_t e_off = (uint32_t)(fl.l4e - A0);
+            uint32_t h_e = hx;
+            bool far = false;
+            const bool pad = use && fl.l4e != X1 && fl.l4e != E;
+            if (use && fl.l4e != X1 && fl.l4e == E) h_e = hA_n + pn;
+            if (__builtin_amdgcn_ballot_w64(pad)) {  // short frames with padding
+                uint32_t hs[kHdrSegs];
+#pragma unroll
+                for (int i = 0; i < kHdrSegs; ++i) hs[i] = seg_halves(seg[i]);
+                if (pad) {
+                    if (e_off < hb_end)
+                        h_e = hA[0] + hdr_below(seg, hs, e_off);
+                    else
+                        far = true;
+                }
+            }
+            if (!__builtin_amdgcn_ballot_w64(far)) {
+                r = fold16(h_e - h_s - fl.fhalf);  // exact halves-sum, < 2^32
+                streamed = true;
+            }
+            have_headers = true;  // the parse's inputs are the loaded header blocks
+        } else {
+            // (C') long runs: header blocks loaded per lane, stream prefixes at each frame's
+            // L4 start and end. The first windows' loads go out behind the header loads
+            // and arrive during the parse.
+            load_headers();
+            have_headers = true;
             StreamRun<SU, NT, AIPSTACK_FRAME_PREFETCH(SU)> run;
             run.begin(base, X1, voff);
             fl = parse_lane<TX, true>(seg, S, len, hb_end);
@@ -389,8 +551,10 @@ __device__ __forceinline__ FrameOut process_chunk(const CsrDesc &desc, uint64_t 
             r = fold16((h[1] + p1) - (h[0] + p0) - fl.fhalf);  // exact halves-sum, < 2^32
             streamed = true;
         }
+      }
     }
     if (!streamed) {
+        if (!have_headers) load_headers();
         fl = parse_lane<TX, false>(seg, S, len, hb_end);
         const bool need = fl.ce != fl.cs;
         const LaneMeta meta = lane_meta(fl.cs, fl.ce);
@@ -438,10 +602,14 @@ __global__ __launch_bounds__(kBlock, AIPSTACK_FRAME_WAVES_PER_SIMD) void frame_k
     const uint64_t c_end = min(c + chunks_per_wave, nchunks);
     const uint32_t voff = (uint32_t)lane * 16u;
     const uint32_t not_lane0 = lane == 0 ? 0u : ~0u;
+    constexpr bool kGather = SU > 0 && (!TX || AIPSTACK_FRAME_GATHER_TX);
+    __shared__ FrameLds lds[kGather ? kWavesPerBlock : 1];  // 9 KiB per wave (gathered stream)
+    FrameLds *my = &lds[kGather ? wave_in_block : 0];
     for (; c < c_end; ++c) {
         const uint64_t p0 = c * kWave;
         int cnt;
-        const FrameOut o = process_chunk<TX, U, P, NT, SU>(desc, p0, n, lane, voff, not_lane0, cnt);
+        const FrameOut o =
+            process_chunk<TX, U, P, NT, SU>(desc, p0, n, lane, voff, not_lane0, my, cnt);
         if (lane < cnt) {
             if constexpr (SPLIT)
                 records[p0 + lane] = (uint64_t)o.w0 | (uint64_t)o.w1 << 32;

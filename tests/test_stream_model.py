@@ -250,3 +250,108 @@ def test_gathered_model_matches_oracle(oracle, case, U):
         if (a[j] & 1) == 0:
             r = ((r & 0xFF) << 8) | (r >> 8)
         assert r == oracle.inverted(buf, a[j], l[j]), (case, j, a[j], l[j])
+
+
+# ---- frame stream with headers captured from the stream (frame_kernels.hip) -------------
+
+def captured_frame_model(buf, S, E, l4s, l4e):
+    """process_chunk's gathered stream for one back-to-back chunk: the union of the frames'
+    header blocks [A0_j, (S_j + 128) & ~31) within the run goes to a compact array in
+    window order (slot = union segments below), each lane reads its blocks back from its
+    compact slot, and the L4 halves-sum is H(l4e) - H(l4s) from H at every A0_j. Returns
+    (sums, blocks_ok); a frame whose L4 end lies past its blocks and before its end
+    ('far') gets None."""
+    cnt = len(S)
+    A = S[0] & ~15
+    X1 = E[-1]
+    nseg = (X1 - A + 15) >> 4
+    raw = np.zeros(nseg * 16, dtype=np.uint8)
+    raw[:X1 - A] = buf[A:X1]
+    full = raw.view("<u2").astype(np.uint64).reshape(nseg, 8).sum(axis=1)
+    H = np.concatenate([[0], np.cumsum(full)])
+    hx = int(H[nseg]) - (int(full[nseg - 1]) - _below(raw[(nseg - 1) * 16:nseg * 16],
+                                                       (X1 - A) & 15 or 16))
+    r0 = [((s & ~15) - A) >> 4 for s in S]
+    r1 = [min(r0[j] + ((((s + 128) & ~31) - (s & ~15)) >> 4), nseg) for j, s in enumerate(S)]
+    bit = np.zeros(nseg, dtype=bool)
+    for j in range(cnt):
+        bit[r0[j]:r1[j]] = True
+    slots = [raw[g * 16:g * 16 + 16] for g in range(nseg) if bit[g]]   # window order
+    cslot, prev = [], 0
+    count = 0
+    for j in range(cnt):
+        u = max(r0[j], prev)
+        nw = max(0, r1[j] - u)
+        cslot.append(count - (u - r0[j]))
+        count += nw
+        prev = r1[j]
+    assert count == len(slots)
+    blocks_ok = True
+    segs = []
+    for j in range(cnt):
+        mine = [slots[cslot[j] + i] if i < r1[j] - r0[j] else np.zeros(16, np.uint8)
+                for i in range(8)]
+        want = [raw[(r0[j] + i) * 16:(r0[j] + i + 1) * 16] if r0[j] + i < r1[j]
+                else np.zeros(16, np.uint8) for i in range(8)]
+        blocks_ok &= all(np.array_equal(a, b) for a, b in zip(mine, want))
+        segs.append(np.concatenate(mine))
+    hA = [int(H[r0[j]]) for j in range(cnt)]
+    sums = []
+    for j in range(cnt):
+        A0 = S[j] & ~15
+        blk = segs[j]
+        below = lambda off: int(np.concatenate([blk[:off], np.zeros(off & 1, np.uint8)])
+                                .view("<u2").astype(np.uint64).sum())
+        h_s = hA[j] + below(l4s[j] - A0)
+        if l4e[j] == X1:
+            h_e = hx
+        elif l4e[j] == E[j]:
+            nb = segs[j + 1][:16]
+            h_e = hA[j + 1] + _below(nb, E[j] & 15)
+        elif l4e[j] - A0 < ((S[j] + 128) & ~31) - A0:     # e_off < hb_end
+            h_e = hA[j] + below(l4e[j] - A0)
+        else:
+            sums.append(None)
+            continue
+        sums.append((h_e - h_s) & M32)
+    return sums, blocks_ok
+
+
+@pytest.mark.parametrize("case", ["mixed", "short", "padded", "mtu", "aligned_end", "tiny"])
+def test_captured_frame_model_exact(case):
+    rng = np.random.default_rng(hash(("capture", case)) % 2**32)
+    for trial in range(40):
+        cnt = int(rng.integers(1, 65))
+        lo, hi = {"mixed": (34, 1515), "short": (34, 100), "padded": (60, 300),
+                  "mtu": (1514, 1515), "aligned_end": (34, 200), "tiny": (0, 40)}[case]
+        lens = rng.integers(lo, hi, cnt)
+        base = 4096 + int(rng.integers(0, 64))
+        S = [base + int(x) for x in np.concatenate([[0], np.cumsum(lens)[:-1]])]
+        E = [s + int(n) for s, n in zip(S, lens)]
+        if case == "aligned_end":
+            shift = (16 - E[-1] % 16) % 16
+            S = [s + shift for s in S]
+            E = [e + shift for e in E]
+        buf = rng.integers(0, 256, size=E[-1] + 4096, dtype=np.uint8)
+        buf[S[0]:S[0] + 300] = 0xFF
+        l4s, l4e = [], []
+        for s, e in zip(S, E):
+            hl = 4 * int(rng.integers(5, 16))
+            start = min(s + 14 + hl, e)
+            room = e - start
+            ln = int(rng.integers(0, room + 1)) if case == "padded" and room else room
+            l4s.append(start)
+            l4e.append(start + ln)
+        sums, ok = captured_frame_model(buf, S, E, l4s, l4e)
+        assert ok, (case, trial)
+        for j in range(cnt):
+            if sums[j] is not None:
+                assert sums[j] == _exact_halves(buf, l4s[j], l4e[j]) & M32, (case, trial, j)
+
+
+def _exact_halves(buf, s, e):
+    """Exact sum of little-endian 16-bit halves at even absolute addresses over [s, e)."""
+    lo, hi = s & ~1, (e + 1) & ~1
+    raw = np.zeros(hi - lo, dtype=np.uint8)
+    raw[s - lo:e - lo] = buf[s:e]
+    return int(raw.view("<u2").astype(np.uint64).sum())
