@@ -314,6 +314,9 @@ __device__ __forceinline__ uint32_t hdr_below(const u32x4 (&seg)[kHdrSegs],
 // Which lanes of window w hold header segments is bit (w & 31) of word (w >> 5) of an LDS
 // bit table per lane slot, so runs of at most kGatherWindows windows take this path.
 constexpr uint32_t kGatherWindows = 128;
+#ifndef AIPSTACK_FRAME_NT  // experiments: 0 = the frame stream loads with the default policy
+#define AIPSTACK_FRAME_NT 1
+#endif
 #ifndef AIPSTACK_FRAME_GATHER_TX  // Tx keeps per-lane header loads
 #define AIPSTACK_FRAME_GATHER_TX 0
 #endif
@@ -612,7 +615,11 @@ __global__ __launch_bounds__(kBlock, AIPSTACK_FRAME_WAVES_PER_SIMD) void frame_k
             process_chunk<TX, U, P, NT, SU>(desc, p0, n, lane, voff, not_lane0, my, cnt);
         if (lane < cnt) {
             if constexpr (SPLIT)
+#if AIPSTACK_EXP_NO_RECORDS  // experiment: price of the record stores (wrong output)
+                asm volatile("" ::"v"(o.w0), "v"(o.w1));
+#else
                 records[p0 + lane] = (uint64_t)o.w0 | (uint64_t)o.w1 << 32;
+#endif
             else
                 store_frame<TX>(o.S, o.w0, o.w1, status, p0 + lane);
         }
@@ -635,7 +642,7 @@ int launch_frames(const void *d_base, const uint64_t *d_offsets, uint64_t n, uin
     const uint64_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
     if (blocks > 0x7FFFFFFFull || cpw > 0xFFFFFFFFull) return AIPSTACK_CHKSUM_EINVAL;
 #define AIPSTACK_LAUNCH_FRAMES(P, SU)                                                          \
-    hipLaunchKernelGGL((frame_kernel<TX, 2, P, true, SU, SPLIT>), dim3((unsigned)blocks),        \
+    hipLaunchKernelGGL((frame_kernel<TX, 2, P, AIPSTACK_FRAME_NT != 0, SU, SPLIT>), dim3((unsigned)blocks),        \
                        dim3(kBlock), 0, stream, desc, n, (uint32_t)cpw, d_status, d_records)
 #define AIPSTACK_LAUNCH_FRAMES_SU(P)              \
     switch (su) {                                 \
