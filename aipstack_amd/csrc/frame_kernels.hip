@@ -323,25 +323,54 @@ constexpr uint32_t kGatherWindows = 128;
 constexpr uint32_t kHdrSlots = kWave * kHdrSegs;  // at most 8 segments per frame
 
 struct FrameLds {
-    u32x4 bits[kWave];            // per lane slot: 128 window bits
-    u32x4 slots[kHdrSlots];    // the compact header segments
+    uint64_t wmask[kGatherWindows + 8];  // per window: the lanes holding header segments
+                                         // (+8: whole groups past the last window read 0)
+    u32x4 slots[kHdrSlots];          // the compact header segments
 };
 
+// Capture hook: group(w) fetches the group's U window masks into SGPRs (broadcast LDS
+// reads); window(v, w) writes the lanes of the mask to consecutive compact slots.
+template <int U>
 struct HeaderCapture {
-    const uint32_t *bits;  // this lane's 4 words
+    const uint64_t *wmask;
     u32x4 *slots;
-    uint32_t word;         // the current group's word
-    uint32_t count;        // header segments before the current window (wave-uniform)
-    __device__ __forceinline__ void group(uint32_t w) { word = bits[(w >> 5) & 3u]; }
+    uint32_t count;  // header segments before the current window (wave-uniform)
+    uint64_t mk[U];
+    __device__ __forceinline__ void group(uint32_t w) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t wu = w + (uint32_t)u;
+            const uint64_t x = wmask[wu];  // wu < kGatherWindows + U: zeroed
+            mk[u] = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32) |
+                    (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)x);
+        }
+    }
+    // The store runs under exec = the window's mask, set and restored inside one asm
+    // statement (the compiler would test each lane's bit with VALU instead).
     __device__ __forceinline__ void window(const u32x4 &v, uint32_t w) {
-        const bool hit = (word >> (w & 31u)) & 1u;
-        const uint64_t m = __builtin_amdgcn_ballot_w64(hit);
+        static_assert(U <= 8, "wmask holds 8 zero words past the last window");
+        const uint64_t m = mk[w & (uint32_t)(U - 1)];
         const uint32_t below =
             __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        if (hit) slots[count + below] = v;
+        typedef __attribute__((address_space(3))) u32x4 lds_seg;
+        const uint32_t addr = (uint32_t)(uintptr_t)(lds_seg *)(slots + count) + 16u * below;
+        uint64_t save;
+        asm volatile(
+            "s_and_saveexec_b64 %0, %2\n\t"
+            "ds_write_b128 %1, %3\n\t"
+            "s_mov_b64 exec, %0"
+            : "=&s"(save)
+            : "v"(addr), "s"(m), "v"(v)
+            : "memory");
         count += (uint32_t)__builtin_popcountll(m);
     }
 };
+
+// Bits [lo, hi) of a 64-bit word (lo < 64, lo <= hi).
+__device__ __forceinline__ uint64_t bit_range(uint32_t lo, uint32_t hi) {
+    const uint64_t top = hi >= 64u ? ~0ull : ((1ull << hi) - 1ull);
+    return top & ~((1ull << lo) - 1ull);
+}
 
 // H(l4s) - H(A0) from the header blocks: l4s - A0 = (S & 15) + 14 + IHL * 4 lies in
 // [34, 89], i.e. in segment 2..5 (any other offset only feeds lanes whose sum is unused).
@@ -430,23 +459,21 @@ __device__ __forceinline__ FrameOut process_chunk(const CsrDesc &desc, uint64_t 
             const bool act = lane < cnt;
             const uint32_t r0 = act ? (uint32_t)((A0 - base) >> 4) : nseg;
             const uint32_t r1 = min(r0 + (hb_end >> 4), nseg);
-            // the bit table: 8 atomic ORs per lane (its header segments)
+            // the window masks: each lane ORs its header segments in (at most two windows)
             {
                 uint32_t z;  // made here (a zero quad kept live across the loop was spilled)
                 asm volatile("v_mov_b32 %0, 0" : "=v"(z));
-                lds->bits[lane] = u32x4{z, z, z, z};
+                reinterpret_cast<u32x4 *>(lds->wmask)[lane] = u32x4{z, z, z, z};
+                if (lane < 4) reinterpret_cast<u32x4 *>(lds->wmask)[kWave + lane] = u32x4{z, z, z, z};
             }
             __builtin_amdgcn_wave_barrier();
-            {
-                uint32_t *words = reinterpret_cast<uint32_t *>(lds->bits);
-#pragma unroll
-                for (int i = 0; i < kHdrSegs; ++i) {
-                    const uint32_t g = r0 + (uint32_t)i;
-                    if (g < r1)
-                        __hip_atomic_fetch_or(&words[4u * (g & 63u) + (g >> 11)],
-                                              1u << ((g >> 6) & 31u), __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_WAVEFRONT);
-                }
+            if (r1 > r0) {
+                const uint32_t w0 = r0 >> 6, e0 = r1 - (w0 << 6);
+                __hip_atomic_fetch_or(&lds->wmask[w0], bit_range(r0 & 63u, min(e0, 64u)),
+                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                if (e0 > 64u)
+                    __hip_atomic_fetch_or(&lds->wmask[w0 + 1u], bit_range(0u, e0 - 64u),
+                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -460,10 +487,9 @@ __device__ __forceinline__ FrameOut process_chunk(const CsrDesc &desc, uint64_t 
             const uint32_t nw = r1 > uj ? r1 - uj : 0u;
             const uint32_t cslot = (wave_incl_scan(nw) - nw) - (uj - r0);
             const uint32_t nmine = r1 - r0;
-            HeaderCapture cap;
-            cap.bits = reinterpret_cast<const uint32_t *>(&lds->bits[lane]);
+            HeaderCapture<SU> cap;
+            cap.wmask = lds->wmask;
             cap.slots = lds->slots;
-            cap.word = 0;
             cap.count = 0;
             const uint64_t bs[1] = {act ? A0 : X1};
             uint32_t hA[1], hx;
