@@ -722,9 +722,10 @@ __device__ __forceinline__ int wave_max_scan(int v) {
 // [64w, 64w + 64), and lane k loads index c = 64w + k from the chunk that owns it, at
 // gbase_owner + 16 c (gbase_j = (a_j & ~15) - 16 cs_j).
 //
-// Owners: per group of U windows each chunk marks, in LDS, the lane where it starts (one
-// write per lane; lanes that start nothing write a trash slot), then a max-scan per window.
-// The owner also tells the loading lane whether its segment is the chunk's first (bytes
+// Owners: the non-empty chunks' load parameters sit in LDS by rank; per group of U windows
+// each chunk starting there ORs its start lane into its window's 64-bit mask, and lane k of
+// window w takes rank base_w - 1 + popcount(mask bits <= k) (two mbcnt; round 2 -- a mark
+// table and a DPP max-scan per window before). The owner also tells the loading lane whether its segment is the chunk's first (bytes
 // below a_j & 15 are not the chunk's) or last (bytes from the chunk's end on are not), and
 // the lane masks those bytes off before it sums the segment ("cleaned" segments, mask table
 // in LDS). The cleaned segments of chunk j then hold exactly its bytes, so with
@@ -741,7 +742,12 @@ __device__ __forceinline__ int wave_max_scan(int v) {
 // unconditionally (a window past the stream sums zeros and holds no boundary), so the loads
 // stay straight-line and every wait is counted (vmcnt(N)), also across the back edge.
 // ---------------------------------------------------------------------------------
-constexpr int kGatherSlots = kWave + 1;  // per window: 64 lanes + a trash slot
+// Per-wave LDS scratch of the gathered stream: the owners' load parameters by rank (rank =
+// non-empty chunks before it), and the chunk-start masks of the current group's windows.
+struct GatherLds {
+    u32x4 owner[kWave];   // {gbase lo, gbase hi, first_info, last_info}
+    uint64_t starts[8];   // per window of the group: bit k = a chunk starts at lane k
+};
 
 // LDS table of byte masks: entry head * 16 + (tail - 1) keeps bytes [head, tail) of a
 // 16-byte segment (head 0..15, tail 1..16). Filled once per block by fill_keep_table().
@@ -757,56 +763,49 @@ __device__ __forceinline__ void fill_keep_table(KeepTable &t) {
 
 template <int U, bool NT>
 struct ChunkLoader {
+    static_assert(U <= 8, "GatherLds holds 8 window masks");
     uint32_t T;
-    uint32_t gb_lo, gb_hi;  // this lane's chunk: segment c (compact) is at gbase + 16 c
-    uint32_t first_info;    // cs_j | (a_j & 15) << 24: first segment, head bytes to drop
-    uint32_t last_info;     // (cs_j + ns_j - 1) | tail << 24: last segment, bytes kept
-    uint32_t mark_slot;     // the lane its chunk starts at, within its window
     uint32_t start_win;     // the window its chunk starts in (~0: empty chunk)
-    int cur;                // owner of the previous window's last lane (wave-uniform)
+    uint32_t start_bit;     // the lane its chunk starts at, within that window
+    uint32_t base;          // non-empty chunks starting before the next group (uniform)
     int lane;
-    uint32_t (*mark)[kGatherSlots];
+    GatherLds *g;
 
-    // Windows [w, w + U): loads into v, and each lane's keep-table index into keep.
+    // Windows [w, w + U): loads into v, and each lane's keep-table index into keep. The
+    // owner of compact index 64w + k is the last chunk starting at or before it: its rank
+    // is base_w - 1 + (starts at lanes <= k of window w) = base_w + bit0 - 1 + mbcnt(m >> 1).
     __device__ __forceinline__ void issue(uint32_t w, u32x4 (&v)[U], uint32_t (&keep)[U]) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) mark[u][lane] = 0u;
+        if (lane < U) g->starts[lane] = 0ull;
         __builtin_amdgcn_wave_barrier();
         const uint32_t du = start_win - w;  // < U: starts in this group
-        uint32_t *slot = du < (uint32_t)U ? &mark[du][mark_slot] : &mark[0][kWave];
-        *slot = (uint32_t)lane + 1u;
+        if (du < (uint32_t)U)
+            __hip_atomic_fetch_or(&g->starts[du], 1ull << start_bit, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_WAVEFRONT);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
-        uint32_t m[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) m[u] = mark[u][lane];
-        __builtin_amdgcn_wave_barrier();
-        // inclusive max-scan (0 = no chunk starts at or before this lane in the window)
-#define AIPSTACK_GMAX(ctrl, rowmask)                                                         \
-    _Pragma("unroll") for (int u = 0; u < U; ++u)                                           \
-        m[u] = max(m[u], (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m[u], ctrl, rowmask, 0xF, \
-                                                               false));
-        AIPSTACK_GMAX(0x111, 0xF)
-        AIPSTACK_GMAX(0x112, 0xF)
-        AIPSTACK_GMAX(0x114, 0xF)
-        AIPSTACK_GMAX(0x118, 0xF)
-        AIPSTACK_GMAX(0x142, 0xA)
-        AIPSTACK_GMAX(0x143, 0xC)
-#undef AIPSTACK_GMAX
+        uint64_t m[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int owner = m[u] ? (int)m[u] - 1 : cur;
-            cur = __builtin_amdgcn_readlane(owner, 63);
+            const uint64_t x = g->starts[u];
+            m[u] = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32) |
+                   (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)x);
+        }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t m1 = m[u] >> 1;
+            const uint32_t rank = base + ((uint32_t)m[u] & 1u) - 1u +
+                                  __builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0u));
+            base += (uint32_t)__builtin_popcountll(m[u]);
+            const u32x4 od = g->owner[rank & (uint32_t)(kWave - 1)];
             const uint32_t c0 = (w + (uint32_t)u) * (uint32_t)kWave + (uint32_t)lane;
             const uint32_t c = min(c0, T - 1u);
-            const int src = owner << 2;
-            const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)gb_lo);
-            const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)gb_hi);
-            const uint32_t fi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)first_info);
-            const uint32_t li = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)last_info);
+            const uint32_t fi = od[2], li = od[3];
             const uint32_t head = c == (fi & 0xFFFFFFu) ? fi >> 24 : 0u;
             const uint32_t tail = c == (li & 0xFFFFFFu) ? li >> 24 : 16u;
             keep[u] = head * 16u + tail - 1u;
-            const uint64_t addr = (((uint64_t)hi << 32) | lo) + 16ull * c;
+            const uint64_t addr = (((uint64_t)od[1] << 32) | od[0]) + 16ull * c;
             typedef __attribute__((address_space(1))) const u32x4 gseg;
             const gseg *p = (const gseg *)(addr);
             if constexpr (NT)
@@ -817,12 +816,12 @@ struct ChunkLoader {
     }
 };
 
-// The chain kernel's 64 chunk sums. `mark`: this wave's LDS scratch (U windows of
-// kGatherSlots); `keep`: the block's mask table (fill_keep_table). Returns lane j's exact
+// The chain kernel's 64 chunk sums. `g`: this wave's LDS scratch; `keep`: the block's mask
+// table (fill_keep_table). Returns lane j's exact
 // halves-sum of its chunk.
 template <int U, bool NT>
 __device__ __forceinline__ uint32_t sum_gathered_chunks(uint64_t a, uint32_t l, int lane,
-                                                        uint32_t (*mark)[kGatherSlots],
+                                                        GatherLds *glds,
                                                         const KeepTable &keep_table) {
     const uint32_t rs = (uint32_t)a & 15u;
     const uint32_t ns = l ? (rs + l + 15u) >> 4 : 0u;
@@ -834,15 +833,19 @@ __device__ __forceinline__ uint32_t sum_gathered_chunks(uint64_t a, uint32_t l, 
     ChunkLoader<U, NT> ld;
     ld.T = T;
     const uint64_t gbase = (a & ~(uint64_t)15) - 16ull * cs;
-    ld.gb_lo = (uint32_t)gbase;
-    ld.gb_hi = (uint32_t)(gbase >> 32);
-    ld.first_info = cs | rs << 24;
-    ld.last_info = (cs + ns - 1u) | ((((rs + l - 1u) & 15u) + 1u) << 24);
+    // the owners' load parameters, by rank among the non-empty chunks
+    const uint64_t ne = __builtin_amdgcn_ballot_w64(ns != 0u);
+    const uint32_t rank =
+        __builtin_amdgcn_mbcnt_hi((uint32_t)(ne >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ne, 0u));
+    if (ns)
+        glds->owner[rank] = u32x4{(uint32_t)gbase, (uint32_t)(gbase >> 32), cs | rs << 24,
+                               (cs + ns - 1u) | ((((rs + l - 1u) & 15u) + 1u) << 24)};
+    __builtin_amdgcn_wave_barrier();
     ld.start_win = ns ? (cs >> 6) : ~0u;
-    ld.mark_slot = cs & 63u;
-    ld.cur = 0;
+    ld.start_bit = cs & 63u;
+    ld.base = 0;
     ld.lane = lane;
-    ld.mark = mark;
+    ld.g = glds;
     // this lane's boundary: G at segment cs (an empty chunk's cs is the next one's)
     const uint32_t bwin = cs >> 6;
     const int bsrc = (int)((cs & 63u) << 2);

@@ -146,7 +146,7 @@ __global__ __launch_bounds__(kBlock, 5) void chksum_chain_kernel(
     uint32_t chunks_per_wave, uint16_t *__restrict__ out, uint32_t flags) {
     __shared__ uint64_t lds_acc[kWavesPerBlock][kWave];  // per-chain sum of chunk sums
     __shared__ int lds_mark[kWavesPerBlock][kWave];      // chain starting at chunk lane
-    __shared__ uint32_t lds_gmark[kWavesPerBlock][SU][kGatherSlots];  // gathered stream owners
+    __shared__ GatherLds lds_gather[kWavesPerBlock];                  // gathered stream owners
     __shared__ KeepTable lds_keep;                                    // its segment masks
     fill_keep_table(lds_keep);
     __syncthreads();
@@ -205,7 +205,7 @@ __global__ __launch_bounds__(kBlock, 5) void chksum_chain_kernel(
             if (before) q ^= carry_par;
             // the 64 chunk sums: one gathered stream over just the chunks' bytes
             const uint32_t sums =
-                sum_gathered_chunks<SU, NT>(a, valid ? l : 0u, lane, lds_gmark[wave_in_block],
+                sum_gathered_chunks<SU, NT>(a, valid ? l : 0u, lane, &lds_gather[wave_in_block],
                                             lds_keep);
             uint32_t r = fold16(sums);
             if ((uint32_t)(a & 1) == q)
