@@ -296,6 +296,109 @@ def cpu_baseline(spec):
     return res, out
 
 
+def cpu_baseline_chain(chain):
+    """Reference IpChksumAccumulator(State).getChksum(IpBufRef chain) (Chksum.h:171-336)
+    over every chain of this rank's CHAIN batch, on a host copy (nodes linked once, outside
+    the timing); 1 thread and every affinity core. Kind "port" (the oracle's chain walk,
+    oracle/chksum_oracle.c) where the reference build is absent."""
+    host = chain["buf"].cpu().numpy()
+    n = chain["n"]
+    out = np.empty(n, dtype=np.uint16)
+    bias = (chain["base"] - host.ctypes.data) % (1 << 64)
+    ref_path = os.path.join(ROOT, "oracle", "_ref", "libref_chksum.so")
+    if os.path.exists(ref_path):
+        kind = "reference"
+        lib = ctypes.CDLL(ref_path)
+        lib.ref_time_batch_chain.restype = ctypes.c_double
+        lib.ref_time_batch_chain.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint64] + \
+            [ctypes.c_void_p] * 4 + [ctypes.c_uint64, ctypes.c_void_p]
+
+        def timed(threads, reps):
+            return lib.ref_time_batch_chain(threads, reps, bias, chain["addr_host"].ctypes.data,
+                                            chain["len_host"].ctypes.data,
+                                            chain["index_host"].ctypes.data,
+                                            chain["states_host"].ctypes.data, n,
+                                            out.ctypes.data)
+    else:
+        kind = "port"
+        lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "libchksum_oracle.so"))
+        lib.oracle_batch_chain.argtypes = [ctypes.c_void_p, ctypes.c_uint64] + \
+            [ctypes.c_void_p] * 4 + [ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32]
+
+        def timed(threads, reps):
+            def one(lo, hi):
+                k0 = int(chain["index_host"][lo])
+                idx = chain["index_host"][lo:hi + 1] - np.uint64(k0)  # kept alive: a local
+                lib.oracle_batch_chain(host.ctypes.data, chain["base"],
+                                       chain["addr_host"][k0:].ctypes.data,
+                                       chain["len_host"][k0:].ctypes.data, idx.ctypes.data,
+                                       chain["states_host"][lo:hi].ctypes.data, hi - lo,
+                                       out[lo:hi].ctypes.data, 1)
+            return _timed_ranges(one, n, threads, reps)
+    return _baseline_result(timed, chain["payload"], n, kind,
+                            f"this rank's whole CHAIN batch ({n} chains of 3 chunks, "
+                            f"{chain['payload']} B) in host memory",
+                            "reference IpChksumAccumulator(State).getChksum(IpBufRef) from "
+                            "Chksum.h compiled -O2 from /root/reference" if kind == "reference"
+                            else "oracle/chksum_oracle.c chain walk")
+
+
+def cpu_baseline_frames(spec, frames_host):
+    """Rx verify / Tx fill on the host: the frame oracle (oracle/frame_oracle.c, a C
+    restatement of the reference's receive checks and send-side fills whose arithmetic is
+    the reference's IpChksum) over this rank's whole frame batch -- kind "port": the
+    reference runs these checks inside its stack, one frame per call, with no entry point
+    of its own to time. 1 thread and every affinity core (disjoint frame ranges; ctypes
+    releases the GIL)."""
+    n, off = spec["n"], spec["offsets"].astype(np.uint64)
+    buf = frames_host.copy()
+    status = np.empty(n, dtype=np.uint8)
+    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "libchksum_oracle.so"))
+    fn = lib.oracle_rx_verify_batch if spec["layout"] == "rx" else lib.oracle_tx_fill_batch
+    fn.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_uint64, ctypes.c_void_p]
+
+    def timed(threads, reps):
+        def one(lo, hi):  # offsets are absolute: pass the slice of n - lo + 1 entries
+            fn(buf.ctypes.data, off[lo:].ctypes.data, hi - lo, status[lo:].ctypes.data)
+        return _timed_ranges(one, n, threads, reps)
+    what = "Rx verify" if spec["layout"] == "rx" else "Tx fill (in place, idempotent)"
+    return _baseline_result(timed, spec["total"], n, "port",
+                            f"{what} of this rank's whole frame batch ({n} frames, "
+                            f"{spec['total']} B) in host memory",
+                            "oracle/frame_oracle.c, compiled -O2")
+
+
+def _timed_ranges(one, n, threads, reps):
+    """Median of `reps` passes (after 1 warm-up) of one(lo, hi) over `threads` disjoint
+    ranges run concurrently (Python threads; the ctypes calls run without the GIL)."""
+    from concurrent.futures import ThreadPoolExecutor
+    bounds = [(n * t // threads, n * (t + 1) // threads) for t in range(threads)]
+    ts = []
+    with ThreadPoolExecutor(max_workers=threads) as ex:
+        for _ in range(reps + 1):
+            t0 = time.perf_counter()
+            list(ex.map(lambda b: one(*b), bounds))
+            ts.append(time.perf_counter() - t0)
+    return float(np.median(ts[1:]))
+
+
+def _baseline_result(timed, total, n, kind, sample, impl):
+    reps = max(3, min(CPU_REPS, 5))
+    t1 = timed(1, reps)
+    cores_all = _affinity_cores()
+    res = {"value": round(total / t1 / 2**30, 3), "unit": "GiB/s", "cores": 1, "kind": kind,
+           "sample": f"{sample}, median of {reps} passes after 1 warm-up, 1 thread ({impl})"}
+    if cores_all > 1:
+        tn = timed(cores_all, 5)
+        res["all_cores"] = {"value": round(total / tn / 2**30, 3), "cores": cores_all,
+                            "threads": cores_all,
+                            "sample": "same batch, disjoint ranges per thread, median of 5"}
+    res["cpu_model"] = _cpu_model()
+    res["nproc"] = os.cpu_count()
+    res["affinity_cores"] = cores_all
+    return res
+
+
 def _affinity_cores():
     try:
         return len(os.sched_getaffinity(0))
@@ -441,9 +544,13 @@ def main():
     if rank == 0 and layout in ("rx", "tx"):
         if not args.no_parity:
             parity = frames_check(spec, frames_host, buf.cpu().numpy(), status.cpu().numpy())
+        if not args.no_cpu_baseline:
+            cpu = cpu_baseline_frames(spec, frames_host)
     elif rank == 0 and layout == "chain":
         if not args.no_parity:
             parity = chain_check(chain, out.cpu().numpy())
+        if not args.no_cpu_baseline:
+            cpu = cpu_baseline_chain(chain)
     elif rank == 0:
         # rank 0 times the CPU baseline on its own shard at every world size (after the
         # timed region; the other ranks wait at the final barrier)

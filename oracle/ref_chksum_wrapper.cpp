@@ -128,6 +128,60 @@ double ref_time_batch_csr(int threads, int reps, const char *base,
     return time_batch(threads, reps, n, base, 0, 0, offsets, out);
 }
 
+// CPU baseline for chains: chain i = chunks [index[i], index[i+1]) of the table (device
+// addresses addr[k] - addr_bias = host addresses), linked as IpBufNodes once, outside the
+// timing, as the stack holds them (a TCP header node + send-ring nodes). Each timed pass
+// computes IpChksumAccumulator(State(states[i])).getChksum(IpBufRef{chain i}) for every
+// chain (Chksum.h:171-174, 263-336), `threads` std::threads over disjoint chain ranges.
+double ref_time_batch_chain(int threads, int reps, std::uint64_t addr_bias,
+                            const std::uint64_t *addr, const std::uint32_t *len,
+                            const std::uint64_t *index, const std::uint32_t *states,
+                            std::uint64_t n, std::uint16_t *out)
+{
+    if (threads < 1)
+        threads = 1;
+    const std::uint64_t nchunks = index[n];
+    std::vector<IpBufNode> nodes(nchunks ? nchunks : 1);
+    std::vector<std::size_t> tot(n);
+    for (std::uint64_t i = 0; i < n; i++) {
+        std::size_t t = 0;
+        for (std::uint64_t k = index[i]; k < index[i + 1]; k++) {
+            nodes[k].ptr = reinterpret_cast<char *>(addr[k] - addr_bias);
+            nodes[k].len = len[k];
+            nodes[k].next = k + 1 < index[i + 1] ? &nodes[k + 1] : nullptr;
+            t += len[k];
+        }
+        tot[i] = t;
+    }
+    auto pass = [&]() {
+        std::vector<std::thread> pool;
+        for (int th = 0; th < threads; th++) {
+            std::uint64_t lo = n * std::uint64_t(th) / std::uint64_t(threads);
+            std::uint64_t hi = n * std::uint64_t(th + 1) / std::uint64_t(threads);
+            pool.emplace_back([&, lo, hi]() {
+                for (std::uint64_t i = lo; i < hi; i++) {
+                    IpChksumAccumulator acc{IpChksumAccumulator::State(states[i])};
+                    out[i] = index[i + 1] > index[i]
+                                 ? acc.getChksum(IpBufRef{&nodes[index[i]], 0, tot[i]})
+                                 : acc.getChksum();
+                }
+            });
+        }
+        for (auto &t : pool)
+            t.join();
+    };
+    pass();
+    std::vector<double> times;
+    for (int r = 0; r < reps; r++) {
+        auto t0 = std::chrono::steady_clock::now();
+        pass();
+        auto t1 = std::chrono::steady_clock::now();
+        times.push_back(std::chrono::duration<double>(t1 - t0).count());
+    }
+    std::sort(times.begin(), times.end());
+    return times.empty() ? 0.0 : times[times.size() / 2];
+}
+
 } // extern "C"
 
 // The reference stack's checksum call sequences (tests/cpp/call_sites.inc, shared text with
