@@ -1,7 +1,7 @@
 #!/bin/bash
-# Chain kernel: two segments per lane per window (product) vs one (lib_prev = HEAD bab2a58).
+# Chain kernel A/B: product vs lib_prev (HEAD bab2a58).
 set -e
-out=gpurun_out/r02z
+out=gpurun_out/${1:-r02z}
 mkdir -p "$out"
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -k "chain" -x -q --timeout 120 --timeout-method thread > "$out/pytest_chain.log" 2>&1
