@@ -534,6 +534,13 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     max_elapsed = float(t.item())
+    # every rank's own wall time and kernel time (control plane only; after the timed region)
+    mine = torch.tensor([elapsed, avg_kernel_s], dtype=torch.float64)
+    ranks = [torch.zeros(2, dtype=torch.float64) for _ in range(world)]
+    if world > 1:
+        dist.all_gather(ranks, mine)
+    else:
+        ranks = [mine]
 
     payload = spec.get("payload", total)
     alg = algorithmic_bytes(layout, n, payload)
@@ -604,6 +611,11 @@ def main():
                                   "median": round(per_launch[len(per_launch) // 2], 2),
                                   "max": round(per_launch[-1], 2)}} if per_launch else {}),
             "algorithmic_bytes_per_launch": alg,
+        },
+        "per_gpu": {
+            "GiB_s": [round(spec.get("payload", total) * args.steps / float(r[0]) / 2**30, 2)
+                      for r in ranks],
+            "kernel_us": [round(float(r[1]) * 1e6, 2) for r in ranks],
         },
         "cpu_baseline": cpu,
         "parity": parity,

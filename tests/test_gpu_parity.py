@@ -390,6 +390,9 @@ def test_bench_two_ranks_one_gpu():
     cpu = d["cpu_baseline"]
     assert cpu is not None and cpu["value"] > 0 and cpu["cores"] == 1
     assert cpu["affinity_cores"] >= 1
+    per = d["per_gpu"]  # every rank's own rate and kernel time
+    assert len(per["GiB_s"]) == 2 and len(per["kernel_us"]) == 2
+    assert min(per["GiB_s"]) > 0 and min(per["kernel_us"]) > 0
 
 
 # ---- host-memory streaming engine ------------------------------------
