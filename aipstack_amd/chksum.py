@@ -561,14 +561,15 @@ def tx_fill(frames, offsets, *, out=None, stream=None, split=True, workspace=Non
         _same_device(frames, workspace, "frames and workspace")
     ws_bytes = workspace.numel() * workspace.element_size()
     launch_stream = torch.cuda.current_stream(frames.device) if stream is None else stream
+    if not hasattr(launch_stream, "cuda_stream"):  # a raw hipStream_t handle
+        launch_stream = torch.cuda.ExternalStream(int(launch_stream), device=frames.device)
     _check(lib.aipstack_chksum_tx_fill_split(frames.data_ptr(), offsets.data_ptr(), n,
                                              out.data_ptr(), workspace.data_ptr(), ws_bytes,
                                              _stream_handle(launch_stream)),
            "aipstack_chksum_tx_fill_split")
     # The caching allocator must not hand the workspace out again before both passes on
     # the launch stream are done with it (it may not be torch's current stream).
-    if hasattr(launch_stream, "cuda_stream"):
-        workspace.record_stream(launch_stream)
+    workspace.record_stream(launch_stream)
     return out
 
 

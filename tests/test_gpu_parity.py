@@ -719,6 +719,28 @@ def test_tx_fill_split_workspace_and_ragged_counts(oracle):
         A.tx_fill(dbuf, doff, workspace=ws[: 8 * n - 8])
 
 
+@pytest.mark.parametrize("raw_handle", [False, True])
+def test_tx_fill_split_on_a_non_current_stream(oracle, raw_handle):
+    """The split fill's temporary workspace stays reserved for the launch stream when that
+    is not torch's current stream (a torch Stream, or a raw hipStream_t handle): torch's
+    allocator may not reuse it while the passes run. Allocations on the current stream
+    meanwhile must not disturb the result."""
+    import torch
+    s = torch.cuda.Stream()
+    buf, off = synth.frames_host(50000, seed=17)
+    dbuf, doff = _d(buf), _d(off)
+    torch.cuda.synchronize()
+    st = A.tx_fill(dbuf, doff, stream=s.cuda_stream if raw_handle else s)
+    junk = [torch.full((8 * 50000,), 0xAB, dtype=torch.uint8, device=DEV) for _ in range(4)]
+    s.synchronize()
+    torch.cuda.synchronize()
+    want = buf.copy()
+    want_st = oracle.tx_fill_batch(want, off)
+    assert np.array_equal(_np(st), want_st)
+    assert np.array_equal(_np(dbuf), want)
+    del junk
+
+
 def test_fill_then_verify_on_gpu():
     buf, off = synth.frames_host(100000, seed=13)
     dbuf, doff = _d(buf), _d(off)
