@@ -786,3 +786,59 @@ def test_tx_fill_edge_frames(oracle, stream_mode, shift, su, split):
     assert np.array_equal(st, want_st)
     got = _np(dbig)[shift:]
     assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
+
+
+# ---- hipGraph capture: the batch entry points never allocate or synchronise ----------------
+
+def test_batches_captured_in_a_graph_and_replayed(oracle):
+    """Strided, CSR, Rx verify and the split Tx fill captured once into one HIP graph
+    (torch.cuda.CUDAGraph) and replayed over new bytes written into the same buffers: every
+    replay matches the oracle (the calls are graph-capturable)."""
+    n, plen = 4096, 1500
+    sbuf = torch.empty(n * plen, dtype=torch.uint8, device=DEV)
+    hbuf, off = synth.mixed_batch(3000)
+    cbuf = torch.empty(hbuf.size, dtype=torch.uint8, device=DEV)
+    coff = _d(off)
+    fr, foff = synth.frames_host(2000, seed=5)
+    rbuf = torch.empty(fr.size, dtype=torch.uint8, device=DEV)
+    tbuf = torch.empty(fr.size, dtype=torch.uint8, device=DEV)
+    dfoff = _d(foff)
+    ws = torch.empty(8 * 2000, dtype=torch.uint8, device=DEV)
+    s_out = torch.empty(n, dtype=torch.uint16, device=DEV)
+    c_out = torch.empty(3000, dtype=torch.uint16, device=DEV)
+    r_out = torch.empty(2000, dtype=torch.uint8, device=DEV)
+    t_out = torch.empty(2000, dtype=torch.uint8, device=DEV)
+
+    def step():
+        A.chksum_batch_strided(sbuf, plen, plen, n, out=s_out)
+        A.chksum_batch_csr(cbuf, coff, out=c_out, final=True)
+        A.rx_verify(rbuf, dfoff, out=r_out)
+        A.tx_fill(tbuf, dfoff, out=t_out, workspace=ws)
+
+    step()  # warm-up outside the capture (the library caches the device's CU count)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        step()
+    for rep in range(3):
+        rng = np.random.default_rng(100 + rep)
+        sh = rng.integers(0, 256, n * plen, dtype=np.uint8)
+        ch = rng.integers(0, 256, hbuf.size, dtype=np.uint8)
+        rx = fr.copy()
+        oracle.tx_fill_batch(rx, foff)
+        _corrupt_rx = rng.random(2000) < 0.2
+        for i in np.nonzero(_corrupt_rx)[0]:
+            rx[int(foff[i]) + int(rng.integers(14, int(foff[i + 1] - foff[i])))] ^= 0x10
+        tx = fr.copy()
+        sbuf.copy_(torch.from_numpy(sh))
+        cbuf.copy_(torch.from_numpy(ch))
+        rbuf.copy_(torch.from_numpy(rx))
+        tbuf.copy_(torch.from_numpy(tx))
+        g.replay()
+        torch.cuda.synchronize()
+        assert np.array_equal(_np(s_out), oracle.batch_strided(sh, plen, plen, n))
+        assert np.array_equal(_np(c_out), oracle.batch_csr(ch, off, final=True))
+        assert np.array_equal(_np(r_out), oracle.rx_verify_batch(rx, foff))
+        want_st = oracle.tx_fill_batch(tx, foff)
+        assert np.array_equal(_np(t_out), want_st)
+        assert np.array_equal(_np(tbuf), tx)
