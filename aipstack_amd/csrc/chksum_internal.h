@@ -15,6 +15,8 @@ int device_cu_count();
 // Frames a wave of the Rx-verify / Tx-fill kernels keeps in flight (tunable "frames":
 // 2, 4 or 8; default 4).
 int tuning_frames_in_flight();
+// Frames per chunk of the frame kernels: 64, or fewer for a small batch (pick_shape).
+uint32_t frames_per_chunk(uint64_t n, int cus);
 
 // Resident-wave budget per CU the grids are sized to (tunable "waves_per_cu"; 0 = each
 // kernel's default).

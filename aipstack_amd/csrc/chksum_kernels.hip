@@ -48,11 +48,14 @@ namespace aipstack_amd {
 namespace {
 
 // ---------------------------------------------------------------------------------
-// The kernel: wave w handles 64-packet chunks [w*cpw, (w+1)*cpw).
+// The kernel: wave w handles chunks [w*cpw, (w+1)*cpw) of `chunk_packets` (<= 64) packets
+// each: 64 for large batches, fewer for small ones, so that a small batch still spreads
+// over many waves (launch(): the small-batch regime).
 // ---------------------------------------------------------------------------------
 template <class Desc, int U, int P, bool NT, bool SEEDED, int SU>
 __global__ __launch_bounds__(kBlock) void chksum_batch_kernel(Desc desc, uint64_t n,
                                                               uint32_t chunks_per_wave,
+                                                              uint32_t chunk_packets,
                                                               uint16_t *__restrict__ out,
                                                               uint32_t flags) {
     const int lane = threadIdx.x & (kWave - 1);
@@ -60,7 +63,8 @@ __global__ __launch_bounds__(kBlock) void chksum_batch_kernel(Desc desc, uint64_
     // keeps the whole packet walk (bounds, loop counters) in SGPRs.
     const uint32_t wave_in_block = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerBlock + wave_in_block;
-    const uint64_t nchunks = (n + kWave - 1) / kWave;
+    const uint64_t cpk = chunk_packets;  // 1..64 (launch_k)
+    const uint64_t nchunks = (n + cpk - 1) / cpk;
     uint64_t c = wave * chunks_per_wave;
     const uint64_t c_end = min(c + chunks_per_wave, nchunks);
     const bool final_flag = (flags & AIPSTACK_CHKSUM_FINAL) != 0;
@@ -68,9 +72,9 @@ __global__ __launch_bounds__(kBlock) void chksum_batch_kernel(Desc desc, uint64_
     const uint32_t not_lane0 = lane == 0 ? 0u : ~0u;     // head-mask lane select
 
     for (; c < c_end; ++c) {
-        const uint64_t p0 = c * kWave;
+        const uint64_t p0 = c * cpk;
         const auto chunk = desc.begin_chunk(p0, n, lane);
-        const int cnt = (int)min((uint64_t)kWave, n - p0);
+        const int cnt = (int)min(cpk, n - p0);
         // every packet's load parameters at once: lane j <-> packet j (VALU, vectorised)
         uint64_t lS, lE;
         desc.lane_bounds(chunk, lane, lS, lE);
@@ -143,7 +147,8 @@ template <bool NT, int SU>
 __global__ __launch_bounds__(kBlock, 5) void chksum_chain_kernel(
     const uint64_t *__restrict__ chunk_addr, const uint32_t *__restrict__ chunk_len,
     const uint64_t *__restrict__ index, const uint32_t *__restrict__ states, uint64_t n,
-    uint32_t chunks_per_wave, uint16_t *__restrict__ out, uint32_t flags) {
+    uint32_t chunks_per_wave, uint32_t chains_per_group, uint16_t *__restrict__ out,
+    uint32_t flags) {
     __shared__ uint64_t lds_acc[kWavesPerBlock][kWave];  // per-chain sum of chunk sums
     __shared__ int lds_mark[kWavesPerBlock][kWave];      // chain starting at chunk lane
     __shared__ GatherLds lds_gather[kWavesPerBlock];                  // gathered stream owners
@@ -153,7 +158,8 @@ __global__ __launch_bounds__(kBlock, 5) void chksum_chain_kernel(
     const int lane = threadIdx.x & (kWave - 1);
     const uint32_t wave_in_block = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerBlock + wave_in_block;
-    const uint64_t ngroups = (n + kWave - 1) / kWave;
+    const uint64_t cpg = chains_per_group;  // 1..64: fewer for small batches (pick_shape)
+    const uint64_t ngroups = (n + cpg - 1) / cpg;
     uint64_t c = wave * chunks_per_wave;
     const uint64_t c_end = min(c + chunks_per_wave, ngroups);
     const bool final_flag = (flags & AIPSTACK_CHKSUM_FINAL) != 0;
@@ -162,16 +168,19 @@ __global__ __launch_bounds__(kBlock, 5) void chksum_chain_kernel(
     CsrDesc idx_desc{0, index};  // the chain index walks like CSR offsets
 
     for (; c < c_end; ++c) {
-        const uint64_t p0 = c * kWave;
+        const uint64_t p0 = c * cpg;
         const auto grp = idx_desc.begin_chunk(p0, n, lane);
-        const int cnt = (int)min((uint64_t)kWave, n - p0);
+        const int cnt = (int)min(cpg, n - p0);
         const uint32_t state = (states != nullptr && p0 + lane < n) ? states[p0 + lane] : 0u;
         // chain `lane` = chunks [cs, ce) (relative to the group's first chunk K0)
         uint64_t cs64, ce64;
         idx_desc.lane_bounds(grp, lane, cs64, ce64);
         const uint64_t K0 = idx_desc.offset_of(grp, 0);
-        const uint64_t K1 = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(grp.end_off >> 32))
-                             << 32) | __builtin_amdgcn_readfirstlane((uint32_t)grp.end_off);
+        // the group's chunks end where chain p0 + cnt starts (lane cnt's index entry)
+        const uint64_t K1 =
+            cnt < kWave ? idx_desc.offset_of(grp, cnt)
+                        : ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(grp.end_off >> 32))
+                           << 32) | __builtin_amdgcn_readfirstlane((uint32_t)grp.end_off);
         const bool chain_nonempty = lane < cnt && ce64 > cs64;
         const uint32_t cs = (uint32_t)(cs64 - K0);  // < 2^32 chunks per group (contract)
         acc[lane] = 0;
@@ -300,10 +309,40 @@ int pick_packets(int u, bool csr) {
 // 266 us on config C).
 int pick_stream(bool csr) { return tuning_stream_windows(csr ? 8 : 2); }
 
+// Small batches. A 64-packet chunk per wave leaves a small batch on a few waves, each
+// streaming ~100 KB with 2 windows (2 KiB) in flight: latency-bound (a 64-packet batch
+// took 23 us, a 4096-packet one 33 us). Below kSmallWavesPerCu waves per CU at 64 packets
+// per chunk, chunks shrink (packets per chunk = the power of two that gives about
+// kSmallTargetPerCu waves per CU, at least 1) and every wave keeps 8 windows in flight.
+constexpr uint64_t kSmallWavesPerCu = 8;
+constexpr uint64_t kSmallTargetPerCu = 4;
+
+struct Shape {
+    uint32_t chunk_packets;  // packets per chunk (64: the large-batch shape)
+    bool small;
+};
+
+Shape pick_shape(uint64_t n, int cus) {
+    const uint64_t chunks64 = (n + kWave - 1) / kWave;
+    if (chunks64 >= (uint64_t)cus * kSmallWavesPerCu) return Shape{(uint32_t)kWave, false};
+    const uint64_t per = (n + (uint64_t)cus * kSmallTargetPerCu - 1) / ((uint64_t)cus * kSmallTargetPerCu);
+    uint32_t cpk = 1;
+    while (cpk < per && cpk < (uint32_t)kWave) cpk <<= 1;
+    return Shape{cpk, true};
+}
+
+// SU for a launch: the tuned value, else 8 windows in the small-batch regime, else the
+// family default.
+int pick_stream_for(bool csr, const Shape &sh) {
+    const int t = tuning().stream.load(std::memory_order_relaxed);
+    if (t < 0 || t == 2 || t == 4 || t == 8) return tuning_stream_windows(0);
+    return sh.small ? 8 : pick_stream(csr);
+}
+
 template <class Desc, int U, int P, bool NT, bool SEEDED, int SU>
-int launch_k(const Desc &desc, uint64_t n, uint16_t *d_out, uint32_t flags,
+int launch_k(const Desc &desc, uint64_t n, const Shape &sh, uint16_t *d_out, uint32_t flags,
              hipStream_t stream) {
-    const uint64_t nchunks = (n + kWave - 1) / kWave;
+    const uint64_t nchunks = (n + sh.chunk_packets - 1) / sh.chunk_packets;
     const int cus = device_cu_count();
     if (cus <= 0) return AIPSTACK_CHKSUM_EHIP;
     uint64_t cpw = (uint64_t)tuning().chunks_per_wave.load(std::memory_order_relaxed);
@@ -318,38 +357,39 @@ int launch_k(const Desc &desc, uint64_t n, uint16_t *d_out, uint32_t flags,
     const uint64_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
     if (blocks > 0x7FFFFFFFull || cpw > 0xFFFFFFFFull) return AIPSTACK_CHKSUM_EINVAL;
     hipLaunchKernelGGL((chksum_batch_kernel<Desc, U, P, NT, SEEDED, SU>), dim3((unsigned)blocks),
-                       dim3(kBlock), 0, stream, desc, n, (uint32_t)cpw, d_out, flags);
+                       dim3(kBlock), 0, stream, desc, n, (uint32_t)cpw, sh.chunk_packets, d_out,
+                       flags);
     return check_hip(hipGetLastError());
 }
 
 template <class Desc, int U, int P, bool SEEDED>
-int launch_s(const Desc &desc, uint64_t n, uint16_t *d_out, uint32_t flags,
+int launch_s(const Desc &desc, uint64_t n, const Shape &sh, uint16_t *d_out, uint32_t flags,
              hipStream_t stream) {
     if (tuning().nontemporal.load(std::memory_order_relaxed) == 0)  // sweeps only
-        return launch_k<Desc, U, P, false, SEEDED, 0>(desc, n, d_out, flags, stream);
-    switch (pick_stream(Desc::kCsr)) {
-        case 0: return launch_k<Desc, U, P, true, SEEDED, 0>(desc, n, d_out, flags, stream);
-        case 2: return launch_k<Desc, U, P, true, SEEDED, 2>(desc, n, d_out, flags, stream);
-        case 8: return launch_k<Desc, U, P, true, SEEDED, 8>(desc, n, d_out, flags, stream);
-        default: return launch_k<Desc, U, P, true, SEEDED, 4>(desc, n, d_out, flags, stream);
+        return launch_k<Desc, U, P, false, SEEDED, 0>(desc, n, sh, d_out, flags, stream);
+    switch (pick_stream_for(Desc::kCsr, sh)) {
+        case 0: return launch_k<Desc, U, P, true, SEEDED, 0>(desc, n, sh, d_out, flags, stream);
+        case 2: return launch_k<Desc, U, P, true, SEEDED, 2>(desc, n, sh, d_out, flags, stream);
+        case 8: return launch_k<Desc, U, P, true, SEEDED, 8>(desc, n, sh, d_out, flags, stream);
+        default: return launch_k<Desc, U, P, true, SEEDED, 4>(desc, n, sh, d_out, flags, stream);
     }
 }
 
 template <class Desc, int U, bool SEEDED>
-int launch_u(const Desc &desc, uint64_t n, uint16_t *d_out, uint32_t flags,
+int launch_u(const Desc &desc, uint64_t n, const Shape &sh, uint16_t *d_out, uint32_t flags,
              hipStream_t stream) {
     int p = pick_packets(U, Desc::kCsr);
     // Every chunk takes stream mode: the per-packet path is never run, so give it the
     // fewest registers (the kernel's occupancy is set by the larger of the two paths).
-    if (desc.back_to_back() && pick_stream(Desc::kCsr) > 0 &&
+    if (desc.back_to_back() && pick_stream_for(Desc::kCsr, sh) > 0 &&
         tuning().nontemporal.load(std::memory_order_relaxed) != 0 &&
         tuning().packets.load(std::memory_order_relaxed) == 0)
         p = 1;
     switch (p) {
-        case 1: return launch_s<Desc, U, 1, SEEDED>(desc, n, d_out, flags, stream);
-        case 2: return launch_s<Desc, U, 2, SEEDED>(desc, n, d_out, flags, stream);
-        case 4: return launch_s<Desc, U, 4, SEEDED>(desc, n, d_out, flags, stream);
-        case 8: return launch_s<Desc, U, 8, SEEDED>(desc, n, d_out, flags, stream);
+        case 1: return launch_s<Desc, U, 1, SEEDED>(desc, n, sh, d_out, flags, stream);
+        case 2: return launch_s<Desc, U, 2, SEEDED>(desc, n, sh, d_out, flags, stream);
+        case 4: return launch_s<Desc, U, 4, SEEDED>(desc, n, sh, d_out, flags, stream);
+        case 8: return launch_s<Desc, U, 8, SEEDED>(desc, n, sh, d_out, flags, stream);
     }
     return AIPSTACK_CHKSUM_EINVAL;
 }
@@ -358,11 +398,14 @@ template <class Desc, bool SEEDED>
 int launch(const Desc &desc, uint64_t n, uint32_t max_len, uint16_t *d_out, uint32_t flags,
            hipStream_t stream) {
     if (n == 0) return AIPSTACK_CHKSUM_OK;
+    const int cus = device_cu_count();
+    if (cus <= 0) return AIPSTACK_CHKSUM_EHIP;
+    const Shape sh = pick_shape(n, cus);
     switch (pick_unroll(max_len)) {
-        case 1: return launch_u<Desc, 1, SEEDED>(desc, n, d_out, flags, stream);
-        case 2: return launch_u<Desc, 2, SEEDED>(desc, n, d_out, flags, stream);
-        case 3: return launch_u<Desc, 3, SEEDED>(desc, n, d_out, flags, stream);
-        case 4: return launch_u<Desc, 4, SEEDED>(desc, n, d_out, flags, stream);
+        case 1: return launch_u<Desc, 1, SEEDED>(desc, n, sh, d_out, flags, stream);
+        case 2: return launch_u<Desc, 2, SEEDED>(desc, n, sh, d_out, flags, stream);
+        case 3: return launch_u<Desc, 3, SEEDED>(desc, n, sh, d_out, flags, stream);
+        case 4: return launch_u<Desc, 4, SEEDED>(desc, n, sh, d_out, flags, stream);
     }
     return AIPSTACK_CHKSUM_EINVAL;
 }
@@ -371,9 +414,10 @@ template <bool NT, int SU>
 int launch_chain(const uint64_t *d_addr, const uint32_t *d_len, const uint64_t *d_index,
                  const uint32_t *d_states, uint64_t n, uint16_t *d_out, uint32_t flags,
                  hipStream_t stream) {
-    const uint64_t nchunks = (n + kWave - 1) / kWave;
     const int cus = device_cu_count();
     if (cus <= 0) return AIPSTACK_CHKSUM_EHIP;
+    const uint32_t cpg = pick_shape(n, cus).chunk_packets;  // chains per group
+    const uint64_t nchunks = (n + cpg - 1) / cpg;
     const uint64_t target_waves = (uint64_t)cus * 2 * kDefaultWavesPerCu;
     uint64_t cpw = (nchunks + target_waves - 1) / target_waves;
     if (cpw == 0) cpw = 1;
@@ -381,7 +425,8 @@ int launch_chain(const uint64_t *d_addr, const uint32_t *d_len, const uint64_t *
     const uint64_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
     if (blocks > 0x7FFFFFFFull || cpw > 0xFFFFFFFFull) return AIPSTACK_CHKSUM_EINVAL;
     hipLaunchKernelGGL((chksum_chain_kernel<NT, SU>), dim3((unsigned)blocks), dim3(kBlock), 0,
-                       stream, d_addr, d_len, d_index, d_states, n, (uint32_t)cpw, d_out, flags);
+                       stream, d_addr, d_len, d_index, d_states, n, (uint32_t)cpw, cpg, d_out,
+                       flags);
     return check_hip(hipGetLastError());
 }
 
@@ -397,6 +442,8 @@ int tuning_stream_windows(int family_default) {
     if (t == 2 || t == 4 || t == 8) return t;
     return family_default;
 }
+
+uint32_t frames_per_chunk(uint64_t n, int cus) { return pick_shape(n, cus).chunk_packets; }
 
 int tuning_frames_in_flight() {
     const int f = tuning().frames.load(std::memory_order_relaxed);

@@ -409,10 +409,11 @@ __device__ __forceinline__ uint32_t l4s_below(const u32x4 (&seg)[kHdrSegs], uint
 #endif
 template <bool TX, int U, int P, bool NT, int SU>
 __device__ __forceinline__ FrameOut process_chunk(const CsrDesc &desc, uint64_t p0, uint64_t n,
-                                                  int lane, uint32_t voff, uint32_t not_lane0,
-                                                  FrameLds *lds, int &cnt_out) {
+                                                  uint32_t cpk, int lane, uint32_t voff,
+                                                  uint32_t not_lane0, FrameLds *lds,
+                                                  int &cnt_out) {
     const auto chunk = desc.begin_chunk(p0, n, lane);
-    const int cnt = (int)min((uint64_t)kWave, n - p0);
+    const int cnt = (int)min((uint64_t)cpk, n - p0);
     cnt_out = cnt;
     uint64_t S, E;
     desc.lane_bounds(chunk, lane, S, E);
@@ -437,9 +438,9 @@ __device__ __forceinline__ FrameOut process_chunk(const CsrDesc &desc, uint64_t 
     u32x4 seg[kHdrSegs];
     auto load_headers = [&]() {
 #pragma unroll
-        for (int i = 0; i < kHdrSegs; ++i)  // past hb_end: out of range, reads 0, no traffic
-            seg[i] = load_segment<false>(hrsrc, 16u * i < hb_end ? hoff + 16u * i : 0xFFFFFFF0u,
-                                         0u);
+        for (int i = 0; i < kHdrSegs; ++i)  // past hb_end or the chunk: out of range, reads 0
+            seg[i] = load_segment<false>(
+                hrsrc, 16u * i < hb_end && lane < cnt ? hoff + 16u * i : 0xFFFFFFF0u, 0u);
     };
     FrameLane fl;
     uint32_t r;
@@ -621,12 +622,14 @@ __device__ __forceinline__ FrameOut process_chunk(const CsrDesc &desc, uint64_t 
 template <bool TX, int U, int P, bool NT, int SU, bool SPLIT>
 __global__ __launch_bounds__(kBlock, AIPSTACK_FRAME_WAVES_PER_SIMD) void frame_kernel(CsrDesc desc, uint64_t n,
                                                        uint32_t chunks_per_wave,
+                                                       uint32_t chunk_packets,
                                                        uint8_t *__restrict__ status,
                                                        uint64_t *__restrict__ records) {
     const int lane = threadIdx.x & (kWave - 1);
     const uint32_t wave_in_block = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerBlock + wave_in_block;
-    const uint64_t nchunks = (n + kWave - 1) / kWave;
+    const uint64_t cpk = chunk_packets;  // frames per chunk, 1..64 (launch_frames)
+    const uint64_t nchunks = (n + cpk - 1) / cpk;
     uint64_t c = wave * chunks_per_wave;
     const uint64_t c_end = min(c + chunks_per_wave, nchunks);
     const uint32_t voff = (uint32_t)lane * 16u;
@@ -635,10 +638,10 @@ __global__ __launch_bounds__(kBlock, AIPSTACK_FRAME_WAVES_PER_SIMD) void frame_k
     __shared__ FrameLds lds[kGather ? kWavesPerBlock : 1];  // 9 KiB per wave (gathered stream)
     FrameLds *my = &lds[kGather ? wave_in_block : 0];
     for (; c < c_end; ++c) {
-        const uint64_t p0 = c * kWave;
+        const uint64_t p0 = c * cpk;
         int cnt;
-        const FrameOut o =
-            process_chunk<TX, U, P, NT, SU>(desc, p0, n, lane, voff, not_lane0, my, cnt);
+        const FrameOut o = process_chunk<TX, U, P, NT, SU>(desc, p0, n, (uint32_t)cpk, lane, voff,
+                                                           not_lane0, my, cnt);
         if (lane < cnt) {
             if constexpr (SPLIT)
 #if AIPSTACK_EXP_NO_RECORDS  // experiment: price of the record stores (wrong output)
@@ -655,9 +658,12 @@ __global__ __launch_bounds__(kBlock, AIPSTACK_FRAME_WAVES_PER_SIMD) void frame_k
 template <bool TX, bool SPLIT = false>
 int launch_frames(const void *d_base, const uint64_t *d_offsets, uint64_t n, uint8_t *d_status,
                   uint64_t *d_records, hipStream_t stream) {
-    const uint64_t nchunks = (n + kWave - 1) / kWave;
     const int cus = device_cu_count();
     if (cus <= 0) return AIPSTACK_CHKSUM_EHIP;
+    // small batches: fewer frames per chunk, so that they spread over many waves (as the
+    // checksum batches, chksum_kernels.hip pick_shape)
+    const uint32_t cpk = frames_per_chunk(n, cus);
+    const uint64_t nchunks = (n + cpk - 1) / cpk;
     CsrDesc desc{(uint64_t)(uintptr_t)d_base, d_offsets};
     const int su = tuning_stream_windows(8);  // measured: 8 > 4 > off > 2 (RX and TX)
     const int wpc = tuning_waves_per_cu();
@@ -669,7 +675,7 @@ int launch_frames(const void *d_base, const uint64_t *d_offsets, uint64_t n, uin
     if (blocks > 0x7FFFFFFFull || cpw > 0xFFFFFFFFull) return AIPSTACK_CHKSUM_EINVAL;
 #define AIPSTACK_LAUNCH_FRAMES(P, SU)                                                          \
     hipLaunchKernelGGL((frame_kernel<TX, 2, P, AIPSTACK_FRAME_NT != 0, SU, SPLIT>), dim3((unsigned)blocks),        \
-                       dim3(kBlock), 0, stream, desc, n, (uint32_t)cpw, d_status, d_records)
+                       dim3(kBlock), 0, stream, desc, n, (uint32_t)cpw, cpk, d_status, d_records)
 #define AIPSTACK_LAUNCH_FRAMES_SU(P)              \
     switch (su) {                                 \
         case 0: AIPSTACK_LAUNCH_FRAMES(P, 0); break; \

@@ -103,6 +103,10 @@ def parse():
                    help="with --e2e: do not page-lock the host batch (CPU copy to staging)")
     p.add_argument("--tx-inplace", action="store_true",
                    help="TX: the one-pass in-place fill (default: the two-pass split fill)")
+    p.add_argument("--small", type=int, default=0, metavar="N",
+                   help="small-batch mode (A or RX): batches of N packets/frames from a ring of "
+                        "64 slots, eager launches vs the same launches replayed from a HIP "
+                        "graph. Prints its own line.")
     p.add_argument("--e2e-streams", type=int, default=4)
     p.add_argument("--e2e-chunk-mib", type=int, default=64)
     return p.parse_args()
@@ -451,6 +455,10 @@ def main():
 
     layout, n, plen = CONFIGS[args.config]
     stream = torch.cuda.current_stream()
+    if args.small:
+        if args.config not in ("A", "RX") or world > 1:
+            raise SystemExit("--small covers configs A and RX on one GPU")
+        return small_batches(args, layout, plen, dev)
     if args.e2e:
         if layout not in ("strided", "csr"):
             raise SystemExit("--e2e covers the packet configs A, B, C")
@@ -625,6 +633,110 @@ def main():
     if world > 1:
         dist.destroy_process_group()
     if parity == "MISMATCH":
+        sys.exit(1)
+
+
+def small_batches(args, layout, plen, dev):
+    """Launch-bound regime: a receive loop hands over small bursts (N packets or frames per
+    batch), each its own launch on one stream. R = 64 ring slots, one batch per slot; K
+    batches timed eagerly (one wrapper call and launch each) and then as replays of one HIP
+    graph that holds the R launches (torch.cuda.CUDAGraph capture of the same calls). HIP
+    events on the stream around K batches; the last batch of each form checked against the
+    oracle."""
+    import torch
+    import aipstack_amd as A
+    from aipstack_amd import synth
+    R, N = 64, args.small
+    K = max(R, (args.steps * 50) // R * R)
+    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "libchksum_oracle.so"))
+    if layout == "strided":
+        buf = torch.empty(R * N * plen, dtype=torch.uint8, device=dev)
+        synth.fill_device(buf, synth.SEED_DATA)
+        outs = [torch.empty(N, dtype=torch.uint16, device=dev) for _ in range(R)]
+        views = [buf[r * N * plen:(r + 1) * N * plen] for r in range(R)]
+
+        def launch(r):
+            A.chksum_batch_strided(views[r], plen, plen, N, out=outs[r])
+        payload = N * plen
+
+        def check(r):
+            lib.oracle_batch_strided.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                                                 ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32]
+            host = views[r].cpu().numpy()
+            want = np.empty(N, dtype=np.uint16)
+            lib.oracle_batch_strided(host.ctypes.data, plen, plen, N, want.ctypes.data, 0)
+            return np.array_equal(outs[r].cpu().numpy(), want)
+    else:
+        frames, off = synth.frames_host(R * N, seed=synth.SEED_DATA, max_payload=1460)
+        lib.oracle_tx_fill_batch.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_uint64, ctypes.c_void_p]
+        st = np.empty(R * N, dtype=np.uint8)
+        off64 = off.astype(np.uint64)  # kept alive across the call
+        lib.oracle_tx_fill_batch(frames.ctypes.data, off64.ctypes.data, R * N, st.ctypes.data)
+        buf = torch.from_numpy(frames).to(dev)
+        offs = [torch.from_numpy((off[r * N:(r + 1) * N + 1]).copy()).to(dev) for r in range(R)]
+        outs = [torch.empty(N, dtype=torch.uint8, device=dev) for _ in range(R)]
+
+        def launch(r):
+            A.rx_verify(buf, offs[r], out=outs[r])
+        payload = int(off[-1]) // R
+
+        def check(r):
+            lib.oracle_rx_verify_batch.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_uint64,
+                                                                           ctypes.c_void_p]
+            o = off[r * N:(r + 1) * N + 1].astype(np.uint64)
+            want = np.empty(N, dtype=np.uint8)
+            lib.oracle_rx_verify_batch(frames.ctypes.data, o.ctypes.data, N, want.ctypes.data)
+            return np.array_equal(outs[r].cpu().numpy(), want)
+    stream = torch.cuda.current_stream()
+    for r in range(R):
+        launch(r)
+    torch.cuda.synchronize()
+
+    def timed(body):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        e0.record(stream)
+        body()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / K, e0.elapsed_time(e1) / 1e3 / K
+
+    def eager():
+        for k in range(K):
+            launch(k % R)
+    eager()  # warm-up
+    wall_e, dev_e = timed(eager)
+    ok_e = check((K - 1) % R)
+    for o in outs:
+        o.zero_()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for r in range(R):
+            launch(r)
+    stream = torch.cuda.current_stream()
+
+    def replays():
+        for _ in range(K // R):
+            g.replay()
+    replays()
+    wall_g, dev_g = timed(replays)
+    ok_g = check(R - 1)
+    res = {
+        "metric": f"small batches ({'packets' if layout == 'strided' else 'frames'} per batch = {N}): "
+                  "us per batch, eager launches vs HIP graph replay",
+        "value": round(wall_g * 1e6, 3), "unit": "us per batch (graph, wall)",
+        "n_gpus": 1, "steps": K, "warmup": K, "higher_is_better": False,
+        "config": {"workload": f"config {args.config} in batches of {N}", "ring_slots": R,
+                   "payload_bytes_per_batch": payload},
+        "eager": {"wall_us": round(wall_e * 1e6, 3), "events_us": round(dev_e * 1e6, 3),
+                  "GiB_s": round(payload / wall_e / 2**30, 2)},
+        "graph": {"wall_us": round(wall_g * 1e6, 3), "events_us": round(dev_g * 1e6, 3),
+                  "GiB_s": round(payload / wall_g / 2**30, 2)},
+        "parity": "bit-exact" if ok_e and ok_g else "MISMATCH",
+    }
+    print(json.dumps(res), flush=True)
+    if not (ok_e and ok_g):
         sys.exit(1)
 
 
