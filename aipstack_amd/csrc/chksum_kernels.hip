@@ -258,6 +258,8 @@ struct Tuning {
                                           // read once; measured faster on configs A and B
     std::atomic<int> stream{0};           // stream mode for back-to-back chunks: windows
                                           // issued together (2, 4, 8); -1 = off
+    std::atomic<int> chunk_packets{0};    // packets per chunk (1, 2, 4, ..., 64); 0 = by
+                                          // batch size (pick_shape)
 
     Tuning() {
         auto env = [](const char *k, std::atomic<int> &v) {
@@ -270,6 +272,7 @@ struct Tuning {
         env("AIPSTACK_CHKSUM_NT", nontemporal);
         env("AIPSTACK_CHKSUM_FRAMES", frames);
         env("AIPSTACK_CHKSUM_STREAM", stream);
+        env("AIPSTACK_CHKSUM_CHUNK_PACKETS", chunk_packets);
 
     }
 };
@@ -314,8 +317,12 @@ int pick_stream(bool csr) { return tuning_stream_windows(csr ? 8 : 2); }
 // took 23 us, a 4096-packet one 33 us). Below kSmallWavesPerCu waves per CU at 64 packets
 // per chunk, chunks shrink (packets per chunk = the power of two that gives about
 // kSmallTargetPerCu waves per CU, at least 1) and every wave keeps 8 windows in flight.
-constexpr uint64_t kSmallWavesPerCu = 8;
-constexpr uint64_t kSmallTargetPerCu = 4;
+// Chosen from a sweep of 8 K..512 K packets / frames per batch (profiles/r02/small_batches/
+// shape_sweep.jsonl): config A in batches of 32 K 9.9 us at 16 packets per chunk (11.7 at
+// 32, 34.5 at 64 with 2 windows), 128 K 32.0 us at 64 packets with 8 windows (41.5 with 2);
+// from 256 K on the large-batch shape is as fast.
+constexpr uint64_t kSmallWavesPerCu = 16;
+constexpr uint64_t kSmallTargetPerCu = 8;
 
 struct Shape {
     uint32_t chunk_packets;  // packets per chunk (64: the large-batch shape)
@@ -323,6 +330,8 @@ struct Shape {
 };
 
 Shape pick_shape(uint64_t n, int cus) {
+    const int t = tuning().chunk_packets.load(std::memory_order_relaxed);
+    if (t >= 1 && t <= kWave && (t & (t - 1)) == 0) return Shape{(uint32_t)t, t < kWave};
     const uint64_t chunks64 = (n + kWave - 1) / kWave;
     if (chunks64 >= (uint64_t)cus * kSmallWavesPerCu) return Shape{(uint32_t)kWave, false};
     const uint64_t per = (n + (uint64_t)cus * kSmallTargetPerCu - 1) / ((uint64_t)cus * kSmallTargetPerCu);
@@ -499,6 +508,7 @@ extern "C" int aipstack_chksum_tune(const char *key, int value) {
     else if (!std::strcmp(key, "nontemporal")) t.nontemporal = value;
     else if (!std::strcmp(key, "frames")) t.frames = value;
     else if (!std::strcmp(key, "stream")) t.stream = value;
+    else if (!std::strcmp(key, "chunk_packets")) t.chunk_packets = value;
     else return AIPSTACK_CHKSUM_EINVAL;
     return AIPSTACK_CHKSUM_OK;
 }

@@ -646,7 +646,8 @@ def small_batches(args, layout, plen, dev):
     import torch
     import aipstack_amd as A
     from aipstack_amd import synth
-    R, N = 64, args.small
+    N = args.small
+    R = int(max(2, min(64, (4 << 30) // (N * (plen or 800)))))  # ring of at most ~4 GB
     K = max(R, (args.steps * 50) // R * R)
     lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "libchksum_oracle.so"))
     if layout == "strided":
@@ -728,6 +729,8 @@ def small_batches(args, layout, plen, dev):
         "value": round(wall_g * 1e6, 3), "unit": "us per batch (graph, wall)",
         "n_gpus": 1, "steps": K, "warmup": K, "higher_is_better": False,
         "config": {"workload": f"config {args.config} in batches of {N}", "ring_slots": R,
+                   "tuning": {k: v for k, v in os.environ.items()
+                              if k.startswith("AIPSTACK_CHKSUM_")},
                    "payload_bytes_per_batch": payload},
         "eager": {"wall_us": round(wall_e * 1e6, 3), "events_us": round(dev_e * 1e6, 3),
                   "GiB_s": round(payload / wall_e / 2**30, 2)},

@@ -213,8 +213,10 @@ int aipstack_chksum_device_check(int device);
  * in flight per wave in Rx verify / Tx fill: 2, 4, 8), "stream" (1 KiB windows a wave
  * issues together in stream mode -- a 64-packet or 64-frame chunk that lies back to back
  * in memory, or chain chunks that lie close together: 2, 4, 8; -1 turns stream mode off,
- * so every packet, frame or chunk is summed on its own). Process-wide;
- * results never depend on them. Returns _OK or _EINVAL for an unknown key. */
+ * so every packet, frame or chunk is summed on its own), "chunk_packets" (packets, frames
+ * or chains per wave chunk: 1, 2, 4, ..., 64; automatic = 64, fewer for small batches so
+ * that they spread over more waves). Process-wide; results never depend on them. Returns
+ * _OK or _EINVAL for an unknown key. */
 int aipstack_chksum_tune(const char *key, int value);
 
 /* ABI version of this header: bumped on any incompatible change. */
