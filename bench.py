@@ -456,8 +456,8 @@ def main():
     layout, n, plen = CONFIGS[args.config]
     stream = torch.cuda.current_stream()
     if args.small:
-        if args.config not in ("A", "RX") or world > 1:
-            raise SystemExit("--small covers configs A and RX on one GPU")
+        if args.config not in ("A", "RX", "TX") or world > 1:
+            raise SystemExit("--small covers configs A, RX and TX on one GPU")
         return small_batches(args, layout, plen, dev)
     if args.e2e:
         if layout not in ("strided", "csr"):
@@ -673,21 +673,27 @@ def small_batches(args, layout, plen, dev):
         st = np.empty(R * N, dtype=np.uint8)
         off64 = off.astype(np.uint64)  # kept alive across the call
         lib.oracle_tx_fill_batch(frames.ctypes.data, off64.ctypes.data, R * N, st.ctypes.data)
-        buf = torch.from_numpy(frames).to(dev)
+        buf = torch.from_numpy(frames).to(dev)  # valid frames: Tx refills them unchanged
         offs = [torch.from_numpy((off[r * N:(r + 1) * N + 1]).copy()).to(dev) for r in range(R)]
         outs = [torch.empty(N, dtype=torch.uint8, device=dev) for _ in range(R)]
+        ws = [torch.empty(8 * N, dtype=torch.uint8, device=dev) for _ in range(R)]
 
         def launch(r):
-            A.rx_verify(buf, offs[r], out=outs[r])
+            if layout == "rx":
+                A.rx_verify(buf, offs[r], out=outs[r])
+            else:
+                A.tx_fill(buf, offs[r], out=outs[r], workspace=ws[r], split=not args.tx_inplace)
         payload = int(off[-1]) // R
 
         def check(r):
-            lib.oracle_rx_verify_batch.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_uint64,
-                                                                           ctypes.c_void_p]
+            fn = lib.oracle_rx_verify_batch if layout == "rx" else lib.oracle_tx_fill_batch
+            fn.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_uint64, ctypes.c_void_p]
             o = off[r * N:(r + 1) * N + 1].astype(np.uint64)
             want = np.empty(N, dtype=np.uint8)
-            lib.oracle_rx_verify_batch(frames.ctypes.data, o.ctypes.data, N, want.ctypes.data)
-            return np.array_equal(outs[r].cpu().numpy(), want)
+            ref = frames.copy()
+            fn(ref.ctypes.data, o.ctypes.data, N, want.ctypes.data)
+            ok = np.array_equal(outs[r].cpu().numpy(), want)
+            return ok and (layout == "rx" or np.array_equal(buf.cpu().numpy(), ref))
     stream = torch.cuda.current_stream()
     for r in range(R):
         launch(r)
@@ -728,7 +734,10 @@ def small_batches(args, layout, plen, dev):
                   "us per batch, eager launches vs HIP graph replay",
         "value": round(wall_g * 1e6, 3), "unit": "us per batch (graph, wall)",
         "n_gpus": 1, "steps": K, "warmup": K, "higher_is_better": False,
-        "config": {"workload": f"config {args.config} in batches of {N}", "ring_slots": R,
+        "config": {"workload": f"config {args.config} in batches of {N}"
+                               + (" (one-pass in-place fill)" if layout == "tx" and args.tx_inplace
+                                  else " (split fill)" if layout == "tx" else ""),
+                   "ring_slots": R,
                    "tuning": {k: v for k, v in os.environ.items()
                               if k.startswith("AIPSTACK_CHKSUM_")},
                    "payload_bytes_per_batch": payload},
