@@ -708,15 +708,15 @@ def test_tx_fill_split_workspace_and_ragged_counts(oracle):
     for n in (1, 63, 64, 65, 4097):
         buf, off = synth.frames_host(n, seed=100 + n)
         dbuf, doff = _d(buf), _d(off)
-        st = _np(A.tx_fill(dbuf, doff, workspace=ws[8:]))
+        st = _np(A.tx_fill(dbuf, doff, workspace=ws[8:], split=True))
         want = buf.copy()
         want_st = oracle.tx_fill_batch(want, off)
         assert np.array_equal(st, want_st)
         assert np.array_equal(_np(dbuf), want)
-        st2 = _np(A.tx_fill(dbuf, doff, workspace=ws[8:]))  # fill is idempotent
+        st2 = _np(A.tx_fill(dbuf, doff, workspace=ws[8:], split=True))  # fill is idempotent
         assert np.array_equal(st2, want_st) and np.array_equal(_np(dbuf), want)
     with pytest.raises(A.ChksumError):
-        A.tx_fill(dbuf, doff, workspace=ws[: 8 * n - 8])
+        A.tx_fill(dbuf, doff, workspace=ws[: 8 * n - 8], split=True)
 
 
 @pytest.mark.parametrize("raw_handle", [False, True])
@@ -730,7 +730,7 @@ def test_tx_fill_split_on_a_non_current_stream(oracle, raw_handle):
     buf, off = synth.frames_host(50000, seed=17)
     dbuf, doff = _d(buf), _d(off)
     torch.cuda.synchronize()
-    st = A.tx_fill(dbuf, doff, stream=s.cuda_stream if raw_handle else s)
+    st = A.tx_fill(dbuf, doff, stream=s.cuda_stream if raw_handle else s, split=True)
     junk = [torch.full((8 * 50000,), 0xAB, dtype=torch.uint8, device=DEV) for _ in range(4)]
     s.synchronize()
     torch.cuda.synchronize()
@@ -813,7 +813,7 @@ def test_batches_captured_in_a_graph_and_replayed(oracle):
         A.chksum_batch_strided(sbuf, plen, plen, n, out=s_out)
         A.chksum_batch_csr(cbuf, coff, out=c_out, final=True)
         A.rx_verify(rbuf, dfoff, out=r_out)
-        A.tx_fill(tbuf, dfoff, out=t_out, workspace=ws)
+        A.tx_fill(tbuf, dfoff, out=t_out, workspace=ws, split=True)
 
     step()  # warm-up outside the capture (the library caches the device's CU count)
     torch.cuda.synchronize()
