@@ -87,8 +87,11 @@ class stdout_to_stderr:
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=5)
+    # Defaults sized for a fresh box: the first GPU-heavy second on a box runs ~3 % slow
+    # (config A: 241 vs 233 us per launch, profiles/r02/warmup/), so ~0.5 s of untimed
+    # launches come first, and 100 timed launches (~23 ms) average over transients.
+    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--warmup", type=int, default=2000)
     p.add_argument("--config", default="A", choices=sorted(CONFIGS))
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-reps", type=int, default=15,
