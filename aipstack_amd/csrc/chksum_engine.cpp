@@ -26,6 +26,7 @@
 #include <cstring>
 #include <mutex>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "aipstack_amd/chksum.h"
@@ -94,6 +95,32 @@ void release(aipstack_chksum_engine *e) {
     for (const Region &r : e->registered) (void)hipHostUnregister(const_cast<char *>(r.p));
 }
 
+// Pageable input into pinned staging: one core copies ~20 GB/s, below the PCIe link the
+// DMA then feeds, so large pieces are copied by several threads over disjoint 4 KiB-aligned
+// ranges (the previous piece's DMA runs meanwhile).
+void stage_copy(void *dst, const void *src, uint64_t bytes) {
+    constexpr uint64_t kPerThreadMin = 4ull << 20;
+    const unsigned hw = std::thread::hardware_concurrency();
+    const uint64_t want = bytes / kPerThreadMin;
+    const unsigned nt = (unsigned)std::min<uint64_t>(std::min<uint64_t>(want, 8), hw ? hw : 1);
+    if (nt <= 1) {
+        std::memcpy(dst, src, bytes);
+        return;
+    }
+    const uint64_t per = ((bytes + nt - 1) / nt + 4095) & ~4095ull;
+    std::vector<std::thread> pool;
+    pool.reserve(nt);
+    for (unsigned t = 0; t < nt; ++t) {
+        const uint64_t lo = (uint64_t)t * per;
+        if (lo >= bytes) break;
+        const uint64_t len = std::min(per, bytes - lo);
+        pool.emplace_back([=] {
+            std::memcpy(static_cast<char *>(dst) + lo, static_cast<const char *>(src) + lo, len);
+        });
+    }
+    for (std::thread &t : pool) t.join();
+}
+
 // Complete slot s: wait for it (blocking) or only if it is done (non-blocking: returns
 // 1 while it is still running), then hand its results to the caller. A HIP error is
 // recorded against the slot's ticket.
@@ -139,7 +166,7 @@ int enqueue(aipstack_chksum_engine *e, uint64_t n, uint16_t *h_out, Chunker chun
         const uint64_t cnt = i1 - i0;
         const void *h_src = src;
         if (bytes && !is_registered(e, src, bytes)) {  // pageable: CPU copy into pinned
-            std::memcpy(s.h_stage, src, bytes);
+            stage_copy(s.h_stage, src, bytes);
             h_src = s.h_stage;
         }
         if (bytes)
