@@ -513,6 +513,15 @@ extern "C" int aipstack_chksum_tune(const char *key, int value) {
     return AIPSTACK_CHKSUM_OK;
 }
 
+extern "C" int aipstack_chksum_launch_shape(uint64_t n, int cus, int csr,
+                                            uint32_t *chunk_packets, int *stream_windows) {
+    if (!chunk_packets || !stream_windows || cus <= 0) return AIPSTACK_CHKSUM_EINVAL;
+    const Shape sh = pick_shape(n, cus);
+    *chunk_packets = sh.chunk_packets;
+    *stream_windows = pick_stream_for(csr != 0, sh);
+    return AIPSTACK_CHKSUM_OK;
+}
+
 extern "C" int aipstack_chksum_batch_chain(const uint64_t *d_chunk_addr,
                                            const uint32_t *d_chunk_len,
                                            const uint64_t *d_chunk_index,

@@ -219,6 +219,14 @@ int aipstack_chksum_device_check(int device);
  * _OK or _EINVAL for an unknown key. */
 int aipstack_chksum_tune(const char *key, int value);
 
+/* The launch shape the batch entry points pick for n packets on a device with `cus` compute
+ * units (host-side query, no GPU needed; honours aipstack_chksum_tune): packets per wave
+ * chunk (64, or fewer for a small batch, so that it spreads over more waves) and stream
+ * windows in flight per wave, for the strided (csr = 0) or CSR (csr = 1) family.
+ * Returns _OK, or _EINVAL for null outputs or cus <= 0. */
+int aipstack_chksum_launch_shape(uint64_t n, int cus, int csr, uint32_t *chunk_packets,
+                                 int *stream_windows);
+
 /* ABI version of this header: bumped on any incompatible change. */
 #define AIPSTACK_CHKSUM_ABI_VERSION 1
 int aipstack_chksum_abi_version(void);

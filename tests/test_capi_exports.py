@@ -89,3 +89,38 @@ def test_python_batch_api_requires_device_tensors():
     import torch
     with pytest.raises(ValueError):
         A.chksum_batch_strided(torch.zeros(16, dtype=torch.uint8), 16, 16, 1)
+
+
+def test_launch_shape_small_and_large_batches():
+    """aipstack_chksum_launch_shape (host-side, no GPU): a batch that fills at least 16 waves
+    per CU at 64 packets per chunk keeps 64-packet chunks and the family's windows (2
+    strided, 8 CSR); smaller batches shrink the chunk to ~8 waves per CU and stream 8
+    windows."""
+    lib = _lib.load()
+    cp, w = ctypes.c_uint32(0), ctypes.c_int(0)
+
+    def shape(n, csr=0, cus=256):
+        assert lib.aipstack_chksum_launch_shape(n, cus, csr, ctypes.byref(cp), ctypes.byref(w)) == 0
+        return cp.value, w.value
+
+    assert shape(1 << 20) == (64, 2) and shape(1 << 20, csr=1) == (64, 8)
+    assert shape(262144) == (64, 2)          # 4096 chunks of 64 = 16 waves per CU
+    assert shape(4095 * 64) == (64, 8)       # one chunk fewer: small regime, 64-packet chunks
+    assert shape(65536) == (32, 8)           # ~8 waves per CU
+    assert shape(32768) == (16, 8)
+    assert shape(4096) == (2, 8)
+    assert shape(1) == (1, 8) and shape(0) == (1, 8)
+    assert shape(65536, cus=32) == (64, 2)   # a smaller device fills sooner
+    for n in (1, 100, 5000, 70000, 200000, 1 << 22):
+        c, _ = shape(n)
+        assert c in (1, 2, 4, 8, 16, 32, 64)
+    assert lib.aipstack_chksum_launch_shape(1, 0, 0, ctypes.byref(cp), ctypes.byref(w)) == \
+        A.AIPSTACK_CHKSUM_EINVAL
+    assert lib.aipstack_chksum_launch_shape(1, 256, 0, None, ctypes.byref(w)) == \
+        A.AIPSTACK_CHKSUM_EINVAL
+    # the tunable overrides the chunk size (and is restored)
+    assert lib.aipstack_chksum_tune(b"chunk_packets", 16) == 0
+    try:
+        assert shape(1 << 20)[0] == 16
+    finally:
+        assert lib.aipstack_chksum_tune(b"chunk_packets", 0) == 0
