@@ -255,7 +255,10 @@ def _torch():
 
 def _stream_handle(stream) -> int:
     torch = _torch()
-    if stream is None:
+    if stream is None:  # torch's current stream on the current device, as a raw handle
+        raw = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+        if raw is not None:  # skips building a Stream object per call (small batches)
+            return int(raw(torch.cuda.current_device()))
         stream = torch.cuda.current_stream()
     return int(stream.cuda_stream) if hasattr(stream, "cuda_stream") else int(stream)
 
