@@ -842,3 +842,81 @@ def test_batches_captured_in_a_graph_and_replayed(oracle):
         want_st = oracle.tx_fill_batch(tx, foff)
         assert np.array_equal(_np(t_out), want_st)
         assert np.array_equal(_np(tbuf), tx)
+
+
+# ---- batch shapes: every packets-per-chunk size on every kernel family ---------------------
+
+@pytest.fixture
+def chunk_packets():
+    """Yields a setter for the chunk-size tunable; restores automatic afterwards."""
+    yield lambda v: _tune("chunk_packets", v)
+    _tune("chunk_packets", 0)
+
+
+@pytest.mark.parametrize("cpk", [1, 2, 8, 32, 64])
+def test_every_chunk_size_on_every_kernel(oracle, chunk_packets, cpk):
+    """Forced packets per chunk (the small-batch shapes of DESIGN 6.7, and 64): strided
+    back-to-back and slotted, CSR, seeded CSR, chains, Rx verify and both Tx fills stay
+    bit-exact at a ragged count that leaves a partial last chunk."""
+    chunk_packets(cpk)
+    n = 3001
+    # strided, back to back (stream mode) and in 2 KiB slots (wave mode)
+    for stride in (1500, 2048):
+        host = synth.random_bytes(60 + stride, n * stride + 5)
+        d = _d(host)
+        got = _np(A.chksum_batch_strided(d, stride, 1500, n, byte_offset=5))
+        assert np.array_equal(got, oracle.batch_strided(host, stride, 1500, n, base_off=5))
+    # CSR and seeded CSR (config C's construction)
+    hbuf, off = synth.mixed_batch(n)
+    dbuf, doff = _d(hbuf), _d(off)
+    assert np.array_equal(_np(A.chksum_batch_csr(dbuf, doff, final=True)),
+                          oracle.batch_csr(hbuf, off, final=True))
+    states = np.random.default_rng(cpk).integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    got = _np(A.chksum_batch_seeded_csr(dbuf, doff, _d(states.view(np.int32))))
+    assert np.array_equal(got, oracle.batch_seeded_csr(hbuf, off, states))
+    # chains: header node + 1-2 payload pieces of one buffer, some empty chains
+    rng = np.random.default_rng(100 + cpk)
+    addrs, lens, idx, sts, want = [], [], [0], [], []
+    for i in range(n):
+        chunks = []
+        if i % 17 != 0:
+            for _ in range(int(rng.integers(1, 4))):
+                o = int(rng.integers(0, hbuf.size - 1600))
+                chunks.append((o, int(rng.integers(0, 1500))))
+        st = int(rng.integers(0, 2**32))
+        flat = np.concatenate([hbuf[o:o + l] for o, l in chunks] + [np.zeros(0, np.uint8)])
+        want.append(oracle.chain(st, flat, [(0, flat.size)] if flat.size else []))
+        for o, l in chunks:
+            if l:
+                addrs.append(dbuf.data_ptr() + o)
+                lens.append(l)
+        idx.append(len(addrs))
+        sts.append(st)
+    got = _np(A.chksum_batch_chain(_d(np.array(addrs, dtype=np.int64)),
+                                   _d(np.array(lens, dtype=np.int32)),
+                                   _d(np.array(idx, dtype=np.int64)),
+                                   _d(np.array(sts, dtype=np.uint32).view(np.int32)), final=True))
+    assert np.array_equal(got, np.array(want, dtype=np.uint16))
+    # frames: Rx verify on filled + corrupted frames, Tx fill both ways
+    fr, foff = synth.frames_host(n, seed=70 + cpk)
+    rx = fr.copy()
+    oracle.tx_fill_batch(rx, foff)
+    _corrupt(rx, foff, 0.2, cpk)
+    assert np.array_equal(_np(A.rx_verify(_d(rx), _d(foff))), oracle.rx_verify_batch(rx, foff))
+    for split in (False, True):
+        d = _d(fr)
+        st = _np(A.tx_fill(d, _d(foff), split=split))
+        want_fr = fr.copy()
+        assert np.array_equal(st, oracle.tx_fill_batch(want_fr, foff))
+        assert np.array_equal(_np(d), want_fr)
+
+
+@pytest.mark.parametrize("n", [1, 63, 65, 2047, 2049, 65535, 65537, 4095 * 64, 4096 * 64 + 1])
+def test_batch_sizes_at_shape_boundaries(oracle, n):
+    """Automatic shapes at the batch sizes where the chunk size or the regime changes
+    (256 CUs: 2048 / 65536 packets, 4096 chunks of 64), CSR and strided."""
+    hbuf, off = synth.mixed_batch(n)
+    assert np.array_equal(_np(A.chksum_batch_csr(_d(hbuf), _d(off))), oracle.batch_csr(hbuf, off))
+    host = synth.random_bytes(n, n * 1500)
+    assert np.array_equal(_np(A.chksum_batch_strided(_d(host), 1500, 1500, n)),
+                          oracle.batch_strided(host, 1500, 1500, n))
