@@ -24,6 +24,7 @@ from .chksum import (  # noqa: E402
     IpChksumAccumulator,
     IpChksumInverted,
     chksum_batch_chain,
+    chksum_chain_fill,
     chksum_batch_csr,
     chksum_batch_seeded_csr,
     chksum_batch_strided,
@@ -42,6 +43,6 @@ __all__ = [
     "AIPSTACK_CHKSUM_FINAL", "AIPSTACK_CHKSUM_MAX_LEN", "AIPSTACK_CHKSUM_OK", "ChksumEngine",
     "ChksumError",
     "IpBufNode", "IpBufRef", "IpChksum", "IpChksumAccumulator", "IpChksumInverted",
-    "chksum_batch_chain", "chksum_batch_csr", "chksum_batch_seeded_csr", "flatten_chains", "chksum_batch_strided", "device_check",
+    "chksum_batch_chain", "chksum_chain_fill", "chksum_batch_csr", "chksum_batch_seeded_csr", "flatten_chains", "chksum_batch_strided", "device_check",
     "ipBufProcessBytes", "LIB_PATH", "RX_VERDICTS", "rx_verify", "tx_fill",
 ]

@@ -29,6 +29,8 @@ SIGNATURES = {
     "aipstack_chksum_batch_csr": (_c_int, [_c_vp, _c_vp, _c_u64, _c_vp, _c_u32, _c_vp]),
     "aipstack_chksum_batch_seeded_csr": (_c_int, [_c_vp, _c_vp, _c_vp, _c_u64, _c_vp, _c_vp]),
     "aipstack_chksum_batch_chain": (_c_int, [_c_vp, _c_vp, _c_vp, _c_vp, _c_u64, _c_vp, _c_u32, _c_vp]),
+    "aipstack_chksum_batch_chain_fill": (_c_int, [_c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_u64, _c_vp,
+                                                  _c_u32, _c_vp]),
     "aipstack_chksum_rx_verify": (_c_int, [_c_vp, _c_vp, _c_u64, _c_vp, _c_vp]),
     "aipstack_chksum_tx_fill": (_c_int, [_c_vp, _c_vp, _c_u64, _c_vp, _c_vp]),
     "aipstack_chksum_tx_fill_workspace_bytes": (_c_u64, [_c_u64]),

@@ -34,6 +34,7 @@ AIPSTACK_CHKSUM_EINVAL = -1
 AIPSTACK_CHKSUM_EHIP = -2
 AIPSTACK_CHKSUM_ENODEV = -3
 AIPSTACK_CHKSUM_FINAL = 1
+AIPSTACK_CHKSUM_ZERO_AS_FFFF = 2
 AIPSTACK_CHKSUM_MAX_LEN = 65535
 
 
@@ -508,6 +509,40 @@ def chksum_batch_chain(chunk_addr, chunk_len, chunk_index, states=None, *, out=N
         chunk_addr.data_ptr(), chunk_len.data_ptr(), chunk_index.data_ptr(), sp or None, n,
         out.data_ptr(), AIPSTACK_CHKSUM_FINAL if final else 0, _stream_handle(stream))
     _check(st, "aipstack_chksum_batch_chain")
+    return out
+
+
+def chksum_chain_fill(chunk_addr, chunk_len, chunk_index, states, fields, *, out=None,
+                      zero_as_ffff: bool = False, stream=None):
+    """The Tx form of :func:`chksum_batch_chain`: chain i's final checksum
+    (``IpChksumAccumulator(State(states[i])).getChksum(chain i)``) is stored big-endian at
+    DEVICE address ``fields[i]`` (int64 tensor; 0 = no store) -- the checksum field of the
+    header the chain starts with, which must read 0 when the batch runs, as the reference
+    sets it before summing (tcp/IpTcpProto_output.h:1251-1277, udp/IpUdpProto.h:164-179).
+    ``zero_as_ffff`` sends a computed 0 as 0xFFFF (UDP). Returns the checksums (``out``)."""
+    for t, name in ((chunk_addr, "chunk_addr"), (chunk_len, "chunk_len"),
+                    (chunk_index, "chunk_index"), (fields, "fields")):
+        _require_device(t, name)
+    if chunk_addr.element_size() != 8 or chunk_len.element_size() != 4 \
+            or chunk_index.element_size() != 8 or fields.element_size() != 8:
+        raise ValueError("chunk_addr/chunk_index/fields must be 64-bit, chunk_len 32-bit")
+    n = chunk_index.numel() - 1
+    if n < 0:
+        raise ValueError("chunk_index must hold n+1 entries")
+    if fields.numel() < n:
+        raise ValueError("fields must hold n entries")
+    sp = 0
+    if states is not None:
+        _require_device(states, "states")
+        if states.numel() < n or states.element_size() != 4:
+            raise ValueError("states must hold n 32-bit entries")
+        sp = states.data_ptr()
+    out = _out_tensor(out, n, chunk_index)
+    st = _lib.load().aipstack_chksum_batch_chain_fill(
+        chunk_addr.data_ptr(), chunk_len.data_ptr(), chunk_index.data_ptr(), sp or None,
+        fields.data_ptr(), n, out.data_ptr(), AIPSTACK_CHKSUM_ZERO_AS_FFFF if zero_as_ffff else 0,
+        _stream_handle(stream))
+    _check(st, "aipstack_chksum_batch_chain_fill")
     return out
 
 

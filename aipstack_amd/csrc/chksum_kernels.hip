@@ -138,6 +138,24 @@ __global__ __launch_bounds__(kBlock) void chksum_batch_kernel(Desc desc, uint64_
 // accumulator, exact for any number of chunks per chain.
 // ---------------------------------------------------------------------------------
 
+// A 16-bit store at any byte address (one global_store_short: gfx9 runs in unaligned mode).
+typedef uint16_t u16_any_align __attribute__((aligned(1)));
+
+// Second pass of the chain fill: chain i's checksum (from the chained batch's output) stored
+// big-endian into its header field, one chain per thread, after every chain has been read
+// (no field store can race a read of the same chain). CHAIN bench shape, 1 M chains: 13.5 us
+// here, but the chain kernel of the next launch then runs ~37 us longer (the partially
+// written lines go back to HBM under its stream): 299 us per fill against 298 with the
+// stores inside the chain kernel and 248 for the chained batch alone.
+__global__ __launch_bounds__(kBlock) void chain_field_scatter_kernel(
+    const uint64_t *__restrict__ fields, const uint16_t *__restrict__ sums, uint64_t n) {
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        const uint64_t fa = fields[i];
+        if (fa) *reinterpret_cast<u16_any_align *>(fa) = (uint16_t)bswap16(sums[i]);
+    }
+}
+
 __device__ __forceinline__ uint32_t parity_below(uint64_t mask, uint32_t s) {  // s in 0..64
     const uint64_t below = s == 0 ? 0ull : (~0ull >> (64u - s));
     return (uint32_t)__builtin_popcountll(mask & below) & 1u;
@@ -237,6 +255,8 @@ __global__ __launch_bounds__(kBlock, 5) void chksum_chain_kernel(
         const uint64_t t = (uint64_t)state + fold16(s32);
         uint32_t r = fold16((uint32_t)t + (uint32_t)(t >> 32));
         r = final_flag ? (~r & 0xFFFFu) : r;
+        if ((flags & AIPSTACK_CHKSUM_ZERO_AS_FFFF) && r == 0)  // udp/IpUdpProto.h:176-178
+            r = 0xFFFFu;
         if (lane < cnt)
             out[p0 + lane] = (uint16_t)r;
     }
@@ -421,8 +441,8 @@ int launch(const Desc &desc, uint64_t n, uint32_t max_len, uint16_t *d_out, uint
 
 template <bool NT, int SU>
 int launch_chain(const uint64_t *d_addr, const uint32_t *d_len, const uint64_t *d_index,
-                 const uint32_t *d_states, uint64_t n, uint16_t *d_out, uint32_t flags,
-                 hipStream_t stream) {
+                 const uint32_t *d_states, const uint64_t *d_fields, uint64_t n,
+                 uint16_t *d_out, uint32_t flags, hipStream_t stream) {
     const int cus = device_cu_count();
     if (cus <= 0) return AIPSTACK_CHKSUM_EHIP;
     const uint32_t cpg = pick_shape(n, cus).chunk_packets;  // chains per group
@@ -436,6 +456,13 @@ int launch_chain(const uint64_t *d_addr, const uint32_t *d_len, const uint64_t *
     hipLaunchKernelGGL((chksum_chain_kernel<NT, SU>), dim3((unsigned)blocks), dim3(kBlock), 0,
                        stream, d_addr, d_len, d_index, d_states, n, (uint32_t)cpw, cpg, d_out,
                        flags);
+    if (d_fields) {  // chain fill: the field stores as a pass of their own
+        const int st = check_hip(hipGetLastError());
+        if (st != AIPSTACK_CHKSUM_OK) return st;
+        const uint64_t sblocks = min((n + kBlock - 1) / kBlock, (uint64_t)cus * 64);
+        hipLaunchKernelGGL(chain_field_scatter_kernel, dim3((unsigned)sblocks), dim3(kBlock), 0,
+                           stream, d_fields, d_out, n);
+    }
     return check_hip(hipGetLastError());
 }
 
@@ -522,6 +549,25 @@ extern "C" int aipstack_chksum_launch_shape(uint64_t n, int cus, int csr,
     return AIPSTACK_CHKSUM_OK;
 }
 
+namespace {
+int chain_batch(const uint64_t *d_chunk_addr, const uint32_t *d_chunk_len,
+                const uint64_t *d_chunk_index, const uint32_t *d_states,
+                const uint64_t *d_fields, uint64_t n, uint16_t *d_out, uint32_t flags,
+                void *stream) {
+    // SU: gathered-stream windows per group ("stream" tunable: 2 or 4; off and 8 map to
+    // 2 -- every chunk goes through the gathered stream, and 8 windows spill registers).
+    // Measured on CHAIN (profiles/r02/bench_CHAIN_cleaned_sweep.jsonl): 2 windows, 73 VGPRs,
+    // 6 waves per SIMD, 286-291 us; 4 windows, 96 VGPRs, 5 waves, 300-302 us.
+#define AIPSTACK_LAUNCH_CHAIN(NT, SU)                                                       \
+    return launch_chain<NT, SU>(d_chunk_addr, d_chunk_len, d_chunk_index, d_states, d_fields, \
+                                n, d_out, flags, (hipStream_t)stream)
+    if (!tuning().nontemporal.load(std::memory_order_relaxed)) AIPSTACK_LAUNCH_CHAIN(false, 2);
+    if (tuning_stream_windows(2) == 4) AIPSTACK_LAUNCH_CHAIN(true, 4);
+    AIPSTACK_LAUNCH_CHAIN(true, 2);
+#undef AIPSTACK_LAUNCH_CHAIN
+}
+}  // namespace
+
 extern "C" int aipstack_chksum_batch_chain(const uint64_t *d_chunk_addr,
                                            const uint32_t *d_chunk_len,
                                            const uint64_t *d_chunk_index,
@@ -530,15 +576,21 @@ extern "C" int aipstack_chksum_batch_chain(const uint64_t *d_chunk_addr,
     if (n == 0) return AIPSTACK_CHKSUM_OK;
     if (!d_chunk_addr || !d_chunk_len || !d_chunk_index || !d_out) return AIPSTACK_CHKSUM_EINVAL;
     if (n > (1ull << 40)) return AIPSTACK_CHKSUM_EINVAL;
-    // SU: gathered-stream windows per group ("stream" tunable: 2 or 4; off and 8 map to
-    // 2 -- every chunk goes through the gathered stream, and 8 windows spill registers).
-    // Measured on CHAIN (profiles/r02/bench_CHAIN_cleaned_sweep.jsonl): 2 windows, 73 VGPRs,
-    // 6 waves per SIMD, 286-291 us; 4 windows, 96 VGPRs, 5 waves, 300-302 us.
-#define AIPSTACK_LAUNCH_CHAIN(NT, SU)                                                       \
-    return launch_chain<NT, SU>(d_chunk_addr, d_chunk_len, d_chunk_index, d_states, n,     \
-                                d_out, flags, (hipStream_t)stream)
-    if (!tuning().nontemporal.load(std::memory_order_relaxed)) AIPSTACK_LAUNCH_CHAIN(false, 2);
-    if (tuning_stream_windows(2) == 4) AIPSTACK_LAUNCH_CHAIN(true, 4);
-    AIPSTACK_LAUNCH_CHAIN(true, 2);
-#undef AIPSTACK_LAUNCH_CHAIN
+    return chain_batch(d_chunk_addr, d_chunk_len, d_chunk_index, d_states, nullptr, n, d_out,
+                       flags & AIPSTACK_CHKSUM_FINAL, stream);
+}
+
+extern "C" int aipstack_chksum_batch_chain_fill(const uint64_t *d_chunk_addr,
+                                                const uint32_t *d_chunk_len,
+                                                const uint64_t *d_chunk_index,
+                                                const uint32_t *d_states,
+                                                const uint64_t *d_field_addr, uint64_t n,
+                                                uint16_t *d_out, uint32_t flags, void *stream) {
+    if (n == 0) return AIPSTACK_CHKSUM_OK;
+    if (!d_chunk_addr || !d_chunk_len || !d_chunk_index || !d_field_addr || !d_out)
+        return AIPSTACK_CHKSUM_EINVAL;
+    if (n > (1ull << 40)) return AIPSTACK_CHKSUM_EINVAL;
+    return chain_batch(d_chunk_addr, d_chunk_len, d_chunk_index, d_states, d_field_addr, n,
+                       d_out, AIPSTACK_CHKSUM_FINAL | (flags & AIPSTACK_CHKSUM_ZERO_AS_FFFF),
+                       stream);
 }

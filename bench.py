@@ -104,6 +104,9 @@ def parse():
                         "(host-memory streaming engine; PCIe-inclusive). Prints its own line.")
     p.add_argument("--e2e-pageable", action="store_true",
                    help="with --e2e: do not page-lock the host batch (CPU copy to staging)")
+    p.add_argument("--chain-fill", action="store_true",
+                   help="CHAIN: the Tx form (aipstack_chksum_batch_chain_fill): each chain's "
+                        "checksum is also stored big-endian into its 20-B header node")
     p.add_argument("--tx-inplace", action="store_true",
                    help="TX: the one-pass in-place fill (default: the two-pass split fill)")
     p.add_argument("--small", type=int, default=0, metavar="N",
@@ -216,8 +219,37 @@ def make_chains(spec, dev):
         "len": torch.from_numpy(lens.view(np.int32)).to(dev),
         "index": torch.from_numpy(index.view(np.int64)).to(dev),
         "states": torch.from_numpy(states.view(np.int32)).to(dev),
+        # --chain-fill: each header's TCP checksum field (offset 16 of the 20-B node)
+        "fields": torch.from_numpy((addr[0::3] + np.uint64(16)).view(np.int64)).to(dev),
         "payload": (CHAIN_HDR + CHAIN_PAYLOAD) * n,
     }
+
+
+def chain_fill_check(chain):
+    """--chain-fill: the timed launches kept refilling the fields, so zero them again, take
+    the oracle's checksums over that state, fill once and compare both the returned values
+    and every header's stored field (big-endian at header + 16)."""
+    import aipstack_amd as A
+    hdr = chain["buf"][:CHAIN_HDR_STRIDE * chain["n"]].view(-1, CHAIN_HDR_STRIDE)
+    hdr[:, 16:18] = 0
+    host = chain["buf"].cpu().numpy()
+    want = chain_oracle(chain, host)
+    got = A.chksum_chain_fill(chain["addr"], chain["len"], chain["index"], chain["states"],
+                              chain["fields"]).cpu().numpy()
+    fld = hdr[:, 16:18].cpu().numpy().astype(np.uint16)
+    ok = np.array_equal(got, want) and np.array_equal((fld[:, 0] << 8) | fld[:, 1], want)
+    return "bit-exact (every chain and stored field vs oracle)" if ok else "MISMATCH"
+
+
+def chain_oracle(chain, host):
+    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "libchksum_oracle.so"))
+    lib.oracle_batch_chain.argtypes = [ctypes.c_void_p, ctypes.c_uint64] + \
+        [ctypes.c_void_p] * 4 + [ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32]
+    want = np.empty(chain["n"], dtype=np.uint16)
+    lib.oracle_batch_chain(host.ctypes.data, chain["base"], chain["addr_host"].ctypes.data,
+                           chain["len_host"].ctypes.data, chain["index_host"].ctypes.data,
+                           chain["states_host"].ctypes.data, chain["n"], want.ctypes.data, 1)
+    return want
 
 
 def chain_check(chain, got):
@@ -498,6 +530,9 @@ def main():
             A.chksum_batch_csr(buf, d_off, out=out, stream=stream)
         elif layout == "rx":
             A.rx_verify(buf, d_off, out=status, stream=stream)
+        elif layout == "chain" and args.chain_fill:
+            A.chksum_chain_fill(chain["addr"], chain["len"], chain["index"], chain["states"],
+                                chain["fields"], out=out, stream=stream)
         elif layout == "chain":
             A.chksum_batch_chain(chain["addr"], chain["len"], chain["index"], chain["states"],
                                  out=out, final=True, stream=stream)
@@ -555,6 +590,8 @@ def main():
 
     payload = spec.get("payload", total)
     alg = algorithmic_bytes(layout, n, payload)
+    if layout == "chain" and args.chain_fill:
+        alg += 10 * n  # + the field address read and the 2-byte field written per chain
 
     # ---- parity of this run's output against the oracle / reference (rank 0 sample)
     parity = None
@@ -566,7 +603,8 @@ def main():
             cpu = cpu_baseline_frames(spec, frames_host)
     elif rank == 0 and layout == "chain":
         if not args.no_parity:
-            parity = chain_check(chain, out.cpu().numpy())
+            parity = (chain_fill_check(chain) if args.chain_fill
+                      else chain_check(chain, out.cpu().numpy()))
         if not args.no_cpu_baseline:
             cpu = cpu_baseline_chain(chain)
     elif rank == 0:
@@ -609,6 +647,8 @@ def main():
             "parallelism": f"disjoint packet shards x{world}, no collective",
             **({"tx_fill": "in-place, one pass" if args.tx_inplace else
                 "split: read pass + scatter pass (both timed)"} if layout == "tx" else {}),
+            **({"chain_fill": "checksum also stored big-endian into each header node"}
+               if layout == "chain" and args.chain_fill else {}),
         },
         "roofline": {
             "bound": "hbm",

@@ -220,6 +220,19 @@ struct BatchChksum {
             reinterpret_cast<std::uint32_t const *>(d_states), n, d_out,
             final_chksum ? AIPSTACK_CHKSUM_FINAL : 0u, stream);
     }
+    // The Tx form: chain i's final checksum stored big-endian at d_field_addr[i] (the field
+    // reading 0, as the reference sets it before summing); zeroAsFfff for UDP.
+    static int chainFill(std::uint64_t const *d_chunk_addr, std::uint32_t const *d_chunk_len,
+                         std::uint64_t const *d_chunk_index,
+                         IpChksumAccumulator::State const *d_states,
+                         std::uint64_t const *d_field_addr, std::uint64_t n,
+                         std::uint16_t *d_out, bool zeroAsFfff = false,
+                         void *stream = nullptr) {
+        return aipstack_chksum_batch_chain_fill(
+            d_chunk_addr, d_chunk_len, d_chunk_index,
+            reinterpret_cast<std::uint32_t const *>(d_states), d_field_addr, n, d_out,
+            zeroAsFfff ? AIPSTACK_CHKSUM_ZERO_AS_FFFF : 0u, stream);
+    }
     // Raw Ethernet frames at CSR offsets: receive verdicts / send-side fill (AIPSTACK_RX_*).
     static int rxVerify(void const *d_frames, std::uint64_t const *d_offsets, std::uint64_t n,
                         std::uint8_t *d_verdict, void *stream = nullptr) {

@@ -97,6 +97,23 @@ int aipstack_chksum_batch_chain(const uint64_t *d_chunk_addr, const uint32_t *d_
                                 const uint64_t *d_chunk_index, const uint32_t *d_states,
                                 uint64_t n, uint16_t *d_out, uint32_t flags, void *stream);
 
+/* Flag of aipstack_chksum_batch_chain_fill: a computed checksum of 0 is sent as 0xFFFF
+ * (UDP, reference udp/IpUdpProto.h:176-178). */
+#define AIPSTACK_CHKSUM_ZERO_AS_FFFF 2u
+
+/* The send side of the chained batch: the reference's Tx call sites sum a pseudo-header
+ * State, the header node and the payload chunks, then write the checksum into the header
+ * (tcp/IpTcpProto_output.h:1251-1277, udp/IpUdpProto.h:164-179, ip/IpStack.h:1184).
+ * Computes the FINAL checksum of chain i into d_out[i] as aipstack_chksum_batch_chain does,
+ * then (a second, stream-ordered pass) stores it big-endian at DEVICE address
+ * d_field_addr[i] (any alignment; 0 = no store). As in the reference, the field's two bytes
+ * must read 0 when the batch runs (they are summed), and no field may lie inside another
+ * chain's bytes. Flags: AIPSTACK_CHKSUM_ZERO_AS_FFFF. */
+int aipstack_chksum_batch_chain_fill(const uint64_t *d_chunk_addr, const uint32_t *d_chunk_len,
+                                     const uint64_t *d_chunk_index, const uint32_t *d_states,
+                                     const uint64_t *d_field_addr, uint64_t n,
+                                     uint16_t *d_out, uint32_t flags, void *stream);
+
 /* ---- frame-level batches: Rx verify / Tx fill on raw Ethernet frames ------------------ */
 
 /* Per-frame verdicts of aipstack_chksum_rx_verify (and statuses of _tx_fill), restating the

@@ -53,6 +53,15 @@ int main() {
     CHECK(aipstack_chksum_batch_chain(addrs, nullptr, off, states, 1, out, 0, nullptr) == EINVAL_);
     CHECK(aipstack_chksum_batch_chain(addrs, lens, nullptr, states, 1, out, 0, nullptr) == EINVAL_);
     CHECK(aipstack_chksum_batch_chain(addrs, lens, off, states, 1, nullptr, 0, nullptr) == EINVAL_);
+    // chain fill: the field table and d_out are required; n == 0 is a no-op
+    CHECK(aipstack_chksum_batch_chain_fill(nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr, 0,
+                                           nullptr) == 0);
+    CHECK(aipstack_chksum_batch_chain_fill(addrs, lens, off, states, nullptr, 1, out, 0, nullptr) ==
+          EINVAL_);
+    CHECK(aipstack_chksum_batch_chain_fill(nullptr, lens, off, states, off, 1, out, 0, nullptr) ==
+          EINVAL_);
+    CHECK(aipstack_chksum_batch_chain_fill(addrs, lens, off, states, off, 1, nullptr, 0, nullptr) ==
+          EINVAL_);
     CHECK(aipstack_chksum_rx_verify(dummy, off, 1, nullptr, nullptr) == EINVAL_);
     CHECK(aipstack_chksum_tx_fill(dummy, nullptr, 1, st, nullptr) == EINVAL_);
     // split fill: workspace missing, too small, misaligned

@@ -920,3 +920,78 @@ def test_batch_sizes_at_shape_boundaries(oracle, n):
     host = synth.random_bytes(n, n * 1500)
     assert np.array_equal(_np(A.chksum_batch_strided(_d(host), 1500, 1500, n)),
                           oracle.batch_strided(host, 1500, 1500, n))
+
+
+# ---- chain fill: the Tx call sites' checksum written into the header node ------------------
+
+def test_chain_fill_tcp_tx_shape(oracle):
+    """tcp/IpTcpProto_output.h:1251-1277: pseudo-header State + 20-60 B TCP header node (its
+    checksum field at offset 16 reading 0) + 1-2 send-ring chunks; chain_fill stores each
+    checksum big-endian into its header and returns the same values as the chained batch."""
+    import torch
+    rng = np.random.default_rng(77)
+    n = 50000
+    ring = rng.integers(0, 256, size=1 << 21, dtype=np.uint8)
+    hdrs = rng.integers(0, 256, size=n * 64, dtype=np.uint8)
+    hl = 20 + 4 * rng.integers(0, 11, n)
+    for i in range(n):
+        hdrs[64 * i + 16: 64 * i + 18] = 0            # the checksum field reads 0
+    dring, dh = _d(ring), _d(hdrs)
+    addrs, lens, idx, states, fields = [], [], [0], [], []
+    for i in range(n):
+        addrs.append(dh.data_ptr() + 64 * i)
+        lens.append(int(hl[i]))
+        seg = int(rng.integers(0, 1461))
+        start = int(rng.integers(0, ring.size))
+        first = min(seg, ring.size - start)
+        if first:
+            addrs.append(dring.data_ptr() + start)
+            lens.append(first)
+        if seg > first:
+            addrs.append(dring.data_ptr())
+            lens.append(seg - first)
+        idx.append(len(addrs))
+        states.append(int(rng.integers(0, 2**20)))
+        fields.append(dh.data_ptr() + 64 * i + 16)
+    args = (_d(np.array(addrs, dtype=np.int64)), _d(np.array(lens, dtype=np.int32)),
+            _d(np.array(idx, dtype=np.int64)), _d(np.array(states, dtype=np.int32)))
+    want = _np(A.chksum_batch_chain(*args, final=True))
+    got = _np(A.chksum_chain_fill(*args, _d(np.array(fields, dtype=np.int64))))
+    torch.cuda.synchronize()
+    assert np.array_equal(got, want)
+    filled = _np(dh)
+    expect = hdrs.copy()
+    for i in range(n):
+        expect[64 * i + 16] = want[i] >> 8
+        expect[64 * i + 17] = want[i] & 0xFF
+    assert np.array_equal(filled, expect)
+    # and the filled header now verifies: the chain sums to 0xFFFF, IpChksum == 0
+    again = _np(A.chksum_batch_chain(*args, final=True))
+    assert np.all(again == 0)
+
+
+def test_chain_fill_udp_zero_as_ffff_and_skipped_fields():
+    """udp/IpUdpProto.h:176-178: a computed 0 goes out as 0xFFFF (flag), else as 0; a field
+    address of 0 stores nothing; odd field addresses."""
+    import torch
+    n = 64
+    buf = torch.zeros(4096, dtype=torch.uint8, device=DEV)
+    base = buf.data_ptr()
+    # chain i: 8 zero bytes at 33 + 40 i (a UDP header, checksum field at +6) with state
+    # 0xFFFF -> sum 0xFFFF -> final checksum 0
+    addr = torch.tensor([base + 33 + 40 * i for i in range(n)], dtype=torch.int64, device=DEV)
+    ln = torch.full((n,), 8, dtype=torch.int32, device=DEV)
+    idx = torch.arange(n + 1, dtype=torch.int64, device=DEV)
+    st = torch.full((n,), 0xFFFF, dtype=torch.int32, device=DEV)
+    fields = torch.tensor([base + 33 + 40 * i + 6 if i % 5 else 0 for i in range(n)],
+                          dtype=torch.int64, device=DEV)
+    out = _np(A.chksum_chain_fill(addr, ln, idx, st, fields))
+    assert np.all(out == 0)
+    assert int(buf.sum().item()) == 0  # 0 written as 0x0000
+    out = _np(A.chksum_chain_fill(addr, ln, idx, st, fields, zero_as_ffff=True))
+    torch.cuda.synchronize()
+    assert np.all(out == 0xFFFF)
+    h = _np(buf)
+    for i in range(n):
+        f = 33 + 40 * i + 6
+        assert (h[f], h[f + 1]) == ((0xFF, 0xFF) if i % 5 else (0, 0)), i
