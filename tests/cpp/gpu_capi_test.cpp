@@ -165,6 +165,72 @@ int main() {
         HIP_OK(hipFree(dws));
     }
 
+    // ---- chains (header node + 1-2 payload pieces) and the chain fill: each checksum stored
+    // big-endian into its header's field (offset 16, zeroed first, as the reference does)
+    {
+        const uint64_t nc = 20000, hdr0 = 1000, pay0 = 4u << 20;
+        for (uint64_t i = 0; i < nc; i++) {
+            h[hdr0 + 32 * i + 16] = 0;
+            h[hdr0 + 32 * i + 17] = 0;
+        }
+        HIP_OK(hipMemcpy(d, h.data(), h.size(), hipMemcpyHostToDevice));
+        std::vector<uint64_t> caddr, cidx{0}, fields(nc);
+        std::vector<uint32_t> clen, cst(nc);
+        for (uint64_t i = 0; i < nc; i++) {
+            caddr.push_back((uint64_t)(uintptr_t)d + hdr0 + 32 * i);
+            clen.push_back(20);
+            const uint64_t start = pay0 + rng() % (64u << 20);
+            const uint32_t l1 = (uint32_t)(rng() % 1461), l2 = (uint32_t)(rng() % 3 ? 0 : rng() % 900);
+            if (l1) { caddr.push_back((uint64_t)(uintptr_t)d + start); clen.push_back(l1); }
+            if (l2) { caddr.push_back((uint64_t)(uintptr_t)d + start + 5000); clen.push_back(l2); }
+            cidx.push_back(caddr.size());
+            cst[i] = (uint32_t)rng();
+            fields[i] = (uint64_t)(uintptr_t)d + hdr0 + 32 * i + 16;
+        }
+        uint64_t *dca = nullptr, *dci = nullptr, *dfl = nullptr;
+        uint32_t *dcl = nullptr, *dcs = nullptr;
+        HIP_OK(hipMalloc(&dca, caddr.size() * 8));
+        HIP_OK(hipMalloc(&dcl, clen.size() * 4));
+        HIP_OK(hipMalloc(&dci, cidx.size() * 8));
+        HIP_OK(hipMalloc(&dcs, nc * 4));
+        HIP_OK(hipMalloc(&dfl, nc * 8));
+        HIP_OK(hipMemcpy(dca, caddr.data(), caddr.size() * 8, hipMemcpyHostToDevice));
+        HIP_OK(hipMemcpy(dcl, clen.data(), clen.size() * 4, hipMemcpyHostToDevice));
+        HIP_OK(hipMemcpy(dci, cidx.data(), cidx.size() * 8, hipMemcpyHostToDevice));
+        HIP_OK(hipMemcpy(dcs, cst.data(), nc * 4, hipMemcpyHostToDevice));
+        HIP_OK(hipMemcpy(dfl, fields.data(), nc * 8, hipMemcpyHostToDevice));
+        std::vector<uint16_t> cwant(nc), cgot(nc);
+        oracle_batch_chain(h.data(), (uint64_t)(uintptr_t)d, caddr.data(), clen.data(), cidx.data(),
+                           cst.data(), nc, cwant.data(), 1);
+        st = aipstack_chksum_batch_chain(dca, dcl, dci, dcs, nc, dout, AIPSTACK_CHKSUM_FINAL, stream);
+        EXPECT(st == 0, "chain launch failed %d", st);
+        HIP_OK(hipMemcpyAsync(cgot.data(), dout, nc * 2, hipMemcpyDeviceToHost, stream));
+        HIP_OK(hipStreamSynchronize(stream));
+        EXPECT(cgot == cwant, "chain: checksums differ from the oracle");
+        HIP_OK(hipMemsetAsync(dout, 0, nc * 2, stream));
+        st = aipstack_chksum_batch_chain_fill(dca, dcl, dci, dcs, dfl, nc, dout, 0, stream);
+        EXPECT(st == 0, "chain fill launch failed %d", st);
+        std::vector<unsigned char> hdrs(32 * nc);
+        HIP_OK(hipMemcpyAsync(cgot.data(), dout, nc * 2, hipMemcpyDeviceToHost, stream));
+        HIP_OK(hipMemcpyAsync(hdrs.data(), d + hdr0, 32 * nc, hipMemcpyDeviceToHost, stream));
+        HIP_OK(hipStreamSynchronize(stream));
+        EXPECT(cgot == cwant, "chain fill: checksums differ from the oracle");
+        for (uint64_t i = 0; i < nc; i++) {
+            const unsigned hi = hdrs[32 * i + 16], lo = hdrs[32 * i + 17];
+            EXPECT(((hi << 8) | lo) == cwant[i], "chain fill: field %lu holds %02x%02x, want %04x",
+                   (unsigned long)i, hi, lo, cwant[i]);
+            EXPECT(std::memcmp(&hdrs[32 * i], &h[hdr0 + 32 * i], 16) == 0 &&
+                       std::memcmp(&hdrs[32 * i + 18], &h[hdr0 + 32 * i + 18], 14) == 0,
+                   "chain fill: header %lu changed outside its field", (unsigned long)i);
+        }
+        HIP_OK(hipMemcpy(d, h.data(), h.size(), hipMemcpyHostToDevice));  // restore
+        HIP_OK(hipFree(dca));
+        HIP_OK(hipFree(dcl));
+        HIP_OK(hipFree(dci));
+        HIP_OK(hipFree(dcs));
+        HIP_OK(hipFree(dfl));
+    }
+
     // ---- argument errors are reported, not executed
     EXPECT(aipstack_chksum_batch_strided(nullptr, 1, 1, 1, dout, 0, stream) == AIPSTACK_CHKSUM_EINVAL, "null base");
     EXPECT(aipstack_chksum_batch_strided(d, 1, 65536, 1, dout, 0, stream) == AIPSTACK_CHKSUM_EINVAL, "len > 65535");
