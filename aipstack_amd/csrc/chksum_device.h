@@ -849,7 +849,7 @@ __device__ __forceinline__ uint32_t sum_gathered_chunks(uint64_t a, uint32_t l, 
     // this lane's boundary: G at segment cs (an empty chunk's cs is the next one's)
     const uint32_t bwin = cs >> 6;
     const int bsrc = (int)((cs & 63u) << 2);
-    uint32_t g = 0, carry = 0;  // carry: prefix at the current window's start, mod 2^32
+    uint32_t gsum = 0, carry = 0;  // carry: prefix at the current window's start, mod 2^32
     auto consume = [&](uint32_t w, const u32x4 (&v)[U], const uint32_t (&keep)[U]) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -863,24 +863,36 @@ __device__ __forceinline__ uint32_t sum_gathered_chunks(uint64_t a, uint32_t l, 
             const uint32_t incl = wave_incl_scan(s);
             if (__builtin_amdgcn_ballot_w64(bwin == wu)) {
                 const uint32_t part = (uint32_t)__builtin_amdgcn_ds_bpermute(bsrc, (int)(incl - s));
-                if (bwin == wu) g = carry + part;
+                if (bwin == wu) gsum = carry + part;
             }
             carry += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
         }
     };
     u32x4 va[U], vb[U];
     uint32_t ka[U], kb[U];
+    // Groups of U windows, double-buffered: group g+1's loads go out before group g is
+    // consumed. The loop runs while at least three groups remain, so both of its issues are
+    // needed and unconditional (counted waits across the back edge); the last one or two
+    // groups are finished straight-line, issuing nothing past the stream.
+    const uint32_t groups = (nwin + U - 1u) / U;
     ld.issue(0, va, ka);
-    const uint32_t npairs = (nwin + 2u * U - 1u) / (2u * U);
-    for (uint32_t i = 0, w = 0; i < npairs; ++i, w += 2u * U) {
-        ld.issue(w + U, vb, kb);
-        consume(w, va, ka);
-        ld.issue(w + 2u * U, va, ka);
-        consume(w + U, vb, kb);
+    uint32_t g = 0;
+    for (; g + 2u < groups; g += 2u) {
+        ld.issue((g + 1u) * U, vb, kb);
+        consume(g * U, va, ka);
+        ld.issue((g + 2u) * U, va, ka);
+        consume((g + 1u) * U, vb, kb);
     }
-    if (bwin >= nwin) g = carry;  // cs == T on a multiple of 64: past the last window
+    if (g + 2u == groups) {
+        ld.issue((g + 1u) * U, vb, kb);
+        consume(g * U, va, ka);
+        consume((g + 1u) * U, vb, kb);
+    } else {
+        consume(g * U, va, ka);
+    }
+    if (bwin >= nwin) gsum = carry;  // cs == T on a multiple of 64: past the last window
     // chunk j ends where chunk j + 1 starts (lane 63: at T, prefix = the final carry)
-    return from_next_lane(g, carry, lane) - g;
+    return from_next_lane(gsum, carry, lane) - gsum;
 }
 
 // Stream mode for one chunk (stream_ok). Lane j < cnt holds packet j = [S, E); returns
