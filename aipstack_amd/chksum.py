@@ -396,14 +396,15 @@ class ChksumEngine:
         self._registered = [a for a in self._registered if a is not arr]
 
     @staticmethod
-    def _host_args(buf: np.ndarray, out, n: int) -> np.ndarray:
+    def _host_args(buf: np.ndarray, out, n: int, dtype=np.uint16) -> np.ndarray:
         if not isinstance(buf, np.ndarray) or not buf.flags.c_contiguous:
             raise ValueError("buf must be a C-contiguous numpy array")
         if out is None:
-            return np.empty(max(n, 0), dtype=np.uint16)
-        if (not isinstance(out, np.ndarray) or out.dtype != np.uint16
+            return np.empty(max(n, 0), dtype=dtype)
+        if (not isinstance(out, np.ndarray) or out.dtype != dtype
                 or not out.flags.c_contiguous or not out.flags.writeable or out.size < n):
-            raise ValueError("out must be a writable C-contiguous uint16 array of >= n elements")
+            raise ValueError(f"out must be a writable C-contiguous {np.dtype(dtype).name} array "
+                             "of >= n elements")
         return out
 
     def strided(self, buf: np.ndarray, stride: int, length: int, n: int, *, out=None,
@@ -468,6 +469,35 @@ class ChksumEngine:
         st = self._lib.aipstack_chksum_engine_wait(self._h, ticket)
         self._inflight.pop(ticket, None)
         _check(st, "aipstack_chksum_engine_wait")
+
+    def rx_verify(self, frames: np.ndarray, offsets: np.ndarray, *, out=None) -> np.ndarray:
+        """Rx verify of raw Ethernet frames in HOST memory (frame i =
+        ``frames[offsets[i]:offsets[i+1]]``): one AIPSTACK_RX_* verdict per frame (uint8),
+        as :func:`rx_verify` on the device."""
+        o = np.ascontiguousarray(offsets, dtype=np.uint64)
+        n = o.size - 1
+        if n > 0 and int(o[-1]) > frames.nbytes:
+            raise ValueError("offsets exceed frames")
+        out = self._host_args(frames, out, n, np.uint8)
+        _check(self._lib.aipstack_chksum_engine_host_rx_verify(
+            self._h, frames.ctypes.data, o.ctypes.data, max(n, 0), out.ctypes.data),
+            "aipstack_chksum_engine_host_rx_verify")
+        return out
+
+    def submit_rx_verify(self, frames: np.ndarray, offsets: np.ndarray, *, out=None):
+        """Enqueue an Rx verify batch; returns (ticket, out) (see submit_strided)."""
+        o = np.ascontiguousarray(offsets, dtype=np.uint64)
+        n = o.size - 1
+        if n > 0 and int(o[-1]) > frames.nbytes:
+            raise ValueError("offsets exceed frames")
+        out = self._host_args(frames, out, n, np.uint8)
+        t = ctypes.c_uint64(0)
+        st = self._lib.aipstack_chksum_engine_submit_rx_verify(
+            self._h, frames.ctypes.data, o.ctypes.data, max(n, 0), out.ctypes.data,
+            ctypes.byref(t))
+        self._keep(t.value, frames, out)
+        _check(st, "aipstack_chksum_engine_submit_rx_verify")
+        return t.value, out
 
     def csr(self, buf: np.ndarray, offsets: np.ndarray, *, out=None,
             final: bool = False) -> np.ndarray:

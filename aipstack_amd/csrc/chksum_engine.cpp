@@ -46,8 +46,9 @@ struct Slot {
     uint16_t *h_out = nullptr;     // pinned host results
     hipEvent_t done = nullptr;
     bool busy = false;
-    uint16_t *user_out = nullptr;  // where h_out goes once the slot completes
+    void *user_out = nullptr;      // where h_out goes once the slot completes
     uint64_t count = 0;
+    uint32_t out_elem = 2;         // bytes per result: 2 (checksums) or 1 (Rx verdicts)
     uint64_t ticket = 0;           // batch this slot's piece belongs to
 };
 
@@ -135,7 +136,7 @@ int drain(aipstack_chksum_engine *e, Slot &s, bool blocking = true) {
     }
     const int st = check_hip(r);
     if (st == AIPSTACK_CHKSUM_OK) {
-        std::memcpy(s.user_out, s.h_out, s.count * sizeof(uint16_t));
+        std::memcpy(s.user_out, s.h_out, s.count * s.out_elem);
     } else {
         e->failed_ticket = s.ticket;
         e->failed_status = st;
@@ -146,9 +147,10 @@ int drain(aipstack_chksum_engine *e, Slot &s, bool blocking = true) {
 
 // Enqueue one batch as chunks over the slots. chunker(i0, &i1, &src, &bytes) describes
 // chunk [i0, i1) of packets and its byte range in host memory; launch(slot, i0, i1)
-// enqueues its kernel. Returns the status of the enqueue; *ticket identifies the batch.
+// enqueues its kernel, whose results (elem bytes per packet) land in the slot's d_out.
+// Returns the status of the enqueue; *ticket identifies the batch.
 template <class Chunker, class Launch>
-int enqueue(aipstack_chksum_engine *e, uint64_t n, uint16_t *h_out, Chunker chunker,
+int enqueue(aipstack_chksum_engine *e, uint64_t n, void *h_out, uint32_t elem, Chunker chunker,
             Launch launch, uint64_t *ticket) {
     if (hipSetDevice(e->device) != hipSuccess) return AIPSTACK_CHKSUM_ENODEV;
     const uint64_t t = e->next_ticket++;
@@ -174,12 +176,13 @@ int enqueue(aipstack_chksum_engine *e, uint64_t n, uint16_t *h_out, Chunker chun
                                               s.stream));
         if (status == AIPSTACK_CHKSUM_OK) status = launch(s, i0, i1);
         if (status == AIPSTACK_CHKSUM_OK)
-            status = check_hip(hipMemcpyAsync(s.h_out, s.d_out, cnt * sizeof(uint16_t),
+            status = check_hip(hipMemcpyAsync(s.h_out, s.d_out, cnt * elem,
                                               hipMemcpyDeviceToHost, s.stream));
         if (status == AIPSTACK_CHKSUM_OK) status = check_hip(hipEventRecord(s.done, s.stream));
         s.busy = status == AIPSTACK_CHKSUM_OK;
-        s.user_out = h_out + i0;
+        s.user_out = static_cast<char *>(h_out) + i0 * elem;
         s.count = cnt;
+        s.out_elem = elem;
         s.ticket = t;
         i0 = i1;
     }
@@ -295,14 +298,15 @@ extern "C" int aipstack_chksum_engine_submit_strided(aipstack_chksum_engine *e,
                                              s.stream);
     };
     std::lock_guard<std::mutex> lock(e->mu);
-    return enqueue(e, n, h_out, chunker, launch, ticket);
+    return enqueue(e, n, h_out, 2, chunker, launch, ticket);
 }
 
-extern "C" int aipstack_chksum_engine_submit_csr(aipstack_chksum_engine *e, const void *h_base,
-                                                 const uint64_t *h_offsets, uint64_t n,
-                                                 uint16_t *h_out, uint32_t flags,
-                                                 uint64_t *ticket) {
-    if (!e || !h_base || !h_offsets || !h_out || !ticket) return AIPSTACK_CHKSUM_EINVAL;
+namespace {
+// CSR batches (checksums or Rx verdicts): whole packets per chunk while they fit, offsets
+// rebased into the slot's staging.
+template <class Kernel>
+int submit_csr_like(aipstack_chksum_engine *e, const void *h_base, const uint64_t *h_offsets,
+                    uint64_t n, void *h_out, uint32_t elem, Kernel kernel, uint64_t *ticket) {
     for (uint64_t i = 0; i < n; ++i)  // contract check: non-decreasing, each <= 65535
         if (h_offsets[i + 1] < h_offsets[i] || h_offsets[i + 1] - h_offsets[i] > AIPSTACK_CHKSUM_MAX_LEN)
             return AIPSTACK_CHKSUM_EINVAL;
@@ -326,10 +330,52 @@ extern "C" int aipstack_chksum_engine_submit_csr(aipstack_chksum_engine *e, cons
         int st = check_hip(hipMemcpyAsync(s.d_off, s.h_off, (cnt + 1) * 8, hipMemcpyHostToDevice,
                                           s.stream));
         if (st != AIPSTACK_CHKSUM_OK) return st;
-        return aipstack_chksum_batch_csr(s.d_bytes, s.d_off, cnt, s.d_out, flags, s.stream);
+        return kernel(s, cnt);
     };
     std::lock_guard<std::mutex> lock(e->mu);
-    return enqueue(e, n, h_out, chunker, launch, ticket);
+    return enqueue(e, n, h_out, elem, chunker, launch, ticket);
+}
+}  // namespace
+
+extern "C" int aipstack_chksum_engine_submit_rx_verify(aipstack_chksum_engine *e,
+                                                       const void *h_base,
+                                                       const uint64_t *h_offsets, uint64_t n,
+                                                       uint8_t *h_verdicts, uint64_t *ticket) {
+    if (!e || !h_base || !h_offsets || !h_verdicts || !ticket) return AIPSTACK_CHKSUM_EINVAL;
+    return submit_csr_like(e, h_base, h_offsets, n, h_verdicts, 1,
+                           [&](Slot &s, uint64_t cnt) {
+                               return aipstack_chksum_rx_verify(s.d_bytes, s.d_off, cnt,
+                                                                reinterpret_cast<uint8_t *>(s.d_out),
+                                                                s.stream);
+                           },
+                           ticket);
+}
+
+extern "C" int aipstack_chksum_engine_host_rx_verify(aipstack_chksum_engine *e, const void *h_base,
+                                                     const uint64_t *h_offsets, uint64_t n,
+                                                     uint8_t *h_verdicts) {
+    if (!e || !h_base || !h_offsets || !h_verdicts) return AIPSTACK_CHKSUM_EINVAL;
+    if (n == 0) return AIPSTACK_CHKSUM_OK;
+    uint64_t t = 0;
+    const int st = aipstack_chksum_engine_submit_rx_verify(e, h_base, h_offsets, n, h_verdicts, &t);
+    if (st != AIPSTACK_CHKSUM_OK) {
+        if (t) (void)aipstack_chksum_engine_wait(e, t);
+        return st;
+    }
+    return aipstack_chksum_engine_wait(e, t);
+}
+
+extern "C" int aipstack_chksum_engine_submit_csr(aipstack_chksum_engine *e, const void *h_base,
+                                                 const uint64_t *h_offsets, uint64_t n,
+                                                 uint16_t *h_out, uint32_t flags,
+                                                 uint64_t *ticket) {
+    if (!e || !h_base || !h_offsets || !h_out || !ticket) return AIPSTACK_CHKSUM_EINVAL;
+    return submit_csr_like(e, h_base, h_offsets, n, h_out, 2,
+                           [&](Slot &s, uint64_t cnt) {
+                               return aipstack_chksum_batch_csr(s.d_bytes, s.d_off, cnt, s.d_out,
+                                                                flags, s.stream);
+                           },
+                           ticket);
 }
 
 extern "C" int aipstack_chksum_engine_poll(aipstack_chksum_engine *e, uint64_t ticket) {

@@ -495,8 +495,8 @@ def main():
             raise SystemExit("--small covers configs A, RX and TX on one GPU")
         return small_batches(args, layout, plen, dev)
     if args.e2e:
-        if layout not in ("strided", "csr"):
-            raise SystemExit("--e2e covers the packet configs A, B, C")
+        if layout not in ("strided", "csr", "rx"):
+            raise SystemExit("--e2e covers the packet configs A, B, C and RX")
         return e2e(args, rank, world, local_rank, layout, n, plen)
 
     # ---- this rank's shard, generated in place (global packets [rank*n, (rank+1)*n))
@@ -804,7 +804,9 @@ def e2e(args, rank, world, local_rank, layout, n, plen):
     off, total = spec["offsets"], spec.get("payload", spec["total"])
     stride = spec.get("stride", plen)
     host = host_shard(spec)
-    out = np.empty(n, dtype=np.uint16)
+    if layout == "rx":  # frames: synthesised (and made valid) on the host by host_shard
+        off, total = spec["offsets"], spec["total"]
+    out = np.empty(n, dtype=np.uint8 if layout == "rx" else np.uint16)
     eng = A.ChksumEngine(int(os.environ.get("AIPSTACK_BENCH_FORCE_DEVICE", local_rank)),
                          chunk_bytes=args.e2e_chunk_mib << 20,
                          nstreams=args.e2e_streams)
@@ -814,6 +816,8 @@ def e2e(args, rank, world, local_rank, layout, n, plen):
     def step():
         if layout == "strided":
             eng.strided(host, stride, plen, n, out=out)
+        elif layout == "rx":
+            eng.rx_verify(host, off, out=out)
         else:
             eng.csr(host, off, out=out)
 
@@ -845,8 +849,13 @@ def e2e(args, rank, world, local_rank, layout, n, plen):
     parity = None
     if rank == 0 and not args.no_parity:
         lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "libchksum_oracle.so"))
-        want = np.empty(n, dtype=np.uint16)
-        if layout == "strided":
+        want = np.empty(n, dtype=out.dtype)
+        if layout == "rx":
+            lib.oracle_rx_verify_batch.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_uint64,
+                                                                           ctypes.c_void_p]
+            o = off.astype(np.uint64)
+            lib.oracle_rx_verify_batch(host.ctypes.data, o.ctypes.data, n, want.ctypes.data)
+        elif layout == "strided":
             lib.oracle_batch_strided.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
                                                  ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32]
             lib.oracle_batch_strided(host.ctypes.data, stride, plen, n, want.ctypes.data, 0)
@@ -859,7 +868,8 @@ def e2e(args, rank, world, local_rank, layout, n, plen):
     value = total * world * args.steps / max_elapsed / 2**30
     if rank == 0:
         print(json.dumps({
-            "metric": "GiB/s checksummed end-to-end (host memory in, host results out)",
+            "metric": "GiB/s " + ("Rx-verified" if layout == "rx" else "checksummed")
+                      + " end-to-end (host memory in, host results out)",
             "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(max_elapsed / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u16",

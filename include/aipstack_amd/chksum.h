@@ -206,6 +206,18 @@ int aipstack_chksum_engine_submit_csr(aipstack_chksum_engine *engine, const void
                                       const uint64_t *h_offsets, uint64_t n, uint16_t *h_out,
                                       uint32_t flags, uint64_t *ticket);
 
+/* Rx verify of raw Ethernet frames held in HOST memory -- the TAP receive path
+ * (tap/linux/TapDeviceLinux.cpp:156-178) batched: h_verdicts[i] = the AIPSTACK_RX_* verdict
+ * of frame i = h_base[h_offsets[i] .. h_offsets[i+1]), as aipstack_chksum_rx_verify
+ * (offsets non-decreasing, each frame <= 65535 bytes, else _EINVAL before any work).
+ * Synchronous and submit forms, as above. */
+int aipstack_chksum_engine_host_rx_verify(aipstack_chksum_engine *engine, const void *h_base,
+                                          const uint64_t *h_offsets, uint64_t n,
+                                          uint8_t *h_verdicts);
+int aipstack_chksum_engine_submit_rx_verify(aipstack_chksum_engine *engine, const void *h_base,
+                                            const uint64_t *h_offsets, uint64_t n,
+                                            uint8_t *h_verdicts, uint64_t *ticket);
+
 /* Completion of a submitted batch: 0 = done (h_out holds the results), 1 = still running
  * (poll only), negative = it failed (or _EINVAL for an unknown ticket). _wait blocks. */
 int aipstack_chksum_engine_poll(aipstack_chksum_engine *engine, uint64_t ticket);

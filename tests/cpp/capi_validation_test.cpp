@@ -88,6 +88,9 @@ int main() {
     std::uint64_t ticket = 0;
     CHECK(aipstack_chksum_engine_submit_strided(nullptr, dummy, 1, 1, 1, out, 0, &ticket) == EINVAL_);
     CHECK(aipstack_chksum_engine_submit_csr(nullptr, dummy, off, 1, out, 0, &ticket) == EINVAL_);
+    std::uint8_t verdicts[4] = {0, 0, 0, 0};
+    CHECK(aipstack_chksum_engine_host_rx_verify(nullptr, dummy, off, 1, verdicts) == EINVAL_);
+    CHECK(aipstack_chksum_engine_submit_rx_verify(nullptr, dummy, off, 1, verdicts, &ticket) == EINVAL_);
     CHECK(aipstack_chksum_engine_poll(nullptr, 1) == EINVAL_);
     CHECK(aipstack_chksum_engine_wait(nullptr, 1) == EINVAL_);
     aipstack_chksum_engine_destroy(nullptr);  // no-op
@@ -109,6 +112,10 @@ int main() {
         CHECK(aipstack_chksum_engine_unregister(e, dummy) == EINVAL_);  // never registered
         CHECK(aipstack_chksum_engine_submit_csr(e, dummy, bad_off, 2, out, 0, &ticket) == EINVAL_);
         CHECK(aipstack_chksum_engine_submit_csr(e, dummy, off, 1, out, 0, nullptr) == EINVAL_);
+        CHECK(aipstack_chksum_engine_host_rx_verify(e, dummy, bad_off, 2, verdicts) == EINVAL_);
+        CHECK(aipstack_chksum_engine_host_rx_verify(e, big.data(), big_off, 1, verdicts) == EINVAL_);
+        CHECK(aipstack_chksum_engine_submit_rx_verify(e, dummy, off, 1, nullptr, &ticket) == EINVAL_);
+        CHECK(aipstack_chksum_engine_host_rx_verify(e, dummy, off, 0, verdicts) == 0);  // no-op
         CHECK(aipstack_chksum_engine_poll(e, 0) == EINVAL_);          // never a ticket
         CHECK(aipstack_chksum_engine_wait(e, 1u << 30) == EINVAL_);   // not issued yet
         // a real batch through submit + poll/wait

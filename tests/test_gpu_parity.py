@@ -451,6 +451,26 @@ def test_engine_async_submit_poll_wait(oracle):
             eng.wait(10**9)  # never issued
 
 
+@pytest.mark.parametrize("register", [False, True])
+def test_engine_host_rx_verify(oracle, register):
+    """Raw frames in host memory (the TAP receive path batched): verdicts as the device
+    batch and the frame oracle give, over several engine chunks; also through submit/wait."""
+    buf, off = synth.frames_host(60000, seed=41)
+    oracle.tx_fill_batch(buf, off)
+    _corrupt(buf, off, 0.2, 3)
+    want = oracle.rx_verify_batch(buf, off)
+    with A.ChksumEngine(0, chunk_bytes=4 << 20, nstreams=3) as eng:
+        if register:
+            eng.register(buf)
+        got = eng.rx_verify(buf, off)
+        assert got.dtype == np.uint8 and np.array_equal(got, want)
+        t, out = eng.submit_rx_verify(buf, off)
+        eng.wait(t)
+        assert np.array_equal(out, want)
+        with pytest.raises(A.ChksumError):
+            eng.rx_verify(buf, np.array([0, 100, 50], dtype=np.uint64))
+
+
 def test_engine_rejects_bad_offsets():
     buf = np.zeros(1 << 20, dtype=np.uint8)
     with A.ChksumEngine(0) as eng:
