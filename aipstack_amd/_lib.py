@@ -48,6 +48,9 @@ SIGNATURES = {
     "aipstack_chksum_engine_host_strided": (_c_int, [_c_vp, _c_vp, _c_u64, _c_u32, _c_u64, _c_vp, _c_u32]),
     "aipstack_chksum_engine_host_csr": (_c_int, [_c_vp, _c_vp, _c_vp, _c_u64, _c_vp, _c_u32]),
     "aipstack_chksum_engine_host_rx_verify": (_c_int, [_c_vp, _c_vp, _c_vp, _c_u64, _c_vp]),
+    "aipstack_chksum_engine_host_tx_fill": (_c_int, [_c_vp, _c_vp, _c_vp, _c_u64, _c_vp]),
+    "aipstack_chksum_engine_submit_tx_fill": (_c_int, [_c_vp, _c_vp, _c_vp, _c_u64, _c_vp, _c_vp]),
+    "aipstack_chksum_tx_fill_records": (_c_int, [_c_vp, _c_vp, _c_u64, _c_vp, _c_vp]),
     "aipstack_chksum_engine_submit_rx_verify": (_c_int, [_c_vp, _c_vp, _c_vp, _c_u64, _c_vp, _c_vp]),
     "aipstack_chksum_engine_submit_strided": (_c_int, [_c_vp, _c_vp, _c_u64, _c_u32, _c_u64, _c_vp,
                                                        _c_u32, ctypes.POINTER(_c_u64)]),

@@ -499,6 +499,41 @@ class ChksumEngine:
         _check(st, "aipstack_chksum_engine_submit_rx_verify")
         return t.value, out
 
+    @staticmethod
+    def _tx_args(frames, offsets, status):
+        if not isinstance(frames, np.ndarray) or not frames.flags.writeable:
+            raise ValueError("frames must be a writable numpy array (filled in place)")
+        o = np.ascontiguousarray(offsets, dtype=np.uint64)
+        n = o.size - 1
+        if n > 0 and int(o[-1]) > frames.nbytes:
+            raise ValueError("offsets exceed frames")
+        return o, n, ChksumEngine._host_args(frames, status, n, np.uint8)
+
+    def tx_fill(self, frames: np.ndarray, offsets: np.ndarray, *, status=None) -> np.ndarray:
+        """Tx fill of raw Ethernet frames in HOST memory, IN PLACE (frame i =
+        ``frames[offsets[i]:offsets[i+1]]``): the IPv4 header and L4 checksum fields are
+        written as :func:`tx_fill` does on the device; returns the per-frame AIPSTACK_TX_*
+        statuses (uint8)."""
+        o, n, status = self._tx_args(frames, offsets, status)
+        _check(self._lib.aipstack_chksum_engine_host_tx_fill(
+            self._h, frames.ctypes.data, o.ctypes.data, max(n, 0), status.ctypes.data),
+            "aipstack_chksum_engine_host_tx_fill")
+        return status
+
+    def submit_tx_fill(self, frames: np.ndarray, offsets: np.ndarray, *, status=None):
+        """Enqueue a Tx fill batch; returns (ticket, status). The frames are filled and
+        `status` written when the batch completes (wait / poll); `frames` must not be
+        touched until then."""
+        o, n, status = self._tx_args(frames, offsets, status)
+        t = ctypes.c_uint64(0)
+        st = self._lib.aipstack_chksum_engine_submit_tx_fill(
+            self._h, frames.ctypes.data, o.ctypes.data, max(n, 0), status.ctypes.data,
+            ctypes.byref(t))
+        # the completion reads the offsets again (it writes the fields into the frames)
+        self._keep(t.value, frames, o, status)
+        _check(st, "aipstack_chksum_engine_submit_tx_fill")
+        return t.value, status
+
     def csr(self, buf: np.ndarray, offsets: np.ndarray, *, out=None,
             final: bool = False) -> np.ndarray:
         o = np.ascontiguousarray(offsets, dtype=np.uint64)

@@ -40,7 +40,7 @@ struct Slot {
     hipStream_t stream = nullptr;
     void *d_bytes = nullptr;       // device staging for packet bytes
     uint64_t *d_off = nullptr;     // device staging for CSR offsets
-    uint16_t *d_out = nullptr;     // device results
+    uint16_t *d_out = nullptr;     // device results (up to 8 bytes per packet)
     void *h_stage = nullptr;       // pinned host staging (pageable inputs)
     uint64_t *h_off = nullptr;     // pinned host staging for rebased offsets
     uint16_t *h_out = nullptr;     // pinned host results
@@ -48,7 +48,12 @@ struct Slot {
     bool busy = false;
     void *user_out = nullptr;      // where h_out goes once the slot completes
     uint64_t count = 0;
-    uint32_t out_elem = 2;         // bytes per result: 2 (checksums) or 1 (Rx verdicts)
+    uint32_t out_elem = 2;         // bytes per result: 2 (checksums), 1 (Rx verdicts), 8 (Tx)
+    // Tx fill: instead of copying the results out, apply the piece's records to the
+    // caller's frames in host memory (frames + offs[i], i < count) and statuses
+    char *tx_frames = nullptr;
+    const uint64_t *tx_offs = nullptr;
+    uint8_t *tx_status = nullptr;
     uint64_t ticket = 0;           // batch this slot's piece belongs to
 };
 
@@ -122,6 +127,51 @@ void stage_copy(void *dst, const void *src, uint64_t bytes) {
     for (std::thread &t : pool) t.join();
 }
 
+// Tx fill from host memory: write the checksum fields (big-endian) of frames [lo, hi) of a
+// completed piece into the caller's frames, and their statuses (record layout: chksum.h,
+// aipstack_chksum_tx_fill_records).
+void apply_tx_range(const uint64_t *rec, char *frames, const uint64_t *offs, uint8_t *status,
+                    uint64_t lo, uint64_t hi) {
+    for (uint64_t i = lo; i < hi; ++i) {
+        const uint64_t x = rec[i];
+        char *f = frames + offs[i];
+        status[i] = (uint8_t)(x >> 48);
+        if ((x >> 40) & 1u) {
+            f[24] = (char)((x >> 8) & 0xFFu);
+            f[25] = (char)(x & 0xFFu);
+        }
+        if ((x >> 41) & 1u) {
+            const uint32_t fo = (uint32_t)(x >> 32) & 0xFFu;
+            f[fo] = (char)((x >> 24) & 0xFFu);
+            f[fo + 1] = (char)((x >> 16) & 0xFFu);
+        }
+    }
+}
+
+// A piece's frames are spread over up to 64 MiB of host memory: every frame is a cache miss,
+// so a large piece is applied by up to 8 threads (16 Ki frames and more each).
+void apply_tx_records(const uint64_t *rec, char *frames, const uint64_t *offs, uint8_t *status,
+                      uint64_t count) {
+    constexpr uint64_t kPerThreadMin = 16384;
+    const unsigned hw = std::thread::hardware_concurrency();
+    const unsigned nt =
+        (unsigned)std::min<uint64_t>(std::min<uint64_t>(count / kPerThreadMin, 8), hw ? hw : 1);
+    if (nt <= 1) {
+        apply_tx_range(rec, frames, offs, status, 0, count);
+        return;
+    }
+    const uint64_t per = (count + nt - 1) / nt;
+    std::vector<std::thread> pool;
+    pool.reserve(nt);
+    for (unsigned t = 0; t < nt; ++t) {
+        const uint64_t lo = (uint64_t)t * per;
+        if (lo >= count) break;
+        const uint64_t hi = std::min(count, lo + per);
+        pool.emplace_back([=] { apply_tx_range(rec, frames, offs, status, lo, hi); });
+    }
+    for (std::thread &t : pool) t.join();
+}
+
 // Complete slot s: wait for it (blocking) or only if it is done (non-blocking: returns
 // 1 while it is still running), then hand its results to the caller. A HIP error is
 // recorded against the slot's ticket.
@@ -135,7 +185,10 @@ int drain(aipstack_chksum_engine *e, Slot &s, bool blocking = true) {
         if (r == hipErrorNotReady) return 1;
     }
     const int st = check_hip(r);
-    if (st == AIPSTACK_CHKSUM_OK) {
+    if (st == AIPSTACK_CHKSUM_OK && s.tx_frames) {
+        apply_tx_records(reinterpret_cast<const uint64_t *>(s.h_out), s.tx_frames, s.tx_offs,
+                         s.tx_status, s.count);
+    } else if (st == AIPSTACK_CHKSUM_OK) {
         std::memcpy(s.user_out, s.h_out, s.count * s.out_elem);
     } else {
         e->failed_ticket = s.ticket;
@@ -161,6 +214,7 @@ int enqueue(aipstack_chksum_engine *e, uint64_t n, void *h_out, uint32_t elem, C
         Slot &s = e->slots[e->next_slot];
         e->next_slot = (e->next_slot + 1) % e->slots.size();
         (void)drain(e, s);  // an earlier piece (this batch's or an older one's) completes
+        s.tx_frames = nullptr;  // a Tx fill's launch sets it again
         uint64_t i1 = 0;
         const char *src = nullptr;
         uint64_t bytes = 0;
@@ -231,10 +285,10 @@ extern "C" int aipstack_chksum_engine_create(int device, uint64_t chunk_bytes, i
         if (st == AIPSTACK_CHKSUM_OK) st = check_hip(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
         if (st == AIPSTACK_CHKSUM_OK) st = check_hip(hipMalloc(&s.d_bytes, chunk_bytes));
         if (st == AIPSTACK_CHKSUM_OK) st = check_hip(hipMalloc(reinterpret_cast<void **>(&s.d_off), (e->chunk_packets + 1) * 8));
-        if (st == AIPSTACK_CHKSUM_OK) st = check_hip(hipMalloc(reinterpret_cast<void **>(&s.d_out), e->chunk_packets * 2));
+        if (st == AIPSTACK_CHKSUM_OK) st = check_hip(hipMalloc(reinterpret_cast<void **>(&s.d_out), e->chunk_packets * 8));
         if (st == AIPSTACK_CHKSUM_OK) st = check_hip(hipHostMalloc(&s.h_stage, chunk_bytes, hipHostMallocDefault));
         if (st == AIPSTACK_CHKSUM_OK) st = check_hip(hipHostMalloc(reinterpret_cast<void **>(&s.h_off), (e->chunk_packets + 1) * 8, hipHostMallocDefault));
-        if (st == AIPSTACK_CHKSUM_OK) st = check_hip(hipHostMalloc(reinterpret_cast<void **>(&s.h_out), e->chunk_packets * 2, hipHostMallocDefault));
+        if (st == AIPSTACK_CHKSUM_OK) st = check_hip(hipHostMalloc(reinterpret_cast<void **>(&s.h_out), e->chunk_packets * 8, hipHostMallocDefault));
         if (st == AIPSTACK_CHKSUM_OK) st = check_hip(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
     }
     if (st != AIPSTACK_CHKSUM_OK) {
@@ -330,7 +384,7 @@ int submit_csr_like(aipstack_chksum_engine *e, const void *h_base, const uint64_
         int st = check_hip(hipMemcpyAsync(s.d_off, s.h_off, (cnt + 1) * 8, hipMemcpyHostToDevice,
                                           s.stream));
         if (st != AIPSTACK_CHKSUM_OK) return st;
-        return kernel(s, cnt);
+        return kernel(s, i0, cnt);
     };
     std::lock_guard<std::mutex> lock(e->mu);
     return enqueue(e, n, h_out, elem, chunker, launch, ticket);
@@ -343,12 +397,43 @@ extern "C" int aipstack_chksum_engine_submit_rx_verify(aipstack_chksum_engine *e
                                                        uint8_t *h_verdicts, uint64_t *ticket) {
     if (!e || !h_base || !h_offsets || !h_verdicts || !ticket) return AIPSTACK_CHKSUM_EINVAL;
     return submit_csr_like(e, h_base, h_offsets, n, h_verdicts, 1,
-                           [&](Slot &s, uint64_t cnt) {
+                           [&](Slot &s, uint64_t, uint64_t cnt) {
                                return aipstack_chksum_rx_verify(s.d_bytes, s.d_off, cnt,
                                                                 reinterpret_cast<uint8_t *>(s.d_out),
                                                                 s.stream);
                            },
                            ticket);
+}
+
+extern "C" int aipstack_chksum_engine_submit_tx_fill(aipstack_chksum_engine *e, void *h_base,
+                                                     const uint64_t *h_offsets, uint64_t n,
+                                                     uint8_t *h_status, uint64_t *ticket) {
+    if (!e || !h_base || !h_offsets || !h_status || !ticket) return AIPSTACK_CHKSUM_EINVAL;
+    char *frames = static_cast<char *>(h_base);
+    return submit_csr_like(e, h_base, h_offsets, n, h_status, 8,
+                           [&](Slot &s, uint64_t i0, uint64_t cnt) {
+                               s.tx_frames = frames;  // applied on completion (drain)
+                               s.tx_offs = h_offsets + i0;
+                               s.tx_status = h_status + i0;
+                               return aipstack_chksum_tx_fill_records(
+                                   s.d_bytes, s.d_off, cnt, reinterpret_cast<uint64_t *>(s.d_out),
+                                   s.stream);
+                           },
+                           ticket);
+}
+
+extern "C" int aipstack_chksum_engine_host_tx_fill(aipstack_chksum_engine *e, void *h_base,
+                                                   const uint64_t *h_offsets, uint64_t n,
+                                                   uint8_t *h_status) {
+    if (!e || !h_base || !h_offsets || !h_status) return AIPSTACK_CHKSUM_EINVAL;
+    if (n == 0) return AIPSTACK_CHKSUM_OK;
+    uint64_t t = 0;
+    const int st = aipstack_chksum_engine_submit_tx_fill(e, h_base, h_offsets, n, h_status, &t);
+    if (st != AIPSTACK_CHKSUM_OK) {
+        if (t) (void)aipstack_chksum_engine_wait(e, t);
+        return st;
+    }
+    return aipstack_chksum_engine_wait(e, t);
 }
 
 extern "C" int aipstack_chksum_engine_host_rx_verify(aipstack_chksum_engine *e, const void *h_base,
@@ -371,7 +456,7 @@ extern "C" int aipstack_chksum_engine_submit_csr(aipstack_chksum_engine *e, cons
                                                  uint64_t *ticket) {
     if (!e || !h_base || !h_offsets || !h_out || !ticket) return AIPSTACK_CHKSUM_EINVAL;
     return submit_csr_like(e, h_base, h_offsets, n, h_out, 2,
-                           [&](Slot &s, uint64_t cnt) {
+                           [&](Slot &s, uint64_t, uint64_t cnt) {
                                return aipstack_chksum_batch_csr(s.d_bytes, s.d_off, cnt, s.d_out,
                                                                 flags, s.stream);
                            },

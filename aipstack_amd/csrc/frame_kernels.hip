@@ -657,7 +657,7 @@ __global__ __launch_bounds__(kBlock, AIPSTACK_FRAME_WAVES_PER_SIMD) void frame_k
 
 template <bool TX, bool SPLIT = false>
 int launch_frames(const void *d_base, const uint64_t *d_offsets, uint64_t n, uint8_t *d_status,
-                  uint64_t *d_records, hipStream_t stream) {
+                  uint64_t *d_records, hipStream_t stream, bool scatter = true) {
     const int cus = device_cu_count();
     if (cus <= 0) return AIPSTACK_CHKSUM_EHIP;
     // small batches: fewer frames per chunk, so that they spread over many waves (as the
@@ -690,7 +690,7 @@ int launch_frames(const void *d_base, const uint64_t *d_offsets, uint64_t n, uin
     }
 #undef AIPSTACK_LAUNCH_FRAMES_SU
 #undef AIPSTACK_LAUNCH_FRAMES
-    if constexpr (SPLIT) {
+    if (SPLIT && scatter) {
         const int st = check_hip(hipGetLastError());
         if (st != AIPSTACK_CHKSUM_OK) return st;
         const uint64_t sblocks = min((n + kBlock - 1) / kBlock, (uint64_t)cus * 64);
@@ -721,6 +721,16 @@ extern "C" int aipstack_chksum_tx_fill(void *d_base, const uint64_t *d_offsets, 
 
 extern "C" uint64_t aipstack_chksum_tx_fill_workspace_bytes(uint64_t n) {
     return n * sizeof(uint64_t);
+}
+
+extern "C" int aipstack_chksum_tx_fill_records(const void *d_base, const uint64_t *d_offsets,
+                                               uint64_t n, uint64_t *d_records, void *stream) {
+    if (n == 0) return AIPSTACK_CHKSUM_OK;
+    if (!d_base || !d_offsets || !d_records || n > (1ull << 40) ||
+        ((uintptr_t)d_records & 7u) != 0)
+        return AIPSTACK_CHKSUM_EINVAL;
+    return launch_frames<true, true>(const_cast<void *>(d_base), d_offsets, n, nullptr, d_records,
+                                     (hipStream_t)stream, false);
 }
 
 extern "C" int aipstack_chksum_tx_fill_split(void *d_base, const uint64_t *d_offsets, uint64_t n,

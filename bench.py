@@ -495,8 +495,8 @@ def main():
             raise SystemExit("--small covers configs A, RX and TX on one GPU")
         return small_batches(args, layout, plen, dev)
     if args.e2e:
-        if layout not in ("strided", "csr", "rx"):
-            raise SystemExit("--e2e covers the packet configs A, B, C and RX")
+        if layout not in ("strided", "csr", "rx", "tx"):
+            raise SystemExit("--e2e covers the packet configs A, B, C, RX and TX")
         return e2e(args, rank, world, local_rank, layout, n, plen)
 
     # ---- this rank's shard, generated in place (global packets [rank*n, (rank+1)*n))
@@ -804,9 +804,13 @@ def e2e(args, rank, world, local_rank, layout, n, plen):
     off, total = spec["offsets"], spec.get("payload", spec["total"])
     stride = spec.get("stride", plen)
     host = host_shard(spec)
-    if layout == "rx":  # frames: synthesised (and made valid) on the host by host_shard
+    frames = layout in ("rx", "tx")
+    if frames:  # frames: synthesised (and, for RX, made valid) on the host by host_shard
         off, total = spec["offsets"], spec["total"]
-    out = np.empty(n, dtype=np.uint8 if layout == "rx" else np.uint16)
+    # Tx fill writes the frames in place: the fill ignores the fields' old contents, so
+    # every step gives the same bytes; parity compares with the oracle's fill of a copy
+    orig = host.copy() if layout == "tx" and rank == 0 and not args.no_parity else None
+    out = np.empty(n, dtype=np.uint8 if frames else np.uint16)
     eng = A.ChksumEngine(int(os.environ.get("AIPSTACK_BENCH_FORCE_DEVICE", local_rank)),
                          chunk_bytes=args.e2e_chunk_mib << 20,
                          nstreams=args.e2e_streams)
@@ -818,6 +822,8 @@ def e2e(args, rank, world, local_rank, layout, n, plen):
             eng.strided(host, stride, plen, n, out=out)
         elif layout == "rx":
             eng.rx_verify(host, off, out=out)
+        elif layout == "tx":
+            eng.tx_fill(host, off, status=out)
         else:
             eng.csr(host, off, out=out)
 
@@ -850,7 +856,14 @@ def e2e(args, rank, world, local_rank, layout, n, plen):
     if rank == 0 and not args.no_parity:
         lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "libchksum_oracle.so"))
         want = np.empty(n, dtype=out.dtype)
-        if layout == "rx":
+        ok_bytes = True
+        if layout == "tx":
+            lib.oracle_tx_fill_batch.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_uint64,
+                                                                         ctypes.c_void_p]
+            o = off.astype(np.uint64)
+            lib.oracle_tx_fill_batch(orig.ctypes.data, o.ctypes.data, n, want.ctypes.data)
+            ok_bytes = np.array_equal(host, orig)
+        elif layout == "rx":
             lib.oracle_rx_verify_batch.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_uint64,
                                                                            ctypes.c_void_p]
             o = off.astype(np.uint64)
@@ -864,11 +877,11 @@ def e2e(args, rank, world, local_rank, layout, n, plen):
                                              ctypes.c_void_p, ctypes.c_uint32]
             o = off.astype(np.uint64)
             lib.oracle_batch_csr(host.ctypes.data, o.ctypes.data, n, want.ctypes.data, 0)
-        parity = "bit-exact" if np.array_equal(out, want) else "MISMATCH"
+        parity = "bit-exact" if ok_bytes and np.array_equal(out, want) else "MISMATCH"
     value = total * world * args.steps / max_elapsed / 2**30
     if rank == 0:
         print(json.dumps({
-            "metric": "GiB/s " + ("Rx-verified" if layout == "rx" else "checksummed")
+            "metric": "GiB/s " + {"rx": "Rx-verified", "tx": "Tx-filled"}.get(layout, "checksummed")
                       + " end-to-end (host memory in, host results out)",
             "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(max_elapsed / args.steps * 1e3, 3),

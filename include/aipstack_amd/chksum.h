@@ -161,6 +161,16 @@ int aipstack_chksum_tx_fill_split(void *d_base, const uint64_t *d_offsets, uint6
                                   uint8_t *d_status, void *d_workspace,
                                   uint64_t workspace_bytes, void *stream);
 
+/* The split fill's read pass alone: per frame the 8-byte record the scatter pass would
+ * apply, frames untouched -- for a caller that applies the fields itself (the host-memory
+ * engine's Tx fill, or a NIC path that patches headers on the way out). Record of frame i:
+ * bits 0-15 the IPv4 header checksum, 16-31 the L4 checksum (the field values, big-endian
+ * when stored), 32-39 the L4 field's offset from the frame start, bit 40 = write the IPv4
+ * field (at offset 24), bit 41 = write the L4 field, bits 48-55 the status (AIPSTACK_RX_*).
+ * d_records 8-byte aligned, n entries. */
+int aipstack_chksum_tx_fill_records(const void *d_base, const uint64_t *d_offsets, uint64_t n,
+                                    uint64_t *d_records, void *stream);
+
 /* ---- 3. host-memory streaming engine ----------------------------------------------- */
 
 /* The reference's packet path starts and ends in host memory (TAP read()/write(),
@@ -217,6 +227,19 @@ int aipstack_chksum_engine_host_rx_verify(aipstack_chksum_engine *engine, const 
 int aipstack_chksum_engine_submit_rx_verify(aipstack_chksum_engine *engine, const void *h_base,
                                             const uint64_t *h_offsets, uint64_t n,
                                             uint8_t *h_verdicts, uint64_t *ticket);
+
+/* Tx fill of raw Ethernet frames held in HOST memory -- the TAP send path batched
+ * (tap/linux/TapDeviceLinux.cpp:122-127): the frames go to the device, the Tx fill's read
+ * pass computes each frame's record (aipstack_chksum_tx_fill_records), 8 bytes per frame come
+ * back, and the engine writes the IPv4 header and L4 checksum fields into the caller's
+ * frames IN PLACE and h_status[i] (as aipstack_chksum_tx_fill) when the batch completes. A
+ * submitted batch's frames, offsets and statuses must stay valid until then. */
+int aipstack_chksum_engine_host_tx_fill(aipstack_chksum_engine *engine, void *h_base,
+                                        const uint64_t *h_offsets, uint64_t n,
+                                        uint8_t *h_status);
+int aipstack_chksum_engine_submit_tx_fill(aipstack_chksum_engine *engine, void *h_base,
+                                          const uint64_t *h_offsets, uint64_t n,
+                                          uint8_t *h_status, uint64_t *ticket);
 
 /* Completion of a submitted batch: 0 = done (h_out holds the results), 1 = still running
  * (poll only), negative = it failed (or _EINVAL for an unknown ticket). _wait blocks. */

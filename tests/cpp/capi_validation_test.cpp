@@ -23,7 +23,7 @@
 
 int main() {
     const int EINVAL_ = AIPSTACK_CHKSUM_EINVAL;
-    char dummy[64] = {0};
+    alignas(8) char dummy[64] = {0};
     std::uint64_t off[2] = {0, 8};
     std::uint16_t out[4];
     std::uint8_t st[4];
@@ -64,6 +64,10 @@ int main() {
           EINVAL_);
     CHECK(aipstack_chksum_rx_verify(dummy, off, 1, nullptr, nullptr) == EINVAL_);
     CHECK(aipstack_chksum_tx_fill(dummy, nullptr, 1, st, nullptr) == EINVAL_);
+    CHECK(aipstack_chksum_tx_fill_records(nullptr, nullptr, 0, nullptr, nullptr) == 0);
+    CHECK(aipstack_chksum_tx_fill_records(dummy, off, 1, nullptr, nullptr) == EINVAL_);
+    CHECK(aipstack_chksum_tx_fill_records(dummy, off, 1, reinterpret_cast<std::uint64_t *>(dummy + 1),
+                                          nullptr) == EINVAL_);
     // split fill: workspace missing, too small, misaligned
     CHECK(aipstack_chksum_tx_fill_workspace_bytes(3) >= 24);
     CHECK(aipstack_chksum_tx_fill_split(dummy, off, 1, st, nullptr, 64, nullptr) == EINVAL_);
@@ -91,6 +95,8 @@ int main() {
     std::uint8_t verdicts[4] = {0, 0, 0, 0};
     CHECK(aipstack_chksum_engine_host_rx_verify(nullptr, dummy, off, 1, verdicts) == EINVAL_);
     CHECK(aipstack_chksum_engine_submit_rx_verify(nullptr, dummy, off, 1, verdicts, &ticket) == EINVAL_);
+    CHECK(aipstack_chksum_engine_host_tx_fill(nullptr, dummy, off, 1, verdicts) == EINVAL_);
+    CHECK(aipstack_chksum_engine_submit_tx_fill(nullptr, dummy, off, 1, verdicts, &ticket) == EINVAL_);
     CHECK(aipstack_chksum_engine_poll(nullptr, 1) == EINVAL_);
     CHECK(aipstack_chksum_engine_wait(nullptr, 1) == EINVAL_);
     aipstack_chksum_engine_destroy(nullptr);  // no-op
@@ -116,6 +122,11 @@ int main() {
         CHECK(aipstack_chksum_engine_host_rx_verify(e, big.data(), big_off, 1, verdicts) == EINVAL_);
         CHECK(aipstack_chksum_engine_submit_rx_verify(e, dummy, off, 1, nullptr, &ticket) == EINVAL_);
         CHECK(aipstack_chksum_engine_host_rx_verify(e, dummy, off, 0, verdicts) == 0);  // no-op
+        CHECK(aipstack_chksum_engine_host_tx_fill(e, dummy, bad_off, 2, verdicts) == EINVAL_);
+        CHECK(aipstack_chksum_engine_host_tx_fill(e, big.data(), big_off, 1, verdicts) == EINVAL_);
+        CHECK(aipstack_chksum_engine_submit_tx_fill(e, dummy, off, 1, nullptr, &ticket) == EINVAL_);
+        CHECK(aipstack_chksum_engine_submit_tx_fill(e, dummy, off, 1, verdicts, nullptr) == EINVAL_);
+        CHECK(aipstack_chksum_engine_host_tx_fill(e, dummy, off, 0, verdicts) == 0);  // no-op
         CHECK(aipstack_chksum_engine_poll(e, 0) == EINVAL_);          // never a ticket
         CHECK(aipstack_chksum_engine_wait(e, 1u << 30) == EINVAL_);   // not issued yet
         // a real batch through submit + poll/wait
