@@ -451,6 +451,33 @@ def test_engine_async_submit_poll_wait(oracle):
             eng.wait(10**9)  # never issued
 
 
+def test_engine_async_frames_in_flight(oracle):
+    """Tx fill, Rx verify and a CSR checksum batch in flight together over small pieces
+    (1 MiB), completed out of order; the Tx batch's offsets are a temporary the engine's
+    completion still reads (kept alive by the wrapper)."""
+    tx_buf, tx_off = synth.frames_host(20000, seed=51)
+    _corrupt(tx_buf, tx_off, 0.1, 52)
+    want_tx = tx_buf.copy()
+    want_st = oracle.tx_fill_batch(want_tx, tx_off)
+    rx_buf, rx_off = synth.frames_host(15000, seed=53)
+    oracle.tx_fill_batch(rx_buf, rx_off)
+    _corrupt(rx_buf, rx_off, 0.3, 54)
+    want_rx = oracle.rx_verify_batch(rx_buf, rx_off)
+    b_buf, b_off = synth.mixed_batch(7000)
+    with A.ChksumEngine(0, chunk_bytes=1 << 20, nstreams=2) as eng:
+        eng.register(rx_buf)
+        tt, st = eng.submit_tx_fill(tx_buf, [int(x) for x in tx_off])
+        tr, vr = eng.submit_rx_verify(rx_buf, rx_off)
+        tb, ob = eng.submit_csr(b_buf, b_off)
+        eng.wait(tb)
+        eng.wait(tt)
+        while not eng.poll(tr):
+            pass
+        assert np.array_equal(st, want_st) and np.array_equal(tx_buf, want_tx)
+        assert np.array_equal(vr, want_rx)
+        assert np.array_equal(ob, oracle.batch_csr(b_buf, b_off))
+
+
 @pytest.mark.parametrize("register", [False, True])
 def test_engine_host_rx_verify(oracle, register):
     """Raw frames in host memory (the TAP receive path batched): verdicts as the device

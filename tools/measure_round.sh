@@ -30,7 +30,7 @@ if [ "$phase" = bench ] || [ "$phase" = all ]; then
         > "$out/bench_$c.json" 2> "$out/bench_$c.err"
   done
   : > "$out/e2e.jsonl"
-  for c in A C; do
+  for c in A C RX TX; do
     timeout -k 10 300 python bench.py --e2e --config $c --steps 5 --warmup 1 >> "$out/e2e.jsonl" 2>> "$out/e2e.err"
     timeout -k 10 300 python bench.py --e2e --e2e-pageable --config $c --steps 3 --warmup 1 >> "$out/e2e.jsonl" 2>> "$out/e2e.err"
   done
