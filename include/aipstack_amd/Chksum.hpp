@@ -8,7 +8,7 @@
 //   IpBufNode / IpBufRef        Buf.h:68-83, 118-251
 //   ipBufProcessBytes           BufUtils.h:129-178
 // in namespace AIpStackAmd, plus BatchChksum: a thin RAII-free C++ wrapper of the GPU
-// batch entry points of chksum.h.
+// batch entry points of chksum.h, and HostChksumEngine: the host-memory engine (owning).
 //
 // Drop-in use inside aipstack itself needs none of this: compile the stack with
 // -DAIPSTACK_EXTERNAL_CHKSUM and link libaipstack_chksum.so, whose extern "C"
@@ -251,6 +251,94 @@ struct BatchChksum {
         return aipstack_chksum_tx_fill_split(d_frames, d_offsets, n, d_status, d_workspace,
                                              workspace_bytes, stream);
     }
+};
+
+// Host-memory batches (the TAP read()/write() path, tap/linux/TapDeviceLinux.cpp:122-127,
+// 156-178) through aipstack_chksum_engine: owns the engine, move-only. Every call returns the
+// C-ABI status (0 = AIPSTACK_CHKSUM_OK); a failed create leaves valid() false.
+class HostChksumEngine {
+public:
+    explicit HostChksumEngine(int device = 0, std::uint64_t chunk_bytes = 0,
+                              int nstreams = 4) {
+        m_status = aipstack_chksum_engine_create(device, chunk_bytes, nstreams, &m_engine);
+    }
+    ~HostChksumEngine() { aipstack_chksum_engine_destroy(m_engine); }
+    HostChksumEngine(HostChksumEngine &&o) noexcept : m_engine(o.m_engine), m_status(o.m_status) {
+        o.m_engine = nullptr;
+    }
+    HostChksumEngine &operator=(HostChksumEngine &&o) noexcept {
+        if (this != &o) {
+            aipstack_chksum_engine_destroy(m_engine);
+            m_engine = o.m_engine;
+            m_status = o.m_status;
+            o.m_engine = nullptr;
+        }
+        return *this;
+    }
+    HostChksumEngine(HostChksumEngine const &) = delete;
+    HostChksumEngine &operator=(HostChksumEngine const &) = delete;
+
+    bool valid() const { return m_engine != nullptr; }
+    int createStatus() const { return m_status; }
+    aipstack_chksum_engine *handle() const { return m_engine; }
+
+    int registerMemory(void *ptr, std::uint64_t bytes) {
+        return aipstack_chksum_engine_register(m_engine, ptr, bytes);
+    }
+    int unregisterMemory(void *ptr) { return aipstack_chksum_engine_unregister(m_engine, ptr); }
+
+    int strided(void const *h_base, std::uint64_t stride, std::uint32_t len, std::uint64_t n,
+                std::uint16_t *h_out, bool final_chksum = false) {
+        return aipstack_chksum_engine_host_strided(m_engine, h_base, stride, len, n, h_out,
+                                                   final_chksum ? AIPSTACK_CHKSUM_FINAL : 0u);
+    }
+    int csr(void const *h_base, std::uint64_t const *h_offsets, std::uint64_t n,
+            std::uint16_t *h_out, bool final_chksum = false) {
+        return aipstack_chksum_engine_host_csr(m_engine, h_base, h_offsets, n, h_out,
+                                               final_chksum ? AIPSTACK_CHKSUM_FINAL : 0u);
+    }
+    int rxVerify(void const *h_frames, std::uint64_t const *h_offsets, std::uint64_t n,
+                 std::uint8_t *h_verdict) {
+        return aipstack_chksum_engine_host_rx_verify(m_engine, h_frames, h_offsets, n, h_verdict);
+    }
+    // Fills the frames IN PLACE (IPv4 header and L4 checksum fields).
+    int txFill(void *h_frames, std::uint64_t const *h_offsets, std::uint64_t n,
+               std::uint8_t *h_status) {
+        return aipstack_chksum_engine_host_tx_fill(m_engine, h_frames, h_offsets, n, h_status);
+    }
+
+    // Asynchronous forms: the buffers must stay valid (and the input unchanged) until the
+    // ticket completes (poll() == 0 or wait()).
+    int submitStrided(void const *h_base, std::uint64_t stride, std::uint32_t len,
+                      std::uint64_t n, std::uint16_t *h_out, bool final_chksum,
+                      std::uint64_t *ticket) {
+        return aipstack_chksum_engine_submit_strided(
+            m_engine, h_base, stride, len, n, h_out, final_chksum ? AIPSTACK_CHKSUM_FINAL : 0u,
+            ticket);
+    }
+    int submitCsr(void const *h_base, std::uint64_t const *h_offsets, std::uint64_t n,
+                  std::uint16_t *h_out, bool final_chksum, std::uint64_t *ticket) {
+        return aipstack_chksum_engine_submit_csr(m_engine, h_base, h_offsets, n, h_out,
+                                                 final_chksum ? AIPSTACK_CHKSUM_FINAL : 0u,
+                                                 ticket);
+    }
+    int submitRxVerify(void const *h_frames, std::uint64_t const *h_offsets, std::uint64_t n,
+                       std::uint8_t *h_verdict, std::uint64_t *ticket) {
+        return aipstack_chksum_engine_submit_rx_verify(m_engine, h_frames, h_offsets, n,
+                                                       h_verdict, ticket);
+    }
+    int submitTxFill(void *h_frames, std::uint64_t const *h_offsets, std::uint64_t n,
+                     std::uint8_t *h_status, std::uint64_t *ticket) {
+        return aipstack_chksum_engine_submit_tx_fill(m_engine, h_frames, h_offsets, n,
+                                                     h_status, ticket);
+    }
+    // 0 = complete, 1 = still running, < 0 = error of that batch
+    int poll(std::uint64_t ticket) { return aipstack_chksum_engine_poll(m_engine, ticket); }
+    int wait(std::uint64_t ticket) { return aipstack_chksum_engine_wait(m_engine, ticket); }
+
+private:
+    aipstack_chksum_engine *m_engine = nullptr;
+    int m_status = AIPSTACK_CHKSUM_EINVAL;
 };
 
 }  // namespace AIpStackAmd

@@ -11,6 +11,7 @@
 #include <random>
 #include <vector>
 
+#include "aipstack_amd/Chksum.hpp"
 #include "aipstack_amd/chksum.h"
 #include "aipstack_amd/synth.h"
 #include "chksum_oracle.h"
@@ -137,6 +138,7 @@ int main() {
         std::vector<unsigned char> want_fr(fh), got_fr(fh.size());
         std::vector<uint8_t> want_st(nf), got_st(nf);
         oracle_tx_fill_batch(want_fr.data(), foff3.data(), nf, want_st.data());
+        const std::vector<uint8_t> want_st_fill(want_st);
         for (int split = 0; split < 2; split++) {
             HIP_OK(hipMemcpy(dfr, fh.data(), fh.size(), hipMemcpyHostToDevice));
             st = split ? aipstack_chksum_tx_fill_split(dfr, dfoff, nf, dst, dws, ws, stream)
@@ -159,6 +161,33 @@ int main() {
         EXPECT(got_st == want_st, "rx_verify: verdicts differ from the oracle");
         EXPECT(aipstack_chksum_tx_fill_split(dfr, dfoff, nf, dst, dws, ws - 8, stream) ==
                    AIPSTACK_CHKSUM_EINVAL, "split fill: short workspace accepted");
+        // the same frames from host memory through the engine (C++ mirror, Chksum.hpp):
+        // filled in place, then verified; synchronously and through submit/wait
+        {
+            AIpStackAmd::HostChksumEngine eng(0, 1 << 20, 3);
+            EXPECT(eng.valid(), "engine create failed %d", eng.createStatus());
+            std::vector<unsigned char> hf(fh);
+            std::vector<uint8_t> hst(nf, 0xEE), hv(nf);
+            EXPECT(eng.txFill(hf.data(), foff3.data(), nf, hst.data()) == 0, "engine tx fill failed");
+            EXPECT(hf == want_fr && hst == want_st_fill,
+                   "engine tx fill: frames or statuses differ from the oracle");
+            std::vector<unsigned char> hf2(fh);
+            uint64_t t1 = 0, t2 = 0;
+            EXPECT(eng.registerMemory(hf2.data(), hf2.size()) == 0, "register failed");
+            EXPECT(eng.submitTxFill(hf2.data(), foff3.data(), nf, hst.data(), &t1) == 0,
+                   "engine submit tx fill failed");
+            EXPECT(eng.wait(t1) == 0 && hf2 == want_fr, "engine submitted tx fill differs");
+            EXPECT(eng.submitRxVerify(hf2.data(), foff3.data(), nf, hv.data(), &t2) == 0,
+                   "engine submit rx verify failed");
+            while (eng.poll(t2) == 1) {
+            }
+            std::vector<uint8_t> want_v(nf);
+            oracle_rx_verify_batch(want_fr.data(), foff3.data(), nf, want_v.data());
+            EXPECT(eng.wait(t2) == 0 && hv == want_v, "engine rx verify differs from the oracle");
+            EXPECT(eng.unregisterMemory(hf2.data()) == 0, "unregister failed");
+            AIpStackAmd::HostChksumEngine moved(std::move(eng));
+            EXPECT(moved.valid() && !eng.valid(), "engine move");
+        }
         HIP_OK(hipFree(dfr));
         HIP_OK(hipFree(dfoff));
         HIP_OK(hipFree(dst));
