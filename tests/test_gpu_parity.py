@@ -395,6 +395,27 @@ def test_bench_two_ranks_one_gpu():
     assert min(per["GiB_s"]) > 0 and min(per["kernel_us"]) > 0
 
 
+def test_bench_e2e_tx_two_ranks_one_gpu():
+    """bench.py --e2e --config TX under torchrun with 2 ranks (each its own frame shard in
+    host memory, filled in place through its engine): one JSON line, rank 0 bit-exact."""
+    import json
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, AIPSTACK_BENCH_FORCE_DEVICE="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
+           "--e2e", "--config", "TX", "--steps", "2", "--warmup", "1"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["parity"] == "bit-exact" and d["value"] > 0
+    assert d["metric"].startswith("GiB/s Tx-filled end-to-end")
+
+
 # ---- host-memory streaming engine (SURVEY 8(f) row 4) ------------------------------------
 
 @pytest.mark.parametrize("register", [False, True])
