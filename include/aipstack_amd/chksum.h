@@ -232,8 +232,9 @@ int aipstack_chksum_engine_submit_rx_verify(aipstack_chksum_engine *engine, cons
  * (tap/linux/TapDeviceLinux.cpp:122-127): the frames go to the device, the Tx fill's read
  * pass computes each frame's record (aipstack_chksum_tx_fill_records), 8 bytes per frame come
  * back, and the engine writes the IPv4 header and L4 checksum fields into the caller's
- * frames IN PLACE and h_status[i] (as aipstack_chksum_tx_fill) when the batch completes. A
- * submitted batch's frames, offsets and statuses must stay valid until then. */
+ * frames IN PLACE and h_status[i] (as aipstack_chksum_tx_fill) when the batch completes (poll
+ * or wait). A submitted batch's frames, offsets and statuses must stay valid until then; one
+ * still pending when the engine is destroyed is left partly filled. */
 int aipstack_chksum_engine_host_tx_fill(aipstack_chksum_engine *engine, void *h_base,
                                         const uint64_t *h_offsets, uint64_t n,
                                         uint8_t *h_status);
