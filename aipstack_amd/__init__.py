@@ -28,12 +28,18 @@ from .chksum import (  # noqa: E402
     chksum_batch_csr,
     chksum_batch_seeded_csr,
     chksum_batch_strided,
+    contract_violations,
     device_check,
+    VIOLATION_CHUNK_LEN,
+    VIOLATION_PACKET_LEN,
+    VIOLATION_SPAN,
     flatten_chains,
     ipBufProcessBytes,
     RX_VERDICTS,
     rx_verify,
     tx_fill,
+    tx_fill_records,
+    apply_tx_records,
 )
 
 LIB_PATH = _lib.LIB_PATH
@@ -44,5 +50,7 @@ __all__ = [
     "ChksumError",
     "IpBufNode", "IpBufRef", "IpChksum", "IpChksumAccumulator", "IpChksumInverted",
     "chksum_batch_chain", "chksum_chain_fill", "chksum_batch_csr", "chksum_batch_seeded_csr", "flatten_chains", "chksum_batch_strided", "device_check",
-    "ipBufProcessBytes", "LIB_PATH", "RX_VERDICTS", "rx_verify", "tx_fill",
+    "ipBufProcessBytes", "LIB_PATH", "RX_VERDICTS", "rx_verify", "tx_fill", "tx_fill_records",
+    "apply_tx_records", "contract_violations", "VIOLATION_CHUNK_LEN", "VIOLATION_PACKET_LEN",
+    "VIOLATION_SPAN",
 ]

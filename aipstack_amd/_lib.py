@@ -41,6 +41,7 @@ SIGNATURES = {
     "aipstack_chksum_abi_version": (_c_int, []),
     "aipstack_chksum_tune": (_c_int, [ctypes.c_char_p, _c_int]),
     "aipstack_chksum_launch_shape": (_c_int, [_c_u64, _c_int, _c_int, _c_vp, _c_vp]),
+    "aipstack_chksum_contract_violations": (_c_int, [_c_int, ctypes.POINTER(_c_u32), _c_int]),
     "aipstack_chksum_engine_create": (_c_int, [_c_int, _c_u64, _c_int, ctypes.POINTER(_c_vp)]),
     "aipstack_chksum_engine_destroy": (None, [_c_vp]),
     "aipstack_chksum_engine_register": (_c_int, [_c_vp, _c_vp, _c_u64]),

@@ -254,13 +254,17 @@ def _torch():
     return torch
 
 
-def _stream_handle(stream) -> int:
+def _stream_handle(stream, like=None) -> int:
+    """The raw hipStream_t of `stream`; for None, torch's current stream of `like`'s device
+    (a tensor), so every wrapper launches on the stream of the device its data lives on."""
     torch = _torch()
-    if stream is None:  # torch's current stream on the current device, as a raw handle
+    if stream is None:  # torch's current stream, as a raw handle
+        dev = like.device.index if like is not None and like.device.index is not None \
+            else torch.cuda.current_device()
         raw = getattr(torch._C, "_cuda_getCurrentRawStream", None)
         if raw is not None:  # skips building a Stream object per call (small batches)
-            return int(raw(torch.cuda.current_device()))
-        stream = torch.cuda.current_stream()
+            return int(raw(dev))
+        stream = torch.cuda.current_stream(dev)
     return int(stream.cuda_stream) if hasattr(stream, "cuda_stream") else int(stream)
 
 
@@ -305,7 +309,7 @@ def chksum_batch_strided(buf, stride: int, length: int, n: int, *, out=None,
     out = _out_tensor(out, n, buf)
     st = _lib.load().aipstack_chksum_batch_strided(
         buf.data_ptr() + byte_offset, stride, length, n, out.data_ptr(),
-        AIPSTACK_CHKSUM_FINAL if final else 0, _stream_handle(stream))
+        AIPSTACK_CHKSUM_FINAL if final else 0, _stream_handle(stream, buf))
     _check(st, "aipstack_chksum_batch_strided")
     return out
 
@@ -322,7 +326,7 @@ def chksum_batch_csr(buf, offsets, *, out=None, final: bool = False, stream=None
     out = _out_tensor(out, n, buf)
     st = _lib.load().aipstack_chksum_batch_csr(
         buf.data_ptr(), offsets.data_ptr(), n, out.data_ptr(),
-        AIPSTACK_CHKSUM_FINAL if final else 0, _stream_handle(stream))
+        AIPSTACK_CHKSUM_FINAL if final else 0, _stream_handle(stream, buf))
     _check(st, "aipstack_chksum_batch_csr")
     return out
 
@@ -343,7 +347,7 @@ def chksum_batch_seeded_csr(buf, offsets, states, *, out=None, stream=None):
     out = _out_tensor(out, n, buf)
     st = _lib.load().aipstack_chksum_batch_seeded_csr(
         buf.data_ptr(), offsets.data_ptr(), states.data_ptr(), n, out.data_ptr(),
-        _stream_handle(stream))
+        _stream_handle(stream, buf))
     _check(st, "aipstack_chksum_batch_seeded_csr")
     return out
 
@@ -391,6 +395,7 @@ class ChksumEngine:
         self._registered.append(arr)
 
     def unregister(self, arr: np.ndarray) -> None:
+        """Unpin `arr`; batches still in flight are completed first (C engine)."""
         _check(self._lib.aipstack_chksum_engine_unregister(self._h, arr.ctypes.data),
                "aipstack_chksum_engine_unregister")
         self._registered = [a for a in self._registered if a is not arr]
@@ -430,8 +435,7 @@ class ChksumEngine:
         st = self._lib.aipstack_chksum_engine_submit_strided(
             self._h, buf.ctypes.data, stride, length, n, out.ctypes.data,
             AIPSTACK_CHKSUM_FINAL if final else 0, ctypes.byref(t))
-        self._keep(t.value, buf, out)
-        _check(st, "aipstack_chksum_engine_submit_strided")
+        self._submitted(st, t.value, "aipstack_chksum_engine_submit_strided", buf, out)
         return t.value, out
 
     def submit_csr(self, buf: np.ndarray, offsets: np.ndarray, *, out=None,
@@ -446,14 +450,23 @@ class ChksumEngine:
         st = self._lib.aipstack_chksum_engine_submit_csr(
             self._h, buf.ctypes.data, o.ctypes.data, max(n, 0), out.ctypes.data,
             AIPSTACK_CHKSUM_FINAL if final else 0, ctypes.byref(t))
-        self._keep(t.value, buf, out)
-        _check(st, "aipstack_chksum_engine_submit_csr")
+        self._submitted(st, t.value, "aipstack_chksum_engine_submit_csr", buf, o, out)
         return t.value, out
 
     def _keep(self, ticket, *arrays):
         # the buffers the GPU and the completion still use stay alive until completion
         if ticket:
             self._inflight[ticket] = arrays
+
+    def _submitted(self, st, ticket, where, *arrays):
+        """After a submit_* C call: keep the arrays of a batch in flight, or, if the submit
+        failed part-way, complete the pieces it did enqueue (they still read `arrays` and,
+        for Tx, write into the frames) before raising."""
+        if st != AIPSTACK_CHKSUM_OK:
+            if ticket:
+                self._lib.aipstack_chksum_engine_wait(self._h, ticket)
+            raise ChksumError(st, where)
+        self._keep(ticket, *arrays)
 
     def poll(self, ticket: int) -> bool:
         """True once batch `ticket` is complete (its `out` filled); False while running."""
@@ -495,8 +508,7 @@ class ChksumEngine:
         st = self._lib.aipstack_chksum_engine_submit_rx_verify(
             self._h, frames.ctypes.data, o.ctypes.data, max(n, 0), out.ctypes.data,
             ctypes.byref(t))
-        self._keep(t.value, frames, out)
-        _check(st, "aipstack_chksum_engine_submit_rx_verify")
+        self._submitted(st, t.value, "aipstack_chksum_engine_submit_rx_verify", frames, o, out)
         return t.value, out
 
     @staticmethod
@@ -530,8 +542,7 @@ class ChksumEngine:
             self._h, frames.ctypes.data, o.ctypes.data, max(n, 0), status.ctypes.data,
             ctypes.byref(t))
         # the completion reads the offsets again (it writes the fields into the frames)
-        self._keep(t.value, frames, o, status)
-        _check(st, "aipstack_chksum_engine_submit_tx_fill")
+        self._submitted(st, t.value, "aipstack_chksum_engine_submit_tx_fill", frames, o, status)
         return t.value, status
 
     def csr(self, buf: np.ndarray, offsets: np.ndarray, *, out=None,
@@ -572,7 +583,7 @@ def chksum_batch_chain(chunk_addr, chunk_len, chunk_index, states=None, *, out=N
     out = _out_tensor(out, n, chunk_index)
     st = _lib.load().aipstack_chksum_batch_chain(
         chunk_addr.data_ptr(), chunk_len.data_ptr(), chunk_index.data_ptr(), sp or None, n,
-        out.data_ptr(), AIPSTACK_CHKSUM_FINAL if final else 0, _stream_handle(stream))
+        out.data_ptr(), AIPSTACK_CHKSUM_FINAL if final else 0, _stream_handle(stream, chunk_index))
     _check(st, "aipstack_chksum_batch_chain")
     return out
 
@@ -606,7 +617,7 @@ def chksum_chain_fill(chunk_addr, chunk_len, chunk_index, states, fields, *, out
     st = _lib.load().aipstack_chksum_batch_chain_fill(
         chunk_addr.data_ptr(), chunk_len.data_ptr(), chunk_index.data_ptr(), sp or None,
         fields.data_ptr(), n, out.data_ptr(), AIPSTACK_CHKSUM_ZERO_AS_FFFF if zero_as_ffff else 0,
-        _stream_handle(stream))
+        _stream_handle(stream, chunk_index))
     _check(st, "aipstack_chksum_batch_chain_fill")
     return out
 
@@ -631,7 +642,7 @@ def rx_verify(frames, offsets, *, out=None, stream=None):
     n = offsets.numel() - 1
     out = _u8_out(out, max(n, 0), frames)
     _check(_lib.load().aipstack_chksum_rx_verify(frames.data_ptr(), offsets.data_ptr(), n,
-                                                 out.data_ptr(), _stream_handle(stream)),
+                                                 out.data_ptr(), _stream_handle(stream, frames)),
            "aipstack_chksum_rx_verify")
     return out
 
@@ -661,7 +672,7 @@ def tx_fill(frames, offsets, *, out=None, stream=None, split=None, workspace=Non
         split = n >= TX_SPLIT_MIN_FRAMES
     if not split:
         _check(lib.aipstack_chksum_tx_fill(frames.data_ptr(), offsets.data_ptr(), n,
-                                           out.data_ptr(), _stream_handle(stream)),
+                                           out.data_ptr(), _stream_handle(stream, frames)),
                "aipstack_chksum_tx_fill")
         return out
     torch = _torch()
@@ -683,6 +694,54 @@ def tx_fill(frames, offsets, *, out=None, stream=None, split=None, workspace=Non
     # the launch stream are done with it (it may not be torch's current stream).
     workspace.record_stream(launch_stream)
     return out
+
+
+def tx_fill_records(frames, offsets, *, out=None, stream=None):
+    """The split Tx fill's read pass alone (``aipstack_chksum_tx_fill_records``): one 8-byte
+    record per frame, nothing written into the frames. Record i = ``w0 | w1 << 32`` with
+    ``w0`` = IPv4 header checksum | L4 checksum << 16 and ``w1`` = L4 field offset (bits
+    0-7) | write the IPv4 field (8) | write the L4 field (9) | status (16-23); the host
+    applies them (:func:`apply_tx_records`). Returns the records (int64 device tensor)."""
+    torch = _torch()
+    _require_device(frames, "frames")
+    _require_offsets(offsets)
+    _same_device(frames, offsets, "frames and offsets")
+    n = max(offsets.numel() - 1, 0)
+    if out is None:
+        out = torch.empty(n, dtype=torch.int64, device=frames.device)
+    else:
+        _require_device(out, "out")
+        if out.element_size() != 8 or out.numel() < n:
+            raise ValueError("out must be a 64-bit device tensor with >= n elements")
+        _same_device(out, frames, "out and frames")
+    _check(_lib.load().aipstack_chksum_tx_fill_records(frames.data_ptr(), offsets.data_ptr(), n,
+                                                       out.data_ptr(), _stream_handle(stream, frames)),
+           "aipstack_chksum_tx_fill_records")
+    return out
+
+
+def apply_tx_records(frames: np.ndarray, offsets: np.ndarray, records: np.ndarray,
+                     status: Optional[np.ndarray] = None) -> np.ndarray:
+    """Apply Tx fill records (:func:`tx_fill_records`) to frames in HOST memory (numpy, in
+    place), as the engine's completion does: the IPv4 header checksum big-endian at frame
+    byte 24, the L4 checksum at the record's field offset, each when its flag is set.
+    Returns the per-frame statuses (uint8)."""
+    rec = np.ascontiguousarray(records).view(np.uint64)
+    o = np.ascontiguousarray(offsets, dtype=np.uint64)[:rec.size]
+    w0 = (rec & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+    w1 = (rec >> np.uint64(32)).astype(np.uint32)
+    if status is None:
+        status = np.empty(rec.size, dtype=np.uint8)
+    status[:rec.size] = (w1 >> 16) & 0xFF
+    flat = frames.reshape(-1).view(np.uint8)
+    for flag, at, val in ((0x100, o + np.uint64(24), w0 & 0xFFFF),
+                          (0x200, o + (w1 & 0xFF).astype(np.uint64), w0 >> 16)):
+        sel = (w1 & flag) != 0
+        a = at[sel].astype(np.int64)
+        v = val[sel]
+        flat[a] = (v >> 8).astype(np.uint8)
+        flat[a + 1] = (v & 0xFF).astype(np.uint8)
+    return status
 
 
 RX_VERDICTS = {0: "NOT_IP4", 1: "DROP_IP_MALFORMED", 2: "DROP_IP_CHKSUM", 3: "FRAGMENT",
@@ -711,6 +770,20 @@ def flatten_chains(refs, host_base: np.ndarray, device_base: int):
         index.append(len(addrs))
     return (np.array(addrs, dtype=np.uint64), np.array(lens, dtype=np.uint32),
             np.array(index, dtype=np.uint64))
+
+
+VIOLATION_PACKET_LEN = 1
+VIOLATION_CHUNK_LEN = 2
+VIOLATION_SPAN = 4
+
+
+def contract_violations(device: int = 0, clear: bool = True) -> int:
+    """Sticky contract-violation bits (VIOLATION_*) the kernels met on `device` since the
+    last clear (``aipstack_chksum_contract_violations``; waits for the device to go idle)."""
+    m = ctypes.c_uint32(0)
+    _check(_lib.load().aipstack_chksum_contract_violations(device, ctypes.byref(m), int(clear)),
+           "aipstack_chksum_contract_violations")
+    return int(m.value)
 
 
 def device_check(device: int = 0) -> int:

@@ -20,6 +20,17 @@ constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 4;
 constexpr int kBlock = kWave * kWavesPerBlock;
 
+// Contract violations seen by this translation unit's kernels on this device: sticky bits
+// (AIPSTACK_CHKSUM_VIOLATION_*, chksum.h), read and cleared from the host through
+// aipstack_chksum_contract_violations(). Each .hip file has its own copy (anonymous
+// namespace); the host side reads them all. Set only on the rare path, with a vector atomic.
+__device__ uint32_t g_violations;
+
+__device__ __forceinline__ void note_violation(bool bad, uint32_t bit) {
+    if (__builtin_amdgcn_ballot_w64(bad) != 0 && bad)
+        __hip_atomic_fetch_or(&g_violations, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // ---------------------------------------------------------------------------------
 // Packet descriptors. A wave walks 64-packet chunks; per chunk the descriptor may fetch
 // per-lane data (lane j <-> packet j of the chunk), then gives

@@ -19,11 +19,20 @@
 // works on the previous batch. Each slot (stream + staging) carries the ticket of the
 // batch piece it holds; a submit that needs a busy slot first completes that slot's piece
 // (back-pressure after nstreams pieces in flight).
+//
+// Errors are kept per ticket: a piece that fails (at enqueue or at completion, whichever
+// call completes it) records its status against its own batch's ticket until that ticket
+// is completed by _poll / _wait, so a failure is never reported for, nor hidden from,
+// another batch. Destroy completes every piece still in flight as _wait would (results
+// delivered, Tx fields applied) before it frees anything.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cstdint>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <new>
 #include <thread>
@@ -55,6 +64,7 @@ struct Slot {
     const uint64_t *tx_offs = nullptr;
     uint8_t *tx_status = nullptr;
     uint64_t ticket = 0;           // batch this slot's piece belongs to
+    uint64_t seq = 0;              // piece number within the engine (1, 2, ...)
 };
 
 struct Region {
@@ -72,8 +82,10 @@ struct aipstack_chksum_engine {
     std::vector<Region> registered;
     size_t next_slot = 0;      // round robin over the slots, across batches
     uint64_t next_ticket = 1;  // tickets are never 0
-    uint64_t failed_ticket = 0;  // most recent batch a completion error was seen for
-    int failed_status = 0;
+    uint64_t pieces = 0;       // pieces enqueued so far (Slot::seq)
+    // tickets with a failed piece -> the first failure's status, until the ticket is
+    // completed (poll / wait) or the engine is destroyed
+    std::map<uint64_t, int> failed;
     std::mutex mu;  // serialises the calls on one engine
 };
 
@@ -84,6 +96,20 @@ bool is_registered(const aipstack_chksum_engine *e, const void *p, uint64_t byte
     for (const Region &r : e->registered)
         if (c >= r.p && c + bytes <= r.p + r.bytes) return true;
     return false;
+}
+
+#ifdef AIPSTACK_ENGINE_FAULT_INJECTION
+// Test builds only (tests/cpp): make chosen pieces fail, at their launch or at their
+// completion, as a HIP error would. Bit k-1 of a mask = piece k (Slot::seq), k <= 64.
+std::atomic<uint64_t> g_fail_at_launch{0}, g_fail_at_completion{0};
+std::atomic<uint64_t> g_wait_delay_us{0};  // _wait sleeps this long outside the engine lock
+bool injected(const std::atomic<uint64_t> &mask, uint64_t seq) {
+    return seq >= 1 && seq <= 64 && ((mask.load() >> (seq - 1)) & 1u);
+}
+#endif
+
+void record_failure(aipstack_chksum_engine *e, uint64_t ticket, int status) {
+    e->failed.emplace(ticket, status);  // the first failure of a batch is kept
 }
 
 void release(aipstack_chksum_engine *e) {
@@ -184,6 +210,9 @@ int drain(aipstack_chksum_engine *e, Slot &s, bool blocking = true) {
         r = hipEventQuery(s.done);
         if (r == hipErrorNotReady) return 1;
     }
+#ifdef AIPSTACK_ENGINE_FAULT_INJECTION
+    if (r == hipSuccess && injected(g_fail_at_completion, s.seq)) r = hipErrorLaunchFailure;
+#endif
     const int st = check_hip(r);
     if (st == AIPSTACK_CHKSUM_OK && s.tx_frames) {
         apply_tx_records(reinterpret_cast<const uint64_t *>(s.h_out), s.tx_frames, s.tx_offs,
@@ -191,8 +220,7 @@ int drain(aipstack_chksum_engine *e, Slot &s, bool blocking = true) {
     } else if (st == AIPSTACK_CHKSUM_OK) {
         std::memcpy(s.user_out, s.h_out, s.count * s.out_elem);
     } else {
-        e->failed_ticket = s.ticket;
-        e->failed_status = st;
+        record_failure(e, s.ticket, st);
     }
     s.busy = false;
     return st;
@@ -213,7 +241,15 @@ int enqueue(aipstack_chksum_engine *e, uint64_t n, void *h_out, uint32_t elem, C
     while (i0 < n && status == AIPSTACK_CHKSUM_OK) {
         Slot &s = e->slots[e->next_slot];
         e->next_slot = (e->next_slot + 1) % e->slots.size();
-        (void)drain(e, s);  // an earlier piece (this batch's or an older one's) completes
+        // An earlier piece (this batch's or an older one's) completes; its failure is
+        // recorded against its own ticket. One of this batch's own pieces failing ends
+        // the enqueue (the rest would be wasted work).
+        const uint64_t prev = s.ticket;
+        const int ds = drain(e, s);
+        if (ds < 0 && prev == t) {
+            status = ds;
+            break;
+        }
         s.tx_frames = nullptr;  // a Tx fill's launch sets it again
         uint64_t i1 = 0;
         const char *src = nullptr;
@@ -228,6 +264,11 @@ int enqueue(aipstack_chksum_engine *e, uint64_t n, void *h_out, uint32_t elem, C
         if (bytes)
             status = check_hip(hipMemcpyAsync(s.d_bytes, h_src, bytes, hipMemcpyHostToDevice,
                                               s.stream));
+        s.seq = ++e->pieces;
+#ifdef AIPSTACK_ENGINE_FAULT_INJECTION
+        if (status == AIPSTACK_CHKSUM_OK && injected(g_fail_at_launch, s.seq))
+            status = AIPSTACK_CHKSUM_EHIP;
+#endif
         if (status == AIPSTACK_CHKSUM_OK) status = launch(s, i0, i1);
         if (status == AIPSTACK_CHKSUM_OK)
             status = check_hip(hipMemcpyAsync(s.h_out, s.d_out, cnt * elem,
@@ -240,15 +281,12 @@ int enqueue(aipstack_chksum_engine *e, uint64_t n, void *h_out, uint32_t elem, C
         s.ticket = t;
         i0 = i1;
     }
-    if (status != AIPSTACK_CHKSUM_OK) {
-        e->failed_ticket = t;
-        e->failed_status = status;
-    }
+    if (status != AIPSTACK_CHKSUM_OK) record_failure(e, t, status);
     return status;
 }
 
 // Complete batch `ticket`: 0 = done (results in place), 1 = still running (non-blocking
-// only), < 0 = it failed.
+// only), < 0 = it failed (its first failure; the record is consumed).
 int complete(aipstack_chksum_engine *e, uint64_t ticket, bool blocking) {
     if (ticket == 0 || ticket >= e->next_ticket) return AIPSTACK_CHKSUM_EINVAL;
     if (hipSetDevice(e->device) != hipSuccess) return AIPSTACK_CHKSUM_ENODEV;
@@ -258,8 +296,18 @@ int complete(aipstack_chksum_engine *e, uint64_t ticket, bool blocking) {
         const int st = drain(e, s, blocking);
         if (st == 1) pending = 1;
     }
-    if (e->failed_ticket == ticket) return e->failed_status;
-    return pending;
+    if (pending) return 1;
+    const auto it = e->failed.find(ticket);
+    if (it == e->failed.end()) return AIPSTACK_CHKSUM_OK;
+    const int st = it->second;
+    e->failed.erase(it);
+    return st;
+}
+
+// Every piece in flight, completed as _wait completes it (results delivered, Tx records
+// applied); failures stay recorded.
+void drain_all(aipstack_chksum_engine *e) {
+    for (Slot &s : e->slots) (void)drain(e, s, true);
 }
 
 }  // namespace
@@ -302,8 +350,12 @@ extern "C" int aipstack_chksum_engine_create(int device, uint64_t chunk_bytes, i
 
 extern "C" void aipstack_chksum_engine_destroy(aipstack_chksum_engine *e) {
     if (!e) return;
-    (void)hipSetDevice(e->device);
-    release(e);  // waits for every stream: pieces still in flight finish, unreported
+    {
+        std::lock_guard<std::mutex> lock(e->mu);
+        (void)hipSetDevice(e->device);
+        drain_all(e);  // pieces in flight complete: results written, Tx fields applied
+    }
+    release(e);
     delete e;
 }
 
@@ -323,6 +375,8 @@ extern "C" int aipstack_chksum_engine_unregister(aipstack_chksum_engine *e, void
     for (size_t i = 0; i < e->registered.size(); ++i) {
         if (e->registered[i].p == host_ptr) {
             (void)hipSetDevice(e->device);
+            // pieces in flight may still DMA from (or, Tx, complete into) the region
+            drain_all(e);
             const int st = check_hip(hipHostUnregister(host_ptr));
             e->registered.erase(e->registered.begin() + (long)i);
             return st;
@@ -471,9 +525,35 @@ extern "C" int aipstack_chksum_engine_poll(aipstack_chksum_engine *e, uint64_t t
 
 extern "C" int aipstack_chksum_engine_wait(aipstack_chksum_engine *e, uint64_t ticket) {
     if (!e) return AIPSTACK_CHKSUM_EINVAL;
+    // The long part -- the GPU finishing the batch -- is waited for without the engine
+    // lock, so _poll and _submit from other threads go on meanwhile. A slot drained (and
+    // re-used) by another thread in between has delivered its piece already; its event then
+    // only makes this wait a little longer.
+    std::vector<hipEvent_t> events;
+    {
+        std::lock_guard<std::mutex> lock(e->mu);
+        if (ticket == 0 || ticket >= e->next_ticket) return AIPSTACK_CHKSUM_EINVAL;
+        for (const Slot &s : e->slots)
+            if (s.busy && s.ticket == ticket) events.push_back(s.done);
+    }
+#ifdef AIPSTACK_ENGINE_FAULT_INJECTION
+    if (const uint64_t us = g_wait_delay_us.load())  // a long GPU wait, made deterministic
+        std::this_thread::sleep_for(std::chrono::microseconds(us));
+#endif
+    for (hipEvent_t ev : events) (void)hipEventSynchronize(ev);
     std::lock_guard<std::mutex> lock(e->mu);
     return complete(e, ticket, true);
 }
+
+#ifdef AIPSTACK_ENGINE_FAULT_INJECTION
+// Test builds only: pieces (engine-wide numbering from 1) that fail at launch / completion.
+extern "C" void aipstack_chksum_engine_test_inject(uint64_t fail_at_launch,
+                                                    uint64_t fail_at_completion) {
+    g_fail_at_launch = fail_at_launch;
+    g_fail_at_completion = fail_at_completion;
+}
+extern "C" void aipstack_chksum_engine_test_wait_delay(uint64_t us) { g_wait_delay_us = us; }
+#endif
 
 extern "C" int aipstack_chksum_engine_host_strided(aipstack_chksum_engine *e, const void *h_base,
                                                    uint64_t stride, uint32_t len, uint64_t n,

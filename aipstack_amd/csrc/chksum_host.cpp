@@ -5,10 +5,10 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstddef>
 #include <cstdint>
 #include <cstring>
-#include <mutex>
 
 #include "aipstack_amd/chksum.h"
 #include "chksum_internal.h"
@@ -27,16 +27,27 @@ int check_hip(hipError_t e) {
     return AIPSTACK_CHKSUM_EHIP;
 }
 
-int device_cu_count() {
+int device_cu_count(hipStream_t stream) {
+    // Keyed by the device the launch stream belongs to (a stream of device 1 launched
+    // while device 0 is current sizes its grid for device 1). Any thread may launch, so
+    // the cache entries are atomics; two threads filling one entry store the same value.
     constexpr int kMaxDev = 64;
-    static int cache[kMaxDev] = {0};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0) return -1;
-    if (dev < kMaxDev && cache[dev] > 0) return cache[dev];
+    static std::atomic<int> cache[kMaxDev];
+    hipDevice_t dev = -1;
+    if (stream != nullptr) {
+        if (hipStreamGetDevice(stream, &dev) != hipSuccess) return -1;
+    } else if (hipGetDevice(&dev) != hipSuccess) {
+        return -1;
+    }
+    if (dev < 0) return -1;
+    if (dev < kMaxDev) {
+        const int c = cache[dev].load(std::memory_order_relaxed);
+        if (c > 0) return c;
+    }
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
         return -1;
-    if (dev < kMaxDev) cache[dev] = cus;
+    if (dev < kMaxDev) cache[dev].store(cus, std::memory_order_relaxed);
     return cus;
 }
 
@@ -68,4 +79,20 @@ extern "C" int aipstack_chksum_device_check(int device) {
     if (e != hipSuccess) return check_hip(e);
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return AIPSTACK_CHKSUM_ENODEV;
     return AIPSTACK_CHKSUM_OK;
+}
+
+extern "C" int aipstack_chksum_contract_violations(int device, uint32_t *mask, int clear) {
+    if (!mask) return AIPSTACK_CHKSUM_EINVAL;
+    const int dc = aipstack_chksum_device_check(device);
+    if (dc != AIPSTACK_CHKSUM_OK) return dc;
+    int prev = 0;
+    if (hipGetDevice(&prev) != hipSuccess) prev = device;
+    int st = check_hip(hipSetDevice(device));
+    if (st == AIPSTACK_CHKSUM_OK) st = check_hip(hipDeviceSynchronize());
+    uint32_t m = 0;
+    if (st == AIPSTACK_CHKSUM_OK) st = take_violations_batch(&m, clear != 0);
+    if (st == AIPSTACK_CHKSUM_OK) st = take_violations_frames(&m, clear != 0);
+    (void)hipSetDevice(prev);
+    if (st == AIPSTACK_CHKSUM_OK) *mask = m;
+    return st;
 }

@@ -9,8 +9,19 @@ namespace aipstack_amd {
 // Records `e` as this thread's last HIP error and maps it to a status code.
 int check_hip(hipError_t e);
 
-// Compute units of the current device (cached per device id); <= 0 on failure.
-int device_cu_count();
+// Compute units of the device `stream` belongs to (the current device for the null
+// stream), cached per device id; <= 0 on failure.
+int device_cu_count(hipStream_t stream);
+
+// Whether a Tx frame launch takes its header segments from the stream (as Rx does) instead
+// of per-lane header loads (tunable "tx_gather": 0 never, 1 always, else automatic = for
+// the records-only read pass, whose output is not followed by in-place field stores).
+bool tuning_tx_gather(bool records_only);
+
+// The contract-violation word of each kernel translation unit on the current device:
+// OR it into *mask, clear it if `clear`.
+int take_violations_batch(uint32_t *mask, bool clear);
+int take_violations_frames(uint32_t *mask, bool clear);
 
 // Frames a wave of the Rx-verify / Tx-fill kernels keeps in flight (tunable "frames":
 // 2, 4 or 8; default 4).

@@ -79,6 +79,9 @@ __global__ __launch_bounds__(kBlock) void chksum_batch_kernel(Desc desc, uint64_
         uint64_t lS, lE;
         desc.lane_bounds(chunk, lane, lS, lE);
         if (lane >= cnt) lE = lS;  // past the batch: empty
+        if constexpr (Desc::kCsr)  // len > 65535 or E < S: outside the contract (chksum.h)
+            note_violation(lE - lS > (uint64_t)AIPSTACK_CHKSUM_MAX_LEN,
+                           AIPSTACK_CHKSUM_VIOLATION_PACKET_LEN);
         // lane j: exact halves-sum of packet j (0 iff all its bytes are 0)
         uint32_t sums = 0;
         bool streamed = false;
@@ -214,6 +217,11 @@ __global__ __launch_bounds__(kBlock, 5) void chksum_chain_kernel(
                 a = chunk_addr[k];
                 l = chunk_len[k];
             }
+            // a chunk over 65535 bytes (outside the contract) is summed as empty: the
+            // gathered stream's compact indices (24 bits) then cannot overflow, so no load
+            // leaves the chunks
+            note_violation(l > AIPSTACK_CHKSUM_MAX_LEN, AIPSTACK_CHKSUM_VIOLATION_CHUNK_LEN);
+            if (l > AIPSTACK_CHKSUM_MAX_LEN) l = 0;
             // which chain: the last chain starting at or before this chunk
             mark[lane] = -1;
             __builtin_amdgcn_wave_barrier();
@@ -280,6 +288,8 @@ struct Tuning {
                                           // issued together (2, 4, 8); -1 = off
     std::atomic<int> chunk_packets{0};    // packets per chunk (1, 2, 4, ..., 64); 0 = by
                                           // batch size (pick_shape)
+    std::atomic<int> tx_gather{-1};       // Tx header segments from the stream: 0 never,
+                                          // 1 always, else for the records-only read pass
 
     Tuning() {
         auto env = [](const char *k, std::atomic<int> &v) {
@@ -293,6 +303,7 @@ struct Tuning {
         env("AIPSTACK_CHKSUM_FRAMES", frames);
         env("AIPSTACK_CHKSUM_STREAM", stream);
         env("AIPSTACK_CHKSUM_CHUNK_PACKETS", chunk_packets);
+        env("AIPSTACK_CHKSUM_TX_GATHER", tx_gather);
 
     }
 };
@@ -372,7 +383,7 @@ template <class Desc, int U, int P, bool NT, bool SEEDED, int SU>
 int launch_k(const Desc &desc, uint64_t n, const Shape &sh, uint16_t *d_out, uint32_t flags,
              hipStream_t stream) {
     const uint64_t nchunks = (n + sh.chunk_packets - 1) / sh.chunk_packets;
-    const int cus = device_cu_count();
+    const int cus = device_cu_count(stream);
     if (cus <= 0) return AIPSTACK_CHKSUM_EHIP;
     uint64_t cpw = (uint64_t)tuning().chunks_per_wave.load(std::memory_order_relaxed);
     if (cpw == 0) {
@@ -427,7 +438,7 @@ template <class Desc, bool SEEDED>
 int launch(const Desc &desc, uint64_t n, uint32_t max_len, uint16_t *d_out, uint32_t flags,
            hipStream_t stream) {
     if (n == 0) return AIPSTACK_CHKSUM_OK;
-    const int cus = device_cu_count();
+    const int cus = device_cu_count(stream);
     if (cus <= 0) return AIPSTACK_CHKSUM_EHIP;
     const Shape sh = pick_shape(n, cus);
     switch (pick_unroll(max_len)) {
@@ -443,7 +454,7 @@ template <bool NT, int SU>
 int launch_chain(const uint64_t *d_addr, const uint32_t *d_len, const uint64_t *d_index,
                  const uint32_t *d_states, const uint64_t *d_fields, uint64_t n,
                  uint16_t *d_out, uint32_t flags, hipStream_t stream) {
-    const int cus = device_cu_count();
+    const int cus = device_cu_count(stream);
     if (cus <= 0) return AIPSTACK_CHKSUM_EHIP;
     const uint32_t cpg = pick_shape(n, cus).chunk_packets;  // chains per group
     const uint64_t nchunks = (n + cpg - 1) / cpg;
@@ -468,6 +479,18 @@ int launch_chain(const uint64_t *d_addr, const uint32_t *d_len, const uint64_t *
 
 }  // namespace
 
+int take_violations_batch(uint32_t *mask, bool clear) {
+    uint32_t v = 0;
+    int st = check_hip(hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_violations), sizeof(v)));
+    if (st != AIPSTACK_CHKSUM_OK) return st;
+    *mask |= v;
+    if (clear && v) {
+        const uint32_t z = 0;
+        st = check_hip(hipMemcpyToSymbol(HIP_SYMBOL(g_violations), &z, sizeof(z)));
+    }
+    return st;
+}
+
 int tuning_waves_per_cu() {
     return tuning().waves_per_cu.load(std::memory_order_relaxed);
 }
@@ -480,6 +503,11 @@ int tuning_stream_windows(int family_default) {
 }
 
 uint32_t frames_per_chunk(uint64_t n, int cus) { return pick_shape(n, cus).chunk_packets; }
+
+bool tuning_tx_gather(bool records_only) {
+    const int t = tuning().tx_gather.load(std::memory_order_relaxed);
+    return t == 0 ? false : t == 1 ? true : records_only;
+}
 
 int tuning_frames_in_flight() {
     const int f = tuning().frames.load(std::memory_order_relaxed);
@@ -536,6 +564,7 @@ extern "C" int aipstack_chksum_tune(const char *key, int value) {
     else if (!std::strcmp(key, "frames")) t.frames = value;
     else if (!std::strcmp(key, "stream")) t.stream = value;
     else if (!std::strcmp(key, "chunk_packets")) t.chunk_packets = value;
+    else if (!std::strcmp(key, "tx_gather")) t.tx_gather = value;
     else return AIPSTACK_CHKSUM_EINVAL;
     return AIPSTACK_CHKSUM_OK;
 }

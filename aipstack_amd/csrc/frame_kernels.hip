@@ -317,9 +317,6 @@ constexpr uint32_t kGatherWindows = 128;
 #ifndef AIPSTACK_FRAME_NT  // experiments: 0 = the frame stream loads with the default policy
 #define AIPSTACK_FRAME_NT 1
 #endif
-#ifndef AIPSTACK_FRAME_GATHER_TX  // Tx keeps per-lane header loads
-#define AIPSTACK_FRAME_GATHER_TX 0
-#endif
 constexpr uint32_t kHdrSlots = kWave * kHdrSegs;  // at most 8 segments per frame
 
 struct FrameLds {
@@ -407,7 +404,9 @@ __device__ __forceinline__ uint32_t l4s_below(const u32x4 (&seg)[kHdrSegs], uint
 #ifndef AIPSTACK_FRAME_PREFETCH
 #define AIPSTACK_FRAME_PREFETCH(SU) ((SU) / 2)
 #endif
-template <bool TX, int U, int P, bool NT, int SU>
+// GATHER: header segments captured from the stream (Rx always; Tx when no in-place field
+// stores follow the pass -- the records-only read pass, launch_frames).
+template <bool TX, int U, int P, bool NT, int SU, bool GATHER>
 __device__ __forceinline__ FrameOut process_chunk(const CsrDesc &desc, uint64_t p0, uint64_t n,
                                                   uint32_t cpk, int lane, uint32_t voff,
                                                   uint32_t not_lane0, FrameLds *lds,
@@ -418,7 +417,10 @@ __device__ __forceinline__ FrameOut process_chunk(const CsrDesc &desc, uint64_t 
     uint64_t S, E;
     desc.lane_bounds(chunk, lane, S, E);
     const uint64_t l64 = E - S;
-    const int len = (lane >= cnt || l64 >= (1ull << 31)) ? 0 : (int)l64;  // 0: NOT_IP4
+    // a frame over 65535 bytes (or E < S) is outside the contract: NOT_IP4, reported
+    const bool too_long = l64 > (uint64_t)AIPSTACK_CHKSUM_MAX_LEN;
+    note_violation(lane < cnt && too_long, AIPSTACK_CHKSUM_VIOLATION_PACKET_LEN);
+    const int len = (lane >= cnt || too_long) ? 0 : (int)l64;  // 0: NOT_IP4
     // (B) headers: aligned segments [A0_j, A0_j + 112) through one range-checked
     // descriptor over the chunk's aligned span (never past the 16-byte blocks holding
     // the chunk's bytes; slots past it read 0). A span beyond what 64 frames of at most
@@ -426,8 +428,10 @@ __device__ __forceinline__ FrameOut process_chunk(const CsrDesc &desc, uint64_t 
     const uint64_t base = (__builtin_amdgcn_readfirstlane((uint32_t)S) & ~15u) |
                           ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(S >> 32)) << 32);
     const uint64_t span = ((desc.base + chunk.end_off + 15u) & ~(uint64_t)15) - base;
+    const bool span_bad = span > (uint64_t)kWave * 65536u + 16u;
+    note_violation(span_bad && lane == 0, AIPSTACK_CHKSUM_VIOLATION_SPAN);
     const uint32_t hrec = __builtin_amdgcn_readfirstlane(
-        span > (uint64_t)kWave * 65536u + 16u ? 0u : (uint32_t)span);  // uniform: SGPR descriptor
+        span_bad ? 0u : (uint32_t)span);  // uniform: SGPR descriptor
     const __amdgpu_buffer_rsrc_t hrsrc = __builtin_amdgcn_make_buffer_rsrc(
         reinterpret_cast<void *>(base), (short)0, hrec, 0x00020000);
     const uint32_t hoff = (uint32_t)((S & ~(uint64_t)15) - base);
@@ -453,7 +457,7 @@ __device__ __forceinline__ FrameOut process_chunk(const CsrDesc &desc, uint64_t 
              << 32) |
             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)E, lastl);
         const uint32_t nseg = ((uint32_t)(X1 - base) + 15u) >> 4;
-        if ((!TX || AIPSTACK_FRAME_GATHER_TX) && ((nseg + 63u) >> 6) <= kGatherWindows) {
+        if (GATHER && ((nseg + 63u) >> 6) <= kGatherWindows) {
             // (B'+C') one pass: the stream gives H at every frame's aligned start A0_j and
             // hands the header segments to LDS; the parse runs on them after the stream.
             const uint64_t A0 = S & ~(uint64_t)15;
@@ -619,7 +623,7 @@ __device__ __forceinline__ FrameOut process_chunk(const CsrDesc &desc, uint64_t 
 #ifndef AIPSTACK_FRAME_WAVES_PER_SIMD  // occupancy the register budget is fitted to
 #define AIPSTACK_FRAME_WAVES_PER_SIMD 4
 #endif
-template <bool TX, int U, int P, bool NT, int SU, bool SPLIT>
+template <bool TX, int U, int P, bool NT, int SU, bool SPLIT, bool GATHER>
 __global__ __launch_bounds__(kBlock, AIPSTACK_FRAME_WAVES_PER_SIMD) void frame_kernel(CsrDesc desc, uint64_t n,
                                                        uint32_t chunks_per_wave,
                                                        uint32_t chunk_packets,
@@ -634,14 +638,14 @@ __global__ __launch_bounds__(kBlock, AIPSTACK_FRAME_WAVES_PER_SIMD) void frame_k
     const uint64_t c_end = min(c + chunks_per_wave, nchunks);
     const uint32_t voff = (uint32_t)lane * 16u;
     const uint32_t not_lane0 = lane == 0 ? 0u : ~0u;
-    constexpr bool kGather = SU > 0 && (!TX || AIPSTACK_FRAME_GATHER_TX);
+    constexpr bool kGather = SU > 0 && GATHER;
     __shared__ FrameLds lds[kGather ? kWavesPerBlock : 1];  // 9 KiB per wave (gathered stream)
     FrameLds *my = &lds[kGather ? wave_in_block : 0];
     for (; c < c_end; ++c) {
         const uint64_t p0 = c * cpk;
         int cnt;
-        const FrameOut o = process_chunk<TX, U, P, NT, SU>(desc, p0, n, (uint32_t)cpk, lane, voff,
-                                                           not_lane0, my, cnt);
+        const FrameOut o = process_chunk<TX, U, P, NT, SU, GATHER>(
+            desc, p0, n, (uint32_t)cpk, lane, voff, not_lane0, my, cnt);
         if (lane < cnt) {
             if constexpr (SPLIT)
 #if AIPSTACK_EXP_NO_RECORDS  // experiment: price of the record stores (wrong output)
@@ -655,16 +659,13 @@ __global__ __launch_bounds__(kBlock, AIPSTACK_FRAME_WAVES_PER_SIMD) void frame_k
     }
 }
 
-template <bool TX, bool SPLIT = false>
-int launch_frames(const void *d_base, const uint64_t *d_offsets, uint64_t n, uint8_t *d_status,
-                  uint64_t *d_records, hipStream_t stream, bool scatter = true) {
-    const int cus = device_cu_count();
-    if (cus <= 0) return AIPSTACK_CHKSUM_EHIP;
+template <bool TX, bool SPLIT, bool GATHER>
+int launch_frames_g(const CsrDesc &desc, uint64_t n, uint8_t *d_status, uint64_t *d_records,
+                    hipStream_t stream, int cus) {
     // small batches: fewer frames per chunk, so that they spread over many waves (as the
     // checksum batches, chksum_kernels.hip pick_shape)
     const uint32_t cpk = frames_per_chunk(n, cus);
     const uint64_t nchunks = (n + cpk - 1) / cpk;
-    CsrDesc desc{(uint64_t)(uintptr_t)d_base, d_offsets};
     const int su = tuning_stream_windows(8);  // measured: 8 > 4 > off > 2 (RX and TX)
     const int wpc = tuning_waves_per_cu();
     const uint64_t target_waves = (uint64_t)cus * (wpc > 0 ? wpc : 128);
@@ -674,8 +675,9 @@ int launch_frames(const void *d_base, const uint64_t *d_offsets, uint64_t n, uin
     const uint64_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
     if (blocks > 0x7FFFFFFFull || cpw > 0xFFFFFFFFull) return AIPSTACK_CHKSUM_EINVAL;
 #define AIPSTACK_LAUNCH_FRAMES(P, SU)                                                          \
-    hipLaunchKernelGGL((frame_kernel<TX, 2, P, AIPSTACK_FRAME_NT != 0, SU, SPLIT>), dim3((unsigned)blocks),        \
-                       dim3(kBlock), 0, stream, desc, n, (uint32_t)cpw, cpk, d_status, d_records)
+    hipLaunchKernelGGL((frame_kernel<TX, 2, P, AIPSTACK_FRAME_NT != 0, SU, SPLIT, GATHER>),   \
+                       dim3((unsigned)blocks), dim3(kBlock), 0, stream, desc, n, (uint32_t)cpw, \
+                       cpk, d_status, d_records)
 #define AIPSTACK_LAUNCH_FRAMES_SU(P)              \
     switch (su) {                                 \
         case 0: AIPSTACK_LAUNCH_FRAMES(P, 0); break; \
@@ -690,17 +692,53 @@ int launch_frames(const void *d_base, const uint64_t *d_offsets, uint64_t n, uin
     }
 #undef AIPSTACK_LAUNCH_FRAMES_SU
 #undef AIPSTACK_LAUNCH_FRAMES
-    if (SPLIT && scatter) {
-        const int st = check_hip(hipGetLastError());
-        if (st != AIPSTACK_CHKSUM_OK) return st;
-        const uint64_t sblocks = min((n + kBlock - 1) / kBlock, (uint64_t)cus * 64);
-        hipLaunchKernelGGL(tx_scatter_kernel, dim3((unsigned)sblocks), dim3(kBlock), 0, stream,
-                           desc.base, d_offsets, d_records, d_status, n);
-    }
     return check_hip(hipGetLastError());
 }
 
+// Rx verify; Tx fill in one pass; the split fill's read pass (SPLIT), followed by the
+// scatter pass unless `scatter` is false (the records-only call). Where the header segments
+// come from (GATHER): Rx and the records-only pass capture them from the stream; a fill
+// that writes the fields in place keeps per-lane header loads, whose default cache policy
+// leaves the field lines in the Infinity Cache for the in-place stores.
+template <bool TX, bool SPLIT = false>
+int launch_frames(const void *d_base, const uint64_t *d_offsets, uint64_t n, uint8_t *d_status,
+                  uint64_t *d_records, hipStream_t stream, bool scatter = true) {
+    const int cus = device_cu_count(stream);
+    if (cus <= 0) return AIPSTACK_CHKSUM_EHIP;
+    CsrDesc desc{(uint64_t)(uintptr_t)d_base, d_offsets};
+    int st;
+    if constexpr (TX) {
+        if (tuning_tx_gather(SPLIT && !scatter))
+            st = launch_frames_g<true, SPLIT, true>(desc, n, d_status, d_records, stream, cus);
+        else
+            st = launch_frames_g<true, SPLIT, false>(desc, n, d_status, d_records, stream, cus);
+    } else {
+        st = launch_frames_g<false, SPLIT, true>(desc, n, d_status, d_records, stream, cus);
+    }
+    if (st != AIPSTACK_CHKSUM_OK) return st;
+    if (SPLIT && scatter) {
+        const uint64_t sblocks = min((n + kBlock - 1) / kBlock, (uint64_t)cus * 64);
+        hipLaunchKernelGGL(tx_scatter_kernel, dim3((unsigned)sblocks), dim3(kBlock), 0, stream,
+                           desc.base, d_offsets, d_records, d_status, n);
+        return check_hip(hipGetLastError());
+    }
+    return AIPSTACK_CHKSUM_OK;
+}
+
 }  // namespace
+
+int take_violations_frames(uint32_t *mask, bool clear) {
+    uint32_t v = 0;
+    int st = check_hip(hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_violations), sizeof(v)));
+    if (st != AIPSTACK_CHKSUM_OK) return st;
+    *mask |= v;
+    if (clear && v) {
+        const uint32_t z = 0;
+        st = check_hip(hipMemcpyToSymbol(HIP_SYMBOL(g_violations), &z, sizeof(z)));
+    }
+    return st;
+}
+
 }  // namespace aipstack_amd
 
 using namespace aipstack_amd;

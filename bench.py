@@ -44,6 +44,8 @@ CONFIGS = {
     # SURVEY 8(f) rows 2-3 (not BASELINE metric lines): raw Ethernet frames
     "RX": ("rx", 1 << 20, None),
     "TX": ("tx", 1 << 20, None),
+    # the split fill's read pass alone (aipstack_chksum_tx_fill_records): the E2E Tx kernel
+    "TXREC": ("txrec", 1 << 20, None),
     # chained + seeded (TCP Tx shape)
     "CHAIN": ("chain", 1 << 20, None),
 }
@@ -58,6 +60,9 @@ WORKLOAD_NAMES = {
           "Rx verify: IPv4 header + L4 checksum verdicts",
     "TX": "1M raw Ethernet frames per GPU (same mix), Tx fill: IPv4 header + L4 checksums "
           "written in place",
+    "TXREC": "1M raw Ethernet frames per GPU (same mix), Tx fill records: the split fill's read "
+             "pass alone (8-B record per frame: both checksums, field offset, flags, status; "
+             "nothing written into the frames)",
     "CHAIN": "1M TCP-Tx-shaped chains per GPU: IpChksumAccumulator(pseudo-header State)"
              ".getChksum(20B header node + 1460B payload in 2 chunks split at a random point)",
 }
@@ -137,7 +142,7 @@ def shard_spec(config, rank, world, n=None):
         spec["payload"] = n * plen
         spec["byte_offset"] = rank * n * stride
         spec["offsets"] = None
-    elif layout in ("rx", "tx", "chain"):
+    elif layout in ("rx", "tx", "txrec", "chain"):
         # each rank synthesises its own frames / chains (seed per rank): they are independent
         spec["seed"] = synth.SEED_DATA + 1000 * rank
         spec["byte_offset"] = 0
@@ -154,7 +159,7 @@ def shard_spec(config, rank, world, n=None):
 def host_shard(spec):
     """The shard's bytes in host memory (numpy), exactly as the device generators make them."""
     from aipstack_amd import synth
-    if spec["layout"] in ("rx", "tx"):
+    if spec["layout"] in ("rx", "tx", "txrec"):
         buf, off = synth.frames_host(spec["n"], seed=spec["seed"], max_payload=1460)
         spec["offsets"], spec["total"] = off, int(off[-1])
         if spec["layout"] == "rx":  # valid frames: fill with the oracle (test infrastructure)
@@ -174,11 +179,14 @@ def host_shard(spec):
 
 def algorithmic_bytes(layout, n, total_payload):
     """L bytes read + 2 bytes written per packet (+8 B offset for CSR).
-    Frames: L read + 8 B offset + 1 B verdict/status (+ 4 B of checksums written, Tx).
+    Frames: L read + 8 B offset + 1 B verdict/status (+ 4 B of checksums written, Tx);
+    Tx records: L read + 8 B offset + 8 B record written.
     Chains: chunk bytes + 12 B (address, length) per chunk + 8 B index + 4 B state + 2 B
     result per chain (3 chunks per chain here)."""
     if layout == "chain":
         return total_payload + 3 * 12 * n + 8 * (n + 1) + 4 * n + 2 * n
+    if layout == "txrec":
+        return total_payload + 16 * n + 8
     if layout in ("rx", "tx"):
         return total_payload + 9 * n + 8 + (4 * n if layout == "tx" else 0)
     b = total_payload + 2 * n
@@ -501,12 +509,13 @@ def main():
 
     # ---- this rank's shard, generated in place (global packets [rank*n, (rank+1)*n))
     spec = shard_spec(args.config, rank, world)
-    if layout in ("rx", "tx"):
+    if layout in ("rx", "tx", "txrec"):
         frames_host = host_shard(spec)          # frames are synthesised on the host
         buf = torch.from_numpy(frames_host).to(dev)
         d_off = torch.from_numpy(spec["offsets"]).to(dev)
         status = torch.empty(n, dtype=torch.uint8, device=dev)
         tx_ws = torch.empty(8 * n, dtype=torch.uint8, device=dev)  # split fill's records
+        records = torch.empty(n, dtype=torch.int64, device=dev)
     if layout == "chain":
         chain = make_chains(spec, dev)
         spec["total"] = chain["payload"]
@@ -530,6 +539,8 @@ def main():
             A.chksum_batch_csr(buf, d_off, out=out, stream=stream)
         elif layout == "rx":
             A.rx_verify(buf, d_off, out=status, stream=stream)
+        elif layout == "txrec":
+            A.tx_fill_records(buf, d_off, out=records, stream=stream)
         elif layout == "chain" and args.chain_fill:
             A.chksum_chain_fill(chain["addr"], chain["len"], chain["index"], chain["states"],
                                 chain["fields"], out=out, stream=stream)
@@ -593,30 +604,48 @@ def main():
     if layout == "chain" and args.chain_fill:
         alg += 10 * n  # + the field address read and the 2-byte field written per chain
 
-    # ---- parity of this run's output against the oracle / reference (rank 0 sample)
+    # ---- parity: EVERY rank checks its own shard (after the timed region) against the
+    # oracle / the reference; rank 0 also times the CPU baseline on its shard
     parity = None
     cpu = None
-    if rank == 0 and layout in ("rx", "tx"):
-        if not args.no_parity:
+    if layout in ("rx", "tx", "txrec"):
+        if not args.no_parity and layout == "txrec":
+            parity = records_check(spec, frames_host, buf.cpu().numpy(), records.cpu().numpy())
+        elif not args.no_parity:
             parity = frames_check(spec, frames_host, buf.cpu().numpy(), status.cpu().numpy())
-        if not args.no_cpu_baseline:
+        if rank == 0 and not args.no_cpu_baseline:
             cpu = cpu_baseline_frames(spec, frames_host)
-    elif rank == 0 and layout == "chain":
+    elif layout == "chain":
         if not args.no_parity:
             parity = (chain_fill_check(chain) if args.chain_fill
                       else chain_check(chain, out.cpu().numpy()))
-        if not args.no_cpu_baseline:
+        if rank == 0 and not args.no_cpu_baseline:
             cpu = cpu_baseline_chain(chain)
-    elif rank == 0:
-        # rank 0 times the CPU baseline on its own shard at every world size (after the
-        # timed region; the other ranks wait at the final barrier)
+    else:
         host_out = out.cpu().numpy()
-        if not args.no_cpu_baseline:
+        if rank == 0 and not args.no_cpu_baseline:
             cpu, want = cpu_baseline(spec)
             if not args.no_parity:
-                parity = "bit-exact" if np.array_equal(host_out, want) else "MISMATCH"
+                parity = ("bit-exact (whole shard vs reference)" if np.array_equal(host_out, want)
+                          else "MISMATCH")
         elif not args.no_parity:
-            parity = oracle_check(spec, host_out)
+            parity = oracle_check(spec, host_out, threads=max(1, _affinity_cores() // world))
+    # which device each rank ran on, gathered on the control plane with its parity
+    props = torch.cuda.get_device_properties(device)
+    mine_info = {"rank": rank, "device": device,
+                 "pci": f"{props.pci_domain_id:04x}:{props.pci_bus_id:02x}:{props.pci_device_id:02x}",
+                 "uuid": str(getattr(props, "uuid", "")), "arch": props.gcnArchName,
+                 "parity": parity}
+    infos = [None] * world
+    if world > 1:
+        dist.all_gather_object(infos, mine_info)
+    else:
+        infos = [mine_info]
+    if not args.no_parity:
+        bad = [i["rank"] for i in infos if not str(i["parity"]).startswith("bit-exact")]
+        parity = (f"bit-exact (each of {world} rank(s) checked its own shard: {parity})" if not bad
+                  else f"MISMATCH on rank(s) {bad}")
+    pcis = [i["pci"] for i in infos]
 
     bytes_all = payload * world  # weak scaling: every rank holds the same-size shard
     value = bytes_all * args.steps / max_elapsed / 2**30
@@ -667,6 +696,12 @@ def main():
             "GiB_s": [round(spec.get("payload", total) * args.steps / float(r[0]) / 2**30, 2)
                       for r in ranks],
             "kernel_us": [round(float(r[1]) * 1e6, 2) for r in ranks],
+            "devices": pcis,
+            "arch": [i["arch"] for i in infos],
+            "distinct_devices": len(set(pcis)) == world,
+            **({"note": "ranks share a device (AIPSTACK_BENCH_FORCE_DEVICE rehearsal): not a "
+                        "multi-GPU measurement"} if len(set(pcis)) != world else {}),
+            "parity": [i["parity"] for i in infos],
         },
         "cpu_baseline": cpu,
         "parity": parity,
@@ -675,7 +710,7 @@ def main():
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
-    if parity == "MISMATCH":
+    if parity is not None and parity.startswith("MISMATCH"):
         sys.exit(1)
 
 
@@ -809,7 +844,7 @@ def e2e(args, rank, world, local_rank, layout, n, plen):
         off, total = spec["offsets"], spec["total"]
     # Tx fill writes the frames in place: the fill ignores the fields' old contents, so
     # every step gives the same bytes; parity compares with the oracle's fill of a copy
-    orig = host.copy() if layout == "tx" and rank == 0 and not args.no_parity else None
+    orig = host.copy() if layout == "tx" and not args.no_parity else None
     out = np.empty(n, dtype=np.uint8 if frames else np.uint16)
     eng = A.ChksumEngine(int(os.environ.get("AIPSTACK_BENCH_FORCE_DEVICE", local_rank)),
                          chunk_bytes=args.e2e_chunk_mib << 20,
@@ -853,7 +888,7 @@ def e2e(args, rank, world, local_rank, layout, n, plen):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     max_elapsed = float(t.item())
     parity = None
-    if rank == 0 and not args.no_parity:
+    if not args.no_parity:  # every rank checks its own shard
         lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "libchksum_oracle.so"))
         want = np.empty(n, dtype=out.dtype)
         ok_bytes = True
@@ -878,6 +913,19 @@ def e2e(args, rank, world, local_rank, layout, n, plen):
             o = off.astype(np.uint64)
             lib.oracle_batch_csr(host.ctypes.data, o.ctypes.data, n, want.ctypes.data, 0)
         parity = "bit-exact" if ok_bytes and np.array_equal(out, want) else "MISMATCH"
+    dev_index = int(os.environ.get("AIPSTACK_BENCH_FORCE_DEVICE", local_rank))
+    props = torch.cuda.get_device_properties(dev_index)
+    mine_info = {"rank": rank, "parity": parity, "arch": props.gcnArchName,
+                 "pci": f"{props.pci_domain_id:04x}:{props.pci_bus_id:02x}:{props.pci_device_id:02x}"}
+    infos = [mine_info]
+    if world > 1:
+        infos = [None] * world
+        dist.all_gather_object(infos, mine_info)
+    if not args.no_parity:
+        bad = [i["rank"] for i in infos if i["parity"] != "bit-exact"]
+        parity = (f"bit-exact (each of {world} rank(s) checked its own shard vs oracle)" if not bad
+                  else f"MISMATCH on rank(s) {bad}")
+    pcis = [i["pci"] for i in infos]
     value = total * world * args.steps / max_elapsed / 2**30
     if rank == 0:
         print(json.dumps({
@@ -891,6 +939,9 @@ def e2e(args, rank, world, local_rank, layout, n, plen):
                        "host_memory": "pageable (CPU copy into pinned staging)"
                        if args.e2e_pageable else "registered (hipHostRegister, DMA direct)",
                        "streams": args.e2e_streams, "chunk_MiB": args.e2e_chunk_mib},
+            "per_gpu": {"devices": pcis, "arch": [i["arch"] for i in infos],
+                        "distinct_devices": len(set(pcis)) == world,
+                        "parity": [i["parity"] for i in infos]},
             **({"per_call_us": {"min": round(per_launch[0], 1),
                                 "median": round(per_launch[len(per_launch) // 2], 1),
                                 "max": round(per_launch[-1], 1)}} if per_launch else {}),
@@ -914,12 +965,50 @@ def frames_check(spec, frames_before, frames_after, status):
     return "bit-exact (verdicts/frames vs oracle)" if ok else "MISMATCH"
 
 
-def oracle_check(spec, got):
-    """Check this rank's whole output against the C oracle on the same bytes."""
-    host = host_shard(spec)
+def records_check(spec, frames_before, frames_after, records):
+    """Tx records: the frames must be untouched; the records applied to a host copy (as the
+    engine applies them) must give the oracle's Tx fill, statuses included."""
+    import aipstack_amd as A
     lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "libchksum_oracle.so"))
+    o = spec["offsets"].astype(np.uint64)
+    n = spec["n"]
+    want = np.empty(n, dtype=np.uint8)
+    lib.oracle_tx_fill_batch.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_uint64, ctypes.c_void_p]
+    ref = frames_before.copy()
+    lib.oracle_tx_fill_batch(ref.ctypes.data, o.ctypes.data, n, want.ctypes.data)
+    mine = frames_before.copy()
+    got = A.apply_tx_records(mine, o, records)
+    ok = (np.array_equal(frames_after, frames_before) and np.array_equal(got, want)
+          and np.array_equal(mine, ref))
+    return "bit-exact (records applied vs oracle Tx fill; frames untouched)" if ok else "MISMATCH"
+
+
+def oracle_check(spec, got, threads=1):
+    """Check this rank's whole output against the reference's own IpChksumInverted (oracle/_ref,
+    `threads` std::threads; where it was built) or else the C oracle, on the same bytes."""
+    host = host_shard(spec)
     n = spec["n"]
     want = np.empty(n, dtype=np.uint16)
+    ref_path = os.path.join(ROOT, "oracle", "_ref", "libref_chksum.so")
+    if os.path.exists(ref_path):
+        ref = ctypes.CDLL(ref_path)
+        if spec["layout"] == "strided":
+            ref.ref_time_batch_strided.restype = ctypes.c_double
+            ref.ref_time_batch_strided.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                                   ctypes.c_uint64, ctypes.c_uint32,
+                                                   ctypes.c_uint64, ctypes.c_void_p]
+            ref.ref_time_batch_strided(threads, 0, host.ctypes.data, spec["stride"], spec["plen"],
+                                       n, want.ctypes.data)  # 0 timed passes: one pass
+        else:
+            ref.ref_time_batch_csr.restype = ctypes.c_double
+            ref.ref_time_batch_csr.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                               ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+            o = spec["offsets"].astype(np.uint64)
+            ref.ref_time_batch_csr(threads, 0, host.ctypes.data, o.ctypes.data, n,
+                                   want.ctypes.data)
+        return ("bit-exact (whole shard vs reference)" if np.array_equal(got, want)
+                else "MISMATCH")
+    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "libchksum_oracle.so"))
     if spec["layout"] == "strided":
         lib.oracle_batch_strided.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
                                              ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32]

@@ -182,7 +182,14 @@ int aipstack_chksum_tx_fill_records(const void *d_base, const uint64_t *d_offset
  * copied into the engine's pinned staging. The host_* calls are synchronous; the submit_*
  * calls enqueue a batch and return a ticket at once, so the caller can fill its next batch
  * (e.g. read() frames into its ring) while the GPU works; _poll / _wait complete it. Calls
- * on one engine from several threads are serialised. */
+ * on one engine from several threads are serialised, except that _wait waits for the GPU
+ * without holding the engine: _poll and _submit_* from other threads proceed meanwhile (a
+ * _submit_* that needs a busy stream still waits for the piece on it).
+ *
+ * Errors are per batch: a piece that fails records its status against its own ticket,
+ * whichever call completes it, and _poll / _wait of that ticket return it (once). Destroy
+ * completes every piece still in flight as _wait would -- results written, Tx fields
+ * applied -- before freeing anything; so does _unregister before it unpins the region. */
 typedef struct aipstack_chksum_engine aipstack_chksum_engine;
 
 int aipstack_chksum_engine_create(int device, uint64_t chunk_bytes, int nstreams,
@@ -233,8 +240,8 @@ int aipstack_chksum_engine_submit_rx_verify(aipstack_chksum_engine *engine, cons
  * pass computes each frame's record (aipstack_chksum_tx_fill_records), 8 bytes per frame come
  * back, and the engine writes the IPv4 header and L4 checksum fields into the caller's
  * frames IN PLACE and h_status[i] (as aipstack_chksum_tx_fill) when the batch completes (poll
- * or wait). A submitted batch's frames, offsets and statuses must stay valid until then; one
- * still pending when the engine is destroyed is left partly filled. */
+ * or wait). A submitted batch's frames, offsets and statuses must stay valid until then (or
+ * until the engine is destroyed, which completes it). */
 int aipstack_chksum_engine_host_tx_fill(aipstack_chksum_engine *engine, void *h_base,
                                         const uint64_t *h_offsets, uint64_t n,
                                         uint8_t *h_status);
@@ -243,11 +250,27 @@ int aipstack_chksum_engine_submit_tx_fill(aipstack_chksum_engine *engine, void *
                                           uint8_t *h_status, uint64_t *ticket);
 
 /* Completion of a submitted batch: 0 = done (h_out holds the results), 1 = still running
- * (poll only), negative = it failed (or _EINVAL for an unknown ticket). _wait blocks. */
+ * (poll only), negative = one of its pieces failed (the first failure's status; h_out /
+ * the frames of the failed pieces are not written), or _EINVAL for a ticket never issued.
+ * _wait blocks. A ticket's failure is reported once; completing it again returns 0. */
 int aipstack_chksum_engine_poll(aipstack_chksum_engine *engine, uint64_t ticket);
 int aipstack_chksum_engine_wait(aipstack_chksum_engine *engine, uint64_t ticket);
 
 /* ---- diagnostics ------------------------------------------------------------------ */
+
+/* Contract violations the kernels met on a device since the last clear (sticky bits). The
+ * batch calls never fault on inputs outside their contract, but their results for the
+ * offending packets are unspecified; these bits say that it happened:
+ *   _PACKET_LEN  a CSR packet or frame longer than 65535 bytes, or offsets decreasing (its
+ *                result: the exact sum up to 2^26 bytes, else 0; frames: NOT_IP4)
+ *   _CHUNK_LEN   a chain chunk longer than 65535 bytes (summed as an empty chunk)
+ *   _SPAN        64 consecutive frames spanning more than 4 MiB (their headers read as 0)
+ * aipstack_chksum_contract_violations waits for the device to go idle (hipDeviceSynchronize),
+ * then stores the bits in *mask and clears them if `clear` is non-zero. */
+#define AIPSTACK_CHKSUM_VIOLATION_PACKET_LEN 1u
+#define AIPSTACK_CHKSUM_VIOLATION_CHUNK_LEN  2u
+#define AIPSTACK_CHKSUM_VIOLATION_SPAN       4u
+int aipstack_chksum_contract_violations(int device, uint32_t *mask, int clear);
 
 /* Static description of a status code. Never NULL. */
 const char *aipstack_chksum_strerror(int status);

@@ -102,6 +102,19 @@ class Oracle:
         return out
 
 
+def load_frame_ref_sets():
+    """(frame_ref_cases.json, {set name: (buf, offsets)}, the frame_ref module): the frame
+    batches the reference-composed fixtures cover, regenerated from their specs."""
+    import frame_ref
+    import make_golden
+    with open(os.path.join(GOLDEN, "frame_ref_cases.json")) as f:
+        doc = json.load(f)
+    sets, _ = make_golden.frame_sets()
+    mb, mo = sets["mix"]
+    sets["mix_filled"] = (make_golden.fill_and_corrupt(mb, mo, doc["mix"], frame_ref), mo)
+    return doc, sets, frame_ref
+
+
 @pytest.fixture(scope="session")
 def oracle():
     return Oracle()

@@ -103,6 +103,10 @@ int main() {
 
     const int dev = aipstack_chksum_device_check(0);
     CHECK(dev == 0 || dev == AIPSTACK_CHKSUM_ENODEV || dev == AIPSTACK_CHKSUM_EHIP);
+    std::uint32_t vmask = 0;
+    CHECK(aipstack_chksum_contract_violations(0, nullptr, 1) == EINVAL_);
+    CHECK(aipstack_chksum_contract_violations(-1, &vmask, 1) == AIPSTACK_CHKSUM_ENODEV);
+    CHECK(aipstack_chksum_contract_violations(0, &vmask, 1) == dev);
     const int ec = aipstack_chksum_engine_create(0, 0, 2, &e);
     if (dev == 0) {
         CHECK(ec == 0 && e != nullptr);

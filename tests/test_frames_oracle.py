@@ -182,3 +182,46 @@ def test_edge_frames_fill_then_verify(oracle):
     assert np.all(v[filled] == RX["ACCEPT"])
     # statuses other than ACCEPT are exactly the verdicts that stop before an L4 sum
     assert np.all(st[~filled] == v[~filled])
+
+
+# ---- the frame decisions pinned by the reference's own call sites -------------------------
+# tests/golden/frame_ref_cases.json: per frame, the answers of the reference stack's checksum
+# call sequences compiled against its Chksum.h/Buf.h (ref_cs_ip4_rx / _tcp_rx / _udp_rx /
+# _udp_tx / _icmp), composed by tests/golden/frame_ref.py. The C frame oracle must give the
+# same verdicts and write the same field values.
+
+@pytest.fixture(scope="module")
+def frame_ref_sets():
+    from conftest import load_frame_ref_sets
+    return load_frame_ref_sets()
+
+
+@pytest.mark.parametrize("name", ["edge", "mix", "mix_filled"])
+def test_frame_oracle_verdicts_match_reference_call_sites(frame_ref_sets, oracle, name):
+    doc, sets, fr = frame_ref_sets
+    buf, off = sets[name]
+    recs = doc[name]
+    assert len(recs) == off.size - 1
+    want = np.array([fr.verdict(buf[int(off[i]):int(off[i + 1])], r) for i, r in enumerate(recs)],
+                    dtype=np.uint8)
+    got = oracle.rx_verify_batch(buf, off)
+    assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
+    if name != "mix":
+        assert set(np.unique(want).tolist()) >= {2, 5, 6, 8}
+
+
+@pytest.mark.parametrize("name", ["edge", "mix", "mix_filled"])
+def test_frame_oracle_fill_matches_reference_call_sites(frame_ref_sets, oracle, name):
+    doc, sets, fr = frame_ref_sets
+    buf, off = sets[name]
+    filled = buf.copy()
+    oracle.tx_fill_batch(filled, off)
+    nfields = 0
+    want = buf.copy()
+    for i, r in enumerate(doc[name]):
+        s = int(off[i])
+        for at, v in fr.fill_fields(buf[s:int(off[i + 1])], r):
+            want[s + at], want[s + at + 1] = v >> 8, v & 0xFF
+            nfields += 1
+    assert nfields > len(doc[name])  # most frames get both fields
+    assert np.array_equal(filled, want), np.nonzero(filled != want)[0][:10]

@@ -27,6 +27,9 @@ import call_sites
 CPP = os.path.join(ROOT, "tests", "cpp")
 BUILD = os.path.join(CPP, "build")
 REF_EXT = os.path.join(ROOT, "oracle", "_ref", "ip_chksum_test_external")
+REF_HOOK_ONLY = os.path.join(ROOT, "oracle", "_ref", "ip_chksum_test_hook_only")
+HOOK_SO = os.path.join(ROOT, "aipstack_amd", "lib", "libaipstack_chksum_hook.so")
+HOOK_A = os.path.join(ROOT, "aipstack_amd", "lib", "libaipstack_chksum_hook.a")
 REF_LIB = os.path.join(ROOT, "oracle", "_ref", "libref_chksum.so")
 ASAN_ENV = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1",
                 UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
@@ -57,6 +60,36 @@ def test_reference_ip_chksum_test_on_our_hook():
     """/root/reference/tests/ip_chksum_test.cpp, unmodified, linked to our IpChksumInverted
     (Chksum.h:50-51): the 0x00FF chain known answer + 10 M random chain-vs-flat splits."""
     _run([REF_EXT], timeout=600)
+
+
+def test_hook_library_needs_no_rocm():
+    """libaipstack_chksum_hook.{so,a}: IpChksumInverted alone (host_hook.cc), for a stack
+    built with -DAIPSTACK_EXTERNAL_CHKSUM (Chksum.h:46-51) on a host without ROCm."""
+    subprocess.run(["make", "-C", os.path.join(ROOT, "aipstack_amd", "csrc")], check=True,
+                   stdout=subprocess.DEVNULL)
+    deps = _run(["ldd", HOOK_SO])
+    libs = [ln.split()[0] for ln in deps.splitlines() if ln.strip()]
+    assert not [l for l in libs if "hip" in l or "hsa" in l or "amd" in l or "rocm" in l], deps
+    assert all(l.startswith(("linux-vdso", "libc.so", "/lib64/ld-linux", "libstdc++", "libm.so",
+                             "libgcc_s")) for l in libs), deps
+    for lib in (HOOK_SO, HOOK_A):
+        syms = _run(["nm", "-D" if lib.endswith(".so") else "-g", "--defined-only", lib])
+        assert any(ln.split()[-1] == "IpChksumInverted" and " T " in ln
+                   for ln in syms.splitlines() if ln.strip()), lib
+    ctl = ctypes.CDLL(HOOK_SO)
+    ctl.IpChksumInverted.restype = ctypes.c_uint16
+    ctl.IpChksumInverted.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
+    assert ctl.IpChksumInverted(b"\xff\xff", 2) == 0xFFFF  # SURVEY 8(c) edge case
+
+
+@pytest.mark.skipif(not os.path.exists(REF_HOOK_ONLY),
+                    reason="reference test not built here (no /root/reference at build time)")
+def test_reference_ip_chksum_test_on_rocm_free_hook():
+    """The reference's own tests/ip_chksum_test.cpp linked to libaipstack_chksum_hook.so only
+    (no HIP runtime in the process)."""
+    deps = _run(["ldd", REF_HOOK_ONLY])
+    assert "amdhip" not in deps and "hsa-runtime" not in deps, deps
+    _run([REF_HOOK_ONLY], timeout=600)
 
 
 def test_repo_ip_chksum_test():

@@ -1,0 +1,46 @@
+#!/bin/bash
+# Round-3 GPU experiments, one mode per gpurun call; output under gpurun_out/r03/<mode>.
+# (Round 2 kept one script per call, tools/gpu_r02*.sh; they are folded into the modes of
+# this file and tools/measure_round.sh.)
+#   txrec   Tx records-only read pass: header capture (default) vs per-lane header loads
+#           (AIPSTACK_CHKSUM_TX_GATHER=0), interleaved; the split fill both ways; rocprof
+#           stats and FETCH/WRITE passes of TXREC; then pytest -m gpu
+#   check   pytest -m gpu, then bench A, C, CHAIN, TXREC, RX (no CPU baseline)
+set -e
+mode=${1:?mode}
+out=gpurun_out/r03/$mode
+mkdir -p "$out"
+export TMPDIR=/tmp
+
+bench() {  # bench NAME ARGS... -> $out/NAME.jsonl (appended)
+  name=$1; shift
+  timeout -k 10 300 python bench.py "$@" >> "$out/$name.jsonl" 2>> "$out/$name.err"
+}
+
+case $mode in
+txrec)
+  for i in 1 2; do
+    bench txrec --config TXREC --steps 100 --per-launch --no-cpu-baseline
+    AIPSTACK_CHKSUM_TX_GATHER=0 bench txrec_lane --config TXREC --steps 100 --per-launch --no-cpu-baseline
+    bench tx --config TX --steps 100 --per-launch --no-cpu-baseline
+    AIPSTACK_CHKSUM_TX_GATHER=1 bench tx_gather --config TX --steps 100 --per-launch --no-cpu-baseline
+  done
+  bench rx --config RX --steps 100 --per-launch --no-cpu-baseline
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/prof_TXREC" -o run \
+      -- python3 bench.py --config TXREC --no-cpu-baseline --no-parity > "$out/prof_TXREC.log" 2>&1
+  tools/pmc_run.sh TXREC "$out/pmc_TXREC"
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+      > "$out/pytest_gpu.log" 2>&1
+  ;;
+check)
+  # the GPU suite, then the timed configs the last change could move
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+      > "$out/pytest_gpu.log" 2>&1
+  for c in A C CHAIN TXREC RX; do
+    bench "bench_$c" --config $c --per-launch --no-cpu-baseline
+  done
+  ;;
+*)
+  echo "unknown mode $mode" >&2; exit 2 ;;
+esac
+echo "r03 $mode done"
