@@ -17,6 +17,7 @@ from .chksum import (  # noqa: E402
     AIPSTACK_CHKSUM_MAX_LEN,
     AIPSTACK_CHKSUM_OK,
     ChksumEngine,
+    ChksumEngineGroup,
     ChksumError,
     IpBufNode,
     IpBufRef,
@@ -27,6 +28,7 @@ from .chksum import (  # noqa: E402
     chksum_chain_fill,
     chksum_batch_csr,
     chksum_batch_seeded_csr,
+    chksum_batch_slotted,
     chksum_batch_strided,
     contract_violations,
     device_check,
@@ -37,8 +39,12 @@ from .chksum import (  # noqa: E402
     ipBufProcessBytes,
     RX_VERDICTS,
     rx_verify,
+    rx_verify_slotted,
+    slots_to_offsets,
     tx_fill,
     tx_fill_records,
+    tx_fill_records_slotted,
+    tx_fill_slotted,
     apply_tx_records,
 )
 
@@ -52,5 +58,6 @@ __all__ = [
     "chksum_batch_chain", "chksum_chain_fill", "chksum_batch_csr", "chksum_batch_seeded_csr", "flatten_chains", "chksum_batch_strided", "device_check",
     "ipBufProcessBytes", "LIB_PATH", "RX_VERDICTS", "rx_verify", "tx_fill", "tx_fill_records",
     "apply_tx_records", "contract_violations", "VIOLATION_CHUNK_LEN", "VIOLATION_PACKET_LEN",
-    "VIOLATION_SPAN",
+    "VIOLATION_SPAN", "chksum_batch_slotted", "rx_verify_slotted", "slots_to_offsets",
+    "tx_fill_records_slotted", "tx_fill_slotted", "ChksumEngineGroup",
 ]

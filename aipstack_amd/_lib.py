@@ -52,13 +52,36 @@ SIGNATURES = {
     "aipstack_chksum_engine_host_tx_fill": (_c_int, [_c_vp, _c_vp, _c_vp, _c_u64, _c_vp]),
     "aipstack_chksum_engine_submit_tx_fill": (_c_int, [_c_vp, _c_vp, _c_vp, _c_u64, _c_vp, _c_vp]),
     "aipstack_chksum_tx_fill_records": (_c_int, [_c_vp, _c_vp, _c_u64, _c_vp, _c_vp]),
+    "aipstack_chksum_batch_slotted": (_c_int, [_c_vp, _c_u64, _c_vp, _c_u64, _c_vp, _c_u32, _c_vp]),
+    "aipstack_chksum_rx_verify_slotted": (_c_int, [_c_vp, _c_u64, _c_vp, _c_u64, _c_vp, _c_vp]),
+    "aipstack_chksum_tx_fill_slotted": (_c_int, [_c_vp, _c_u64, _c_vp, _c_u64, _c_vp, _c_vp]),
+    "aipstack_chksum_tx_fill_records_slotted": (_c_int, [_c_vp, _c_u64, _c_vp, _c_u64, _c_vp, _c_vp]),
     "aipstack_chksum_engine_submit_rx_verify": (_c_int, [_c_vp, _c_vp, _c_vp, _c_u64, _c_vp, _c_vp]),
     "aipstack_chksum_engine_submit_strided": (_c_int, [_c_vp, _c_vp, _c_u64, _c_u32, _c_u64, _c_vp,
                                                        _c_u32, ctypes.POINTER(_c_u64)]),
     "aipstack_chksum_engine_submit_csr": (_c_int, [_c_vp, _c_vp, _c_vp, _c_u64, _c_vp, _c_u32,
                                                    ctypes.POINTER(_c_u64)]),
+    "aipstack_chksum_engine_host_slotted": (_c_int, [_c_vp, _c_vp, _c_u64, _c_vp, _c_u64, _c_vp, _c_u32]),
+    "aipstack_chksum_engine_submit_slotted": (_c_int, [_c_vp, _c_vp, _c_u64, _c_vp, _c_u64, _c_vp, _c_u32,
+                                                       ctypes.POINTER(_c_u64)]),
+    "aipstack_chksum_engine_host_rx_verify_slotted": (_c_int, [_c_vp, _c_vp, _c_u64, _c_vp, _c_u64, _c_vp]),
+    "aipstack_chksum_engine_submit_rx_verify_slotted": (_c_int, [_c_vp, _c_vp, _c_u64, _c_vp, _c_u64,
+                                                                 _c_vp, ctypes.POINTER(_c_u64)]),
+    "aipstack_chksum_engine_host_tx_fill_slotted": (_c_int, [_c_vp, _c_vp, _c_u64, _c_vp, _c_u64, _c_vp]),
+    "aipstack_chksum_engine_submit_tx_fill_slotted": (_c_int, [_c_vp, _c_vp, _c_u64, _c_vp, _c_u64,
+                                                               _c_vp, ctypes.POINTER(_c_u64)]),
     "aipstack_chksum_engine_poll": (_c_int, [_c_vp, _c_u64]),
     "aipstack_chksum_engine_wait": (_c_int, [_c_vp, _c_u64]),
+    "aipstack_chksum_engine_group_create": (_c_int, [_c_vp, _c_int, _c_u64, _c_int, ctypes.POINTER(_c_vp)]),
+    "aipstack_chksum_engine_group_destroy": (None, [_c_vp]),
+    "aipstack_chksum_engine_group_size": (_c_int, [_c_vp]),
+    "aipstack_chksum_engine_group_register": (_c_int, [_c_vp, _c_vp, _c_u64]),
+    "aipstack_chksum_engine_group_unregister": (_c_int, [_c_vp, _c_vp]),
+    "aipstack_chksum_engine_group_host_strided": (_c_int, [_c_vp, _c_vp, _c_u64, _c_u32, _c_u64, _c_vp,
+                                                           _c_u32, _c_vp]),
+    "aipstack_chksum_engine_group_host_csr": (_c_int, [_c_vp, _c_vp, _c_vp, _c_u64, _c_vp, _c_u32, _c_vp]),
+    "aipstack_chksum_engine_group_host_rx_verify": (_c_int, [_c_vp, _c_vp, _c_vp, _c_u64, _c_vp, _c_vp]),
+    "aipstack_chksum_engine_group_host_tx_fill": (_c_int, [_c_vp, _c_vp, _c_vp, _c_u64, _c_vp, _c_vp]),
     # synth.h
     "aipstack_synth_fill_host": (None, [_c_vp, _c_u64, _c_u64, _c_u64]),
     "aipstack_synth_mixed_offsets_host": (_c_u64, [_c_vp, _c_u64, _c_u64]),

@@ -331,6 +331,68 @@ def chksum_batch_csr(buf, offsets, *, out=None, final: bool = False, stream=None
     return out
 
 
+def _require_lens(lens, n_slots_bytes, slot_stride, buf):
+    torch = _torch()
+    _require_device(lens, "lens")
+    if lens.dtype not in (torch.int32, torch.uint32):
+        raise ValueError("lens must be an int32/uint32 device tensor")
+    _same_device(buf, lens, "buf and lens")
+    if slot_stride <= 0 or lens.numel() * slot_stride > n_slots_bytes:
+        raise ValueError("buf must hold n whole slots of slot_stride bytes")
+    return lens.numel()
+
+
+def chksum_batch_slotted(buf, slot_stride: int, lens, *, out=None, final: bool = False,
+                         stream=None):
+    """Ring slots on the GPU: ``out[i] = IpChksumInverted(buf[i*slot_stride:][:lens[i]])``
+    (``IpChksum`` with ``final=True``). ``lens``: int32/uint32 device tensor of n lengths,
+    each <= min(slot_stride, 65535); ``buf`` holds n whole slots."""
+    _require_device(buf, "buf")
+    n = _require_lens(lens, buf.numel() * buf.element_size(), slot_stride, buf)
+    out = _out_tensor(out, n, buf)
+    _check(_lib.load().aipstack_chksum_batch_slotted(
+        buf.data_ptr(), slot_stride, lens.data_ptr(), n, out.data_ptr(),
+        AIPSTACK_CHKSUM_FINAL if final else 0, _stream_handle(stream, buf)),
+        "aipstack_chksum_batch_slotted")
+    return out
+
+
+def rx_verify_slotted(frames, slot_stride: int, lens, *, out=None, stream=None):
+    """Rx verify of a ring of frame slots on the GPU (frame i = the lens[i] bytes at
+    frames[i*slot_stride:]); one AIPSTACK_RX_* verdict per frame."""
+    _require_device(frames, "frames")
+    n = _require_lens(lens, frames.numel() * frames.element_size(), slot_stride, frames)
+    out = _u8_out(out, n, frames)
+    _check(_lib.load().aipstack_chksum_rx_verify_slotted(
+        frames.data_ptr(), slot_stride, lens.data_ptr(), n, out.data_ptr(),
+        _stream_handle(stream, frames)), "aipstack_chksum_rx_verify_slotted")
+    return out
+
+
+def tx_fill_slotted(frames, slot_stride: int, lens, *, out=None, stream=None):
+    """Tx fill, in place, of a ring of frame slots on the GPU; one status per frame."""
+    _require_device(frames, "frames")
+    n = _require_lens(lens, frames.numel() * frames.element_size(), slot_stride, frames)
+    out = _u8_out(out, n, frames)
+    _check(_lib.load().aipstack_chksum_tx_fill_slotted(
+        frames.data_ptr(), slot_stride, lens.data_ptr(), n, out.data_ptr(),
+        _stream_handle(stream, frames)), "aipstack_chksum_tx_fill_slotted")
+    return out
+
+
+def tx_fill_records_slotted(frames, slot_stride: int, lens, *, out=None, stream=None):
+    """The Tx records (see :func:`tx_fill_records`) of a ring of frame slots."""
+    torch = _torch()
+    _require_device(frames, "frames")
+    n = _require_lens(lens, frames.numel() * frames.element_size(), slot_stride, frames)
+    if out is None:
+        out = torch.empty(n, dtype=torch.int64, device=frames.device)
+    _check(_lib.load().aipstack_chksum_tx_fill_records_slotted(
+        frames.data_ptr(), slot_stride, lens.data_ptr(), n, out.data_ptr(),
+        _stream_handle(stream, frames)), "aipstack_chksum_tx_fill_records_slotted")
+    return out
+
+
 def chksum_batch_seeded_csr(buf, offsets, states, *, out=None, stream=None):
     """``out[i] = IpChksumAccumulator(State(states[i])).getChksum(IpBufRef(packet i))`` on
     the GPU (final checksum). ``states`` is a device int32/uint32 tensor of n states."""
@@ -545,6 +607,60 @@ class ChksumEngine:
         self._submitted(st, t.value, "aipstack_chksum_engine_submit_tx_fill", frames, o, status)
         return t.value, status
 
+    # ---- ring slots: frame i = the lens[i] bytes at buf[i * slot_stride:] ----------------
+
+    @staticmethod
+    def _slot_args(buf, slot_stride: int, lens):
+        ln = np.ascontiguousarray(lens, dtype=np.uint32)
+        n = ln.size
+        if slot_stride <= 0 or n * slot_stride > buf.nbytes:
+            raise ValueError("the buffer must hold n whole slots of slot_stride bytes")
+        return ln, n
+
+    def slotted(self, buf: np.ndarray, slot_stride: int, lens, *, out=None,
+                final: bool = False) -> np.ndarray:
+        """Checksums of the packets of a ring of slots in HOST memory
+        (``aipstack_chksum_engine_host_slotted``)."""
+        ln, n = self._slot_args(buf, slot_stride, lens)
+        out = self._host_args(buf, out, n)
+        _check(self._lib.aipstack_chksum_engine_host_slotted(
+            self._h, buf.ctypes.data, slot_stride, ln.ctypes.data, n, out.ctypes.data,
+            AIPSTACK_CHKSUM_FINAL if final else 0), "aipstack_chksum_engine_host_slotted")
+        return out
+
+    def submit_slotted(self, buf: np.ndarray, slot_stride: int, lens, *, out=None,
+                       final: bool = False):
+        ln, n = self._slot_args(buf, slot_stride, lens)
+        out = self._host_args(buf, out, n)
+        t = ctypes.c_uint64(0)
+        st = self._lib.aipstack_chksum_engine_submit_slotted(
+            self._h, buf.ctypes.data, slot_stride, ln.ctypes.data, n, out.ctypes.data,
+            AIPSTACK_CHKSUM_FINAL if final else 0, ctypes.byref(t))
+        self._submitted(st, t.value, "aipstack_chksum_engine_submit_slotted", buf, ln, out)
+        return t.value, out
+
+    def rx_verify_slotted(self, frames: np.ndarray, slot_stride: int, lens, *,
+                          out=None) -> np.ndarray:
+        """Rx verify of a ring of frame slots in HOST memory."""
+        ln, n = self._slot_args(frames, slot_stride, lens)
+        out = self._host_args(frames, out, n, np.uint8)
+        _check(self._lib.aipstack_chksum_engine_host_rx_verify_slotted(
+            self._h, frames.ctypes.data, slot_stride, ln.ctypes.data, n, out.ctypes.data),
+            "aipstack_chksum_engine_host_rx_verify_slotted")
+        return out
+
+    def tx_fill_slotted(self, frames: np.ndarray, slot_stride: int, lens, *,
+                        status=None) -> np.ndarray:
+        """Tx fill, in place, of a ring of frame slots in HOST memory."""
+        if not frames.flags.writeable:
+            raise ValueError("frames must be writable (filled in place)")
+        ln, n = self._slot_args(frames, slot_stride, lens)
+        status = self._host_args(frames, status, n, np.uint8)
+        _check(self._lib.aipstack_chksum_engine_host_tx_fill_slotted(
+            self._h, frames.ctypes.data, slot_stride, ln.ctypes.data, n, status.ctypes.data),
+            "aipstack_chksum_engine_host_tx_fill_slotted")
+        return status
+
     def csr(self, buf: np.ndarray, offsets: np.ndarray, *, out=None,
             final: bool = False) -> np.ndarray:
         o = np.ascontiguousarray(offsets, dtype=np.uint64)
@@ -556,6 +672,95 @@ class ChksumEngine:
             self._h, buf.ctypes.data, o.ctypes.data, n, out.ctypes.data,
             AIPSTACK_CHKSUM_FINAL if final else 0), "aipstack_chksum_engine_host_csr")
         return out
+
+
+class ChksumEngineGroup:
+    """Several devices behind one host-memory batch in ONE process (C-ABI
+    ``aipstack_chksum_engine_group_*``): one engine per entry of ``devices`` (repeats
+    allowed), each batch split into contiguous ranges of about equal bytes run concurrently,
+    one host thread per engine. ``last_status`` holds each engine's status of the last call."""
+
+    def __init__(self, devices, chunk_bytes: int = 0, nstreams: int = 4):
+        self._lib = _lib.load()
+        devs = (ctypes.c_int * len(devices))(*[int(d) for d in devices])
+        h = ctypes.c_void_p()
+        _check(self._lib.aipstack_chksum_engine_group_create(devs, len(devices), chunk_bytes,
+                                                             nstreams, ctypes.byref(h)),
+               "aipstack_chksum_engine_group_create")
+        self._h = h
+        self.size = len(devices)
+        self._registered = []
+        self.last_status = [0] * self.size
+
+    def close(self) -> None:
+        if self._h:
+            self._lib.aipstack_chksum_engine_group_destroy(self._h)
+            self._h = None
+            self._registered = []
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def register(self, arr: np.ndarray) -> None:
+        _check(self._lib.aipstack_chksum_engine_group_register(self._h, arr.ctypes.data,
+                                                               arr.nbytes),
+               "aipstack_chksum_engine_group_register")
+        self._registered.append(arr)
+
+    def unregister(self, arr: np.ndarray) -> None:
+        _check(self._lib.aipstack_chksum_engine_group_unregister(self._h, arr.ctypes.data),
+               "aipstack_chksum_engine_group_unregister")
+        self._registered = [a for a in self._registered if a is not arr]
+
+    def _call(self, fn, where, *args):
+        ds = (ctypes.c_int * self.size)()
+        st = getattr(self._lib, fn)(self._h, *args, ds)
+        self.last_status = list(ds)
+        _check(st, where)
+
+    def strided(self, buf, stride: int, length: int, n: int, *, out=None, final=False):
+        if n and (n - 1) * stride + length > buf.nbytes:
+            raise ValueError("batch exceeds buf")
+        out = ChksumEngine._host_args(buf, out, n)
+        self._call("aipstack_chksum_engine_group_host_strided", "engine group strided",
+                   buf.ctypes.data, stride, length, n, out.ctypes.data,
+                   AIPSTACK_CHKSUM_FINAL if final else 0)
+        return out
+
+    def csr(self, buf, offsets, *, out=None, final=False):
+        o = np.ascontiguousarray(offsets, dtype=np.uint64)
+        n = o.size - 1
+        if n > 0 and int(o[-1]) > buf.nbytes:
+            raise ValueError("offsets exceed buf")
+        out = ChksumEngine._host_args(buf, out, n)
+        self._call("aipstack_chksum_engine_group_host_csr", "engine group csr", buf.ctypes.data,
+                   o.ctypes.data, max(n, 0), out.ctypes.data, AIPSTACK_CHKSUM_FINAL if final else 0)
+        return out
+
+    def rx_verify(self, frames, offsets, *, out=None):
+        o = np.ascontiguousarray(offsets, dtype=np.uint64)
+        n = o.size - 1
+        if n > 0 and int(o[-1]) > frames.nbytes:
+            raise ValueError("offsets exceed frames")
+        out = ChksumEngine._host_args(frames, out, n, np.uint8)
+        self._call("aipstack_chksum_engine_group_host_rx_verify", "engine group rx_verify",
+                   frames.ctypes.data, o.ctypes.data, max(n, 0), out.ctypes.data)
+        return out
+
+    def tx_fill(self, frames, offsets, *, status=None):
+        o, n, status = ChksumEngine._tx_args(frames, offsets, status)
+        self._call("aipstack_chksum_engine_group_host_tx_fill", "engine group tx_fill",
+                   frames.ctypes.data, o.ctypes.data, max(n, 0), status.ctypes.data)
+        return status
 
 
 def chksum_batch_chain(chunk_addr, chunk_len, chunk_index, states=None, *, out=None,
@@ -718,6 +923,11 @@ def tx_fill_records(frames, offsets, *, out=None, stream=None):
                                                        out.data_ptr(), _stream_handle(stream, frames)),
            "aipstack_chksum_tx_fill_records")
     return out
+
+
+def slots_to_offsets(n: int, slot_stride: int) -> np.ndarray:
+    """Frame start offsets of n ring slots (for :func:`apply_tx_records`): i * slot_stride."""
+    return np.arange(n + 1, dtype=np.uint64) * np.uint64(slot_stride)
 
 
 def apply_tx_records(frames: np.ndarray, offsets: np.ndarray, records: np.ndarray,

@@ -58,6 +58,7 @@ __device__ __forceinline__ uint32_t from_next_lane(uint32_t v, uint32_t last, in
 
 struct StridedDesc {
     static constexpr bool kCsr = false;
+    static constexpr bool kStream = true;  // chunks may lie back to back (stream mode)
     uint64_t base;    // absolute address of packet 0
     uint64_t stride;  // bytes between packet starts
     uint32_t len;     // bytes per packet
@@ -86,6 +87,7 @@ struct StridedDesc {
 
 struct CsrDesc {
     static constexpr bool kCsr = true;
+    static constexpr bool kStream = true;
     uint64_t base;            // absolute address offsets are relative to
     const uint64_t *offsets;  // n+1 byte offsets
 
@@ -125,6 +127,50 @@ struct CsrDesc {
     }
     __device__ __forceinline__ uint32_t lane_seed(const Chunk &) const { return 0; }
     bool back_to_back() const { return false; }  // known per chunk only
+    // End of the chunk's bytes (absolute): one past its last packet.
+    __device__ __forceinline__ uint64_t chunk_end(const Chunk &c, int) const {
+        return base + c.end_off;
+    }
+};
+
+// Ring slots: packet i is the lens[i] bytes at base + i * stride -- a receive ring that
+// holds one frame per fixed-size slot with its length beside it (the TAP driver reads one
+// frame per buffer, reference tap/linux/TapDeviceLinux.cpp:156-178). The buffer holds n
+// whole slots. A length above cap = min(stride, 65535) is outside the contract: it is
+// clamped to cap (nothing outside the slot is read) and reported (note_violation).
+struct SlottedDesc {
+    static constexpr bool kCsr = false;
+    static constexpr bool kStream = false;  // slots are not back to back: wave mode only
+    uint64_t base;          // absolute address of slot 0
+    uint64_t stride;        // slot size in bytes
+    const uint32_t *lens;   // n packet lengths
+    uint32_t cap;           // min(stride, 65535)
+
+    struct Chunk {
+        uint64_t s0;   // start of the chunk's first slot
+        uint32_t len;  // lane j: packet j's length (settled)
+    };
+    __device__ __forceinline__ Chunk begin_chunk(uint64_t c0, uint64_t n, int lane) const {
+        const uint64_t i = c0 + (uint64_t)lane;
+        const uint32_t l = i < n ? lens[i] : 0u;
+        note_violation(l > cap, AIPSTACK_CHKSUM_VIOLATION_PACKET_LEN);
+        return Chunk{base + c0 * stride, settle(l < cap ? l : cap)};
+    }
+    __device__ __forceinline__ void bounds(const Chunk &c, int j, uint64_t &S,
+                                           uint64_t &E) const {
+        S = c.s0 + (uint64_t)j * stride;
+        E = S + (uint32_t)__builtin_amdgcn_readlane(c.len, j);
+    }
+    __device__ __forceinline__ void lane_bounds(const Chunk &c, int lane, uint64_t &S,
+                                                uint64_t &E) const {
+        S = c.s0 + (uint64_t)lane * stride;
+        E = S + c.len;
+    }
+    __device__ __forceinline__ uint32_t lane_seed(const Chunk &) const { return 0; }
+    bool back_to_back() const { return false; }
+    __device__ __forceinline__ uint64_t chunk_end(const Chunk &c, int cnt) const {
+        return c.s0 + (uint64_t)cnt * stride;
+    }
 };
 
 struct SeededCsrDesc : CsrDesc {

@@ -61,7 +61,8 @@ struct Slot {
     // Tx fill: instead of copying the results out, apply the piece's records to the
     // caller's frames in host memory (frames + offs[i], i < count) and statuses
     char *tx_frames = nullptr;
-    const uint64_t *tx_offs = nullptr;
+    const uint64_t *tx_offs = nullptr;  // frame i at tx_frames + tx_offs[i] (CSR), or
+    uint64_t tx_stride = 0;             // at tx_frames + i * tx_stride (ring slots)
     uint8_t *tx_status = nullptr;
     uint64_t ticket = 0;           // batch this slot's piece belongs to
     uint64_t seq = 0;              // piece number within the engine (1, 2, ...)
@@ -70,6 +71,7 @@ struct Slot {
 struct Region {
     const char *p;
     uint64_t bytes;
+    bool owned = true;  // registered by this engine (unregistered by it); else adopted
 };
 
 }  // namespace
@@ -124,7 +126,8 @@ void release(aipstack_chksum_engine *e) {
         if (s.done) (void)hipEventDestroy(s.done);
         if (s.stream) (void)hipStreamDestroy(s.stream);
     }
-    for (const Region &r : e->registered) (void)hipHostUnregister(const_cast<char *>(r.p));
+    for (const Region &r : e->registered)
+        if (r.owned) (void)hipHostUnregister(const_cast<char *>(r.p));
 }
 
 // Pageable input into pinned staging: one core copies ~20 GB/s, below the PCIe link the
@@ -156,11 +159,11 @@ void stage_copy(void *dst, const void *src, uint64_t bytes) {
 // Tx fill from host memory: write the checksum fields (big-endian) of frames [lo, hi) of a
 // completed piece into the caller's frames, and their statuses (record layout: chksum.h,
 // aipstack_chksum_tx_fill_records).
-void apply_tx_range(const uint64_t *rec, char *frames, const uint64_t *offs, uint8_t *status,
-                    uint64_t lo, uint64_t hi) {
+void apply_tx_range(const uint64_t *rec, char *frames, const uint64_t *offs, uint64_t stride,
+                    uint8_t *status, uint64_t lo, uint64_t hi) {
     for (uint64_t i = lo; i < hi; ++i) {
         const uint64_t x = rec[i];
-        char *f = frames + offs[i];
+        char *f = frames + (offs ? offs[i] : i * stride);
         status[i] = (uint8_t)(x >> 48);
         if ((x >> 40) & 1u) {
             f[24] = (char)((x >> 8) & 0xFFu);
@@ -176,14 +179,14 @@ void apply_tx_range(const uint64_t *rec, char *frames, const uint64_t *offs, uin
 
 // A piece's frames are spread over up to 64 MiB of host memory: every frame is a cache miss,
 // so a large piece is applied by up to 8 threads (16 Ki frames and more each).
-void apply_tx_records(const uint64_t *rec, char *frames, const uint64_t *offs, uint8_t *status,
-                      uint64_t count) {
+void apply_tx_records(const uint64_t *rec, char *frames, const uint64_t *offs, uint64_t stride,
+                      uint8_t *status, uint64_t count) {
     constexpr uint64_t kPerThreadMin = 16384;
     const unsigned hw = std::thread::hardware_concurrency();
     const unsigned nt =
         (unsigned)std::min<uint64_t>(std::min<uint64_t>(count / kPerThreadMin, 8), hw ? hw : 1);
     if (nt <= 1) {
-        apply_tx_range(rec, frames, offs, status, 0, count);
+        apply_tx_range(rec, frames, offs, stride, status, 0, count);
         return;
     }
     const uint64_t per = (count + nt - 1) / nt;
@@ -193,7 +196,7 @@ void apply_tx_records(const uint64_t *rec, char *frames, const uint64_t *offs, u
         const uint64_t lo = (uint64_t)t * per;
         if (lo >= count) break;
         const uint64_t hi = std::min(count, lo + per);
-        pool.emplace_back([=] { apply_tx_range(rec, frames, offs, status, lo, hi); });
+        pool.emplace_back([=] { apply_tx_range(rec, frames, offs, stride, status, lo, hi); });
     }
     for (std::thread &t : pool) t.join();
 }
@@ -216,7 +219,7 @@ int drain(aipstack_chksum_engine *e, Slot &s, bool blocking = true) {
     const int st = check_hip(r);
     if (st == AIPSTACK_CHKSUM_OK && s.tx_frames) {
         apply_tx_records(reinterpret_cast<const uint64_t *>(s.h_out), s.tx_frames, s.tx_offs,
-                         s.tx_status, s.count);
+                         s.tx_stride, s.tx_status, s.count);
     } else if (st == AIPSTACK_CHKSUM_OK) {
         std::memcpy(s.user_out, s.h_out, s.count * s.out_elem);
     } else {
@@ -359,13 +362,35 @@ extern "C" void aipstack_chksum_engine_destroy(aipstack_chksum_engine *e) {
     delete e;
 }
 
+namespace aipstack_amd {
+// For the engine group (chksum_engine_group.cpp): a region page-locked once for every
+// device (hipHostRegisterPortable) becomes DMA-direct input of this engine too; removing it
+// first completes the pieces in flight (they may still read it).
+void engine_adopt_region(aipstack_chksum_engine *e, const void *p, uint64_t bytes) {
+    std::lock_guard<std::mutex> lock(e->mu);
+    e->registered.push_back(Region{static_cast<const char *>(p), bytes, false});
+}
+void engine_drop_region(aipstack_chksum_engine *e, const void *p) {
+    std::lock_guard<std::mutex> lock(e->mu);
+    for (size_t i = 0; i < e->registered.size(); ++i) {
+        if (e->registered[i].p == p) {
+            (void)hipSetDevice(e->device);
+            drain_all(e);
+            e->registered.erase(e->registered.begin() + (long)i);
+            return;
+        }
+    }
+}
+}  // namespace aipstack_amd
+
 extern "C" int aipstack_chksum_engine_register(aipstack_chksum_engine *e, void *host_ptr,
                                                uint64_t bytes) {
     if (!e || !host_ptr || bytes == 0) return AIPSTACK_CHKSUM_EINVAL;
     std::lock_guard<std::mutex> lock(e->mu);
     if (hipSetDevice(e->device) != hipSuccess) return AIPSTACK_CHKSUM_ENODEV;
     const int st = check_hip(hipHostRegister(host_ptr, bytes, hipHostRegisterDefault));
-    if (st == AIPSTACK_CHKSUM_OK) e->registered.push_back(Region{static_cast<char *>(host_ptr), bytes});
+    if (st == AIPSTACK_CHKSUM_OK)
+        e->registered.push_back(Region{static_cast<char *>(host_ptr), bytes, true});
     return st;
 }
 
@@ -377,7 +402,8 @@ extern "C" int aipstack_chksum_engine_unregister(aipstack_chksum_engine *e, void
             (void)hipSetDevice(e->device);
             // pieces in flight may still DMA from (or, Tx, complete into) the region
             drain_all(e);
-            const int st = check_hip(hipHostUnregister(host_ptr));
+            const int st = e->registered[i].owned ? check_hip(hipHostUnregister(host_ptr))
+                                                  : AIPSTACK_CHKSUM_OK;
             e->registered.erase(e->registered.begin() + (long)i);
             return st;
         }
@@ -468,6 +494,7 @@ extern "C" int aipstack_chksum_engine_submit_tx_fill(aipstack_chksum_engine *e, 
                            [&](Slot &s, uint64_t i0, uint64_t cnt) {
                                s.tx_frames = frames;  // applied on completion (drain)
                                s.tx_offs = h_offsets + i0;
+                               s.tx_stride = 0;
                                s.tx_status = h_status + i0;
                                return aipstack_chksum_tx_fill_records(
                                    s.d_bytes, s.d_off, cnt, reinterpret_cast<uint64_t *>(s.d_out),
@@ -515,6 +542,127 @@ extern "C" int aipstack_chksum_engine_submit_csr(aipstack_chksum_engine *e, cons
                                                                 flags, s.stream);
                            },
                            ticket);
+}
+
+namespace {
+// Ring-slot batches: whole slots per chunk (the piece's slots are DMA'd as one span; the
+// slack after each frame travels too), lengths staged beside them. Every length is checked
+// first: <= min(slot_stride, 65535), else _EINVAL before any work.
+template <class Kernel>
+int submit_slotted_like(aipstack_chksum_engine *e, const void *h_base, uint64_t slot_stride,
+                        const uint32_t *h_len, uint64_t n, void *h_out, uint32_t elem,
+                        Kernel kernel, uint64_t *ticket) {
+    if (slot_stride == 0 || slot_stride > e->chunk_bytes) return AIPSTACK_CHKSUM_EINVAL;
+    const uint64_t cap = std::min<uint64_t>(slot_stride, AIPSTACK_CHKSUM_MAX_LEN);
+    for (uint64_t i = 0; i < n; ++i)
+        if (h_len[i] > cap) return AIPSTACK_CHKSUM_EINVAL;
+    const uint64_t per = std::min<uint64_t>(e->chunk_bytes / slot_stride, e->chunk_packets);
+    const char *base = static_cast<const char *>(h_base);
+    auto chunker = [&](uint64_t i0, uint64_t *i1, const char **src, uint64_t *bytes) {
+        *i1 = std::min(n, i0 + per);
+        *src = base + i0 * slot_stride;
+        *bytes = (*i1 - i0) * slot_stride;
+    };
+    auto launch = [&](Slot &s, uint64_t i0, uint64_t i1) {
+        const uint64_t cnt = i1 - i0;
+        std::memcpy(s.h_off, h_len + i0, cnt * sizeof(uint32_t));  // lengths -> pinned staging
+        int st = check_hip(hipMemcpyAsync(s.d_off, s.h_off, cnt * sizeof(uint32_t),
+                                          hipMemcpyHostToDevice, s.stream));
+        if (st != AIPSTACK_CHKSUM_OK) return st;
+        return kernel(s, i0, cnt, reinterpret_cast<const uint32_t *>(s.d_off));
+    };
+    std::lock_guard<std::mutex> lock(e->mu);
+    return enqueue(e, n, h_out, elem, chunker, launch, ticket);
+}
+}  // namespace
+
+extern "C" int aipstack_chksum_engine_submit_slotted(aipstack_chksum_engine *e, const void *h_base,
+                                                     uint64_t slot_stride, const uint32_t *h_len,
+                                                     uint64_t n, uint16_t *h_out, uint32_t flags,
+                                                     uint64_t *ticket) {
+    if (!e || !h_base || !h_len || !h_out || !ticket) return AIPSTACK_CHKSUM_EINVAL;
+    return submit_slotted_like(e, h_base, slot_stride, h_len, n, h_out, 2,
+                               [&](Slot &s, uint64_t, uint64_t cnt, const uint32_t *d_len) {
+                                   return aipstack_chksum_batch_slotted(s.d_bytes, slot_stride,
+                                                                        d_len, cnt, s.d_out,
+                                                                        flags, s.stream);
+                               },
+                               ticket);
+}
+
+extern "C" int aipstack_chksum_engine_submit_rx_verify_slotted(
+    aipstack_chksum_engine *e, const void *h_base, uint64_t slot_stride, const uint32_t *h_len,
+    uint64_t n, uint8_t *h_verdicts, uint64_t *ticket) {
+    if (!e || !h_base || !h_len || !h_verdicts || !ticket) return AIPSTACK_CHKSUM_EINVAL;
+    return submit_slotted_like(e, h_base, slot_stride, h_len, n, h_verdicts, 1,
+                               [&](Slot &s, uint64_t, uint64_t cnt, const uint32_t *d_len) {
+                                   return aipstack_chksum_rx_verify_slotted(
+                                       s.d_bytes, slot_stride, d_len, cnt,
+                                       reinterpret_cast<uint8_t *>(s.d_out), s.stream);
+                               },
+                               ticket);
+}
+
+extern "C" int aipstack_chksum_engine_submit_tx_fill_slotted(
+    aipstack_chksum_engine *e, void *h_base, uint64_t slot_stride, const uint32_t *h_len,
+    uint64_t n, uint8_t *h_status, uint64_t *ticket) {
+    if (!e || !h_base || !h_len || !h_status || !ticket) return AIPSTACK_CHKSUM_EINVAL;
+    char *frames = static_cast<char *>(h_base);
+    return submit_slotted_like(e, h_base, slot_stride, h_len, n, h_status, 8,
+                               [&](Slot &s, uint64_t i0, uint64_t cnt, const uint32_t *d_len) {
+                                   s.tx_frames = frames + i0 * slot_stride;
+                                   s.tx_offs = nullptr;
+                                   s.tx_stride = slot_stride;
+                                   s.tx_status = h_status + i0;
+                                   return aipstack_chksum_tx_fill_records_slotted(
+                                       s.d_bytes, slot_stride, d_len, cnt,
+                                       reinterpret_cast<uint64_t *>(s.d_out), s.stream);
+                               },
+                               ticket);
+}
+
+namespace {
+// The synchronous calls: submit, then wait (also for the pieces a failed submit enqueued).
+int finish_sync(aipstack_chksum_engine *e, int st, uint64_t t) {
+    if (st != AIPSTACK_CHKSUM_OK) {
+        if (t) (void)aipstack_chksum_engine_wait(e, t);
+        return st;
+    }
+    return aipstack_chksum_engine_wait(e, t);
+}
+}  // namespace
+
+extern "C" int aipstack_chksum_engine_host_slotted(aipstack_chksum_engine *e, const void *h_base,
+                                                   uint64_t slot_stride, const uint32_t *h_len,
+                                                   uint64_t n, uint16_t *h_out, uint32_t flags) {
+    if (!e || !h_base || !h_len || !h_out) return AIPSTACK_CHKSUM_EINVAL;
+    if (n == 0) return AIPSTACK_CHKSUM_OK;
+    uint64_t t = 0;
+    return finish_sync(e, aipstack_chksum_engine_submit_slotted(e, h_base, slot_stride, h_len, n,
+                                                               h_out, flags, &t), t);
+}
+
+extern "C" int aipstack_chksum_engine_host_rx_verify_slotted(aipstack_chksum_engine *e,
+                                                             const void *h_base,
+                                                             uint64_t slot_stride,
+                                                             const uint32_t *h_len, uint64_t n,
+                                                             uint8_t *h_verdicts) {
+    if (!e || !h_base || !h_len || !h_verdicts) return AIPSTACK_CHKSUM_EINVAL;
+    if (n == 0) return AIPSTACK_CHKSUM_OK;
+    uint64_t t = 0;
+    return finish_sync(e, aipstack_chksum_engine_submit_rx_verify_slotted(
+                              e, h_base, slot_stride, h_len, n, h_verdicts, &t), t);
+}
+
+extern "C" int aipstack_chksum_engine_host_tx_fill_slotted(aipstack_chksum_engine *e, void *h_base,
+                                                           uint64_t slot_stride,
+                                                           const uint32_t *h_len, uint64_t n,
+                                                           uint8_t *h_status) {
+    if (!e || !h_base || !h_len || !h_status) return AIPSTACK_CHKSUM_EINVAL;
+    if (n == 0) return AIPSTACK_CHKSUM_OK;
+    uint64_t t = 0;
+    return finish_sync(e, aipstack_chksum_engine_submit_tx_fill_slotted(
+                              e, h_base, slot_stride, h_len, n, h_status, &t), t);
 }
 
 extern "C" int aipstack_chksum_engine_poll(aipstack_chksum_engine *e, uint64_t ticket) {

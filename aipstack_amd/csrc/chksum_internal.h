@@ -39,4 +39,11 @@ int tuning_stream_windows(int family_default);
 
 }  // namespace aipstack_amd
 
+struct aipstack_chksum_engine;
+namespace aipstack_amd {
+// Host engine internals shared with the engine group (chksum_engine.cpp).
+void engine_adopt_region(aipstack_chksum_engine *e, const void *p, uint64_t bytes);
+void engine_drop_region(aipstack_chksum_engine *e, const void *p);
+}  // namespace aipstack_amd
+
 #endif

@@ -405,6 +405,8 @@ int launch_k(const Desc &desc, uint64_t n, const Shape &sh, uint16_t *d_out, uin
 template <class Desc, int U, int P, bool SEEDED>
 int launch_s(const Desc &desc, uint64_t n, const Shape &sh, uint16_t *d_out, uint32_t flags,
              hipStream_t stream) {
+    if constexpr (!Desc::kStream)  // ring slots: the per-packet wave mode only
+        return launch_k<Desc, U, P, true, SEEDED, 0>(desc, n, sh, d_out, flags, stream);
     if (tuning().nontemporal.load(std::memory_order_relaxed) == 0)  // sweeps only
         return launch_k<Desc, U, P, false, SEEDED, 0>(desc, n, sh, d_out, flags, stream);
     switch (pick_stream_for(Desc::kCsr, sh)) {
@@ -421,7 +423,7 @@ int launch_u(const Desc &desc, uint64_t n, const Shape &sh, uint16_t *d_out, uin
     int p = pick_packets(U, Desc::kCsr);
     // Every chunk takes stream mode: the per-packet path is never run, so give it the
     // fewest registers (the kernel's occupancy is set by the larger of the two paths).
-    if (desc.back_to_back() && pick_stream_for(Desc::kCsr, sh) > 0 &&
+    if (Desc::kStream && desc.back_to_back() && pick_stream_for(Desc::kCsr, sh) > 0 &&
         tuning().nontemporal.load(std::memory_order_relaxed) != 0 &&
         tuning().packets.load(std::memory_order_relaxed) == 0)
         p = 1;
@@ -526,6 +528,24 @@ extern "C" int aipstack_chksum_batch_strided(const void *d_base, uint64_t stride
     if (n > (1ull << 40)) return AIPSTACK_CHKSUM_EINVAL;
     StridedDesc d{(uint64_t)(uintptr_t)d_base, stride, len};
     return launch<StridedDesc, false>(d, n, len, d_out, flags, (hipStream_t)stream);
+}
+
+extern "C" int aipstack_chksum_batch_slotted(const void *d_base, uint64_t slot_stride,
+                                             const uint32_t *d_len, uint64_t n, uint16_t *d_out,
+                                             uint32_t flags, void *stream) {
+    if (n == 0) return AIPSTACK_CHKSUM_OK;
+    if (!d_base || !d_len || !d_out || slot_stride == 0 || n > (1ull << 40))
+        return AIPSTACK_CHKSUM_EINVAL;
+    SlottedDesc d;
+    d.base = (uint64_t)(uintptr_t)d_base;
+    d.stride = slot_stride;
+    d.lens = d_len;
+    d.cap = (uint32_t)(slot_stride < AIPSTACK_CHKSUM_MAX_LEN ? slot_stride : AIPSTACK_CHKSUM_MAX_LEN);
+    // U from the typical packet (<= ~2 KiB: one group of 2 segments per lane), not the
+    // slot: C2K (64-1500 B in 2048-B slots) U = 1 / 2 / 3: 286 / 277 / 328 us
+    // (profiles/r03/slots/sweep_C2K.jsonl); longer packets loop over further groups
+    return launch<SlottedDesc, false>(d, n, d.cap < 2000u ? d.cap : 2000u, d_out, flags,
+                                      (hipStream_t)stream);
 }
 
 extern "C" int aipstack_chksum_batch_csr(const void *d_base, const uint64_t *d_offsets,

@@ -406,8 +406,8 @@ __device__ __forceinline__ uint32_t l4s_below(const u32x4 (&seg)[kHdrSegs], uint
 #endif
 // GATHER: header segments captured from the stream (Rx always; Tx when no in-place field
 // stores follow the pass -- the records-only read pass, launch_frames).
-template <bool TX, int U, int P, bool NT, int SU, bool GATHER>
-__device__ __forceinline__ FrameOut process_chunk(const CsrDesc &desc, uint64_t p0, uint64_t n,
+template <class Desc, bool TX, int U, int P, bool NT, int SU, bool GATHER>
+__device__ __forceinline__ FrameOut process_chunk(const Desc &desc, uint64_t p0, uint64_t n,
                                                   uint32_t cpk, int lane, uint32_t voff,
                                                   uint32_t not_lane0, FrameLds *lds,
                                                   int &cnt_out) {
@@ -427,7 +427,7 @@ __device__ __forceinline__ FrameOut process_chunk(const CsrDesc &desc, uint64_t 
     // 65535 bytes can cover (offsets outside the contract, chksum.h) reads nothing.
     const uint64_t base = (__builtin_amdgcn_readfirstlane((uint32_t)S) & ~15u) |
                           ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(S >> 32)) << 32);
-    const uint64_t span = ((desc.base + chunk.end_off + 15u) & ~(uint64_t)15) - base;
+    const uint64_t span = ((desc.chunk_end(chunk, cnt) + 15u) & ~(uint64_t)15) - base;
     const bool span_bad = span > (uint64_t)kWave * 65536u + 16u;
     note_violation(span_bad && lane == 0, AIPSTACK_CHKSUM_VIOLATION_SPAN);
     const uint32_t hrec = __builtin_amdgcn_readfirstlane(
@@ -623,8 +623,8 @@ __device__ __forceinline__ FrameOut process_chunk(const CsrDesc &desc, uint64_t 
 #ifndef AIPSTACK_FRAME_WAVES_PER_SIMD  // occupancy the register budget is fitted to
 #define AIPSTACK_FRAME_WAVES_PER_SIMD 4
 #endif
-template <bool TX, int U, int P, bool NT, int SU, bool SPLIT, bool GATHER>
-__global__ __launch_bounds__(kBlock, AIPSTACK_FRAME_WAVES_PER_SIMD) void frame_kernel(CsrDesc desc, uint64_t n,
+template <class Desc, bool TX, int U, int P, bool NT, int SU, bool SPLIT, bool GATHER>
+__global__ __launch_bounds__(kBlock, AIPSTACK_FRAME_WAVES_PER_SIMD) void frame_kernel(Desc desc, uint64_t n,
                                                        uint32_t chunks_per_wave,
                                                        uint32_t chunk_packets,
                                                        uint8_t *__restrict__ status,
@@ -644,7 +644,7 @@ __global__ __launch_bounds__(kBlock, AIPSTACK_FRAME_WAVES_PER_SIMD) void frame_k
     for (; c < c_end; ++c) {
         const uint64_t p0 = c * cpk;
         int cnt;
-        const FrameOut o = process_chunk<TX, U, P, NT, SU, GATHER>(
+        const FrameOut o = process_chunk<Desc, TX, U, P, NT, SU, GATHER>(
             desc, p0, n, (uint32_t)cpk, lane, voff, not_lane0, my, cnt);
         if (lane < cnt) {
             if constexpr (SPLIT)
@@ -659,8 +659,8 @@ __global__ __launch_bounds__(kBlock, AIPSTACK_FRAME_WAVES_PER_SIMD) void frame_k
     }
 }
 
-template <bool TX, bool SPLIT, bool GATHER>
-int launch_frames_g(const CsrDesc &desc, uint64_t n, uint8_t *d_status, uint64_t *d_records,
+template <class Desc, bool TX, bool SPLIT, bool GATHER>
+int launch_frames_g(const Desc &desc, uint64_t n, uint8_t *d_status, uint64_t *d_records,
                     hipStream_t stream, int cus) {
     // small batches: fewer frames per chunk, so that they spread over many waves (as the
     // checksum batches, chksum_kernels.hip pick_shape)
@@ -675,15 +675,19 @@ int launch_frames_g(const CsrDesc &desc, uint64_t n, uint8_t *d_status, uint64_t
     const uint64_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
     if (blocks > 0x7FFFFFFFull || cpw > 0xFFFFFFFFull) return AIPSTACK_CHKSUM_EINVAL;
 #define AIPSTACK_LAUNCH_FRAMES(P, SU)                                                          \
-    hipLaunchKernelGGL((frame_kernel<TX, 2, P, AIPSTACK_FRAME_NT != 0, SU, SPLIT, GATHER>),   \
+    hipLaunchKernelGGL((frame_kernel<Desc, TX, 2, P, AIPSTACK_FRAME_NT != 0, SU, SPLIT, GATHER>), \
                        dim3((unsigned)blocks), dim3(kBlock), 0, stream, desc, n, (uint32_t)cpw, \
                        cpk, d_status, d_records)
-#define AIPSTACK_LAUNCH_FRAMES_SU(P)              \
-    switch (su) {                                 \
-        case 0: AIPSTACK_LAUNCH_FRAMES(P, 0); break; \
-        case 2: AIPSTACK_LAUNCH_FRAMES(P, 2); break; \
-        case 8: AIPSTACK_LAUNCH_FRAMES(P, 8); break; \
-        default: AIPSTACK_LAUNCH_FRAMES(P, 4);     \
+#define AIPSTACK_LAUNCH_FRAMES_SU(P)                  \
+    if constexpr (!Desc::kStream) {                   \
+        AIPSTACK_LAUNCH_FRAMES(P, 0);                 \
+    } else {                                          \
+        switch (su) {                                 \
+            case 0: AIPSTACK_LAUNCH_FRAMES(P, 0); break; \
+            case 2: AIPSTACK_LAUNCH_FRAMES(P, 2); break; \
+            case 8: AIPSTACK_LAUNCH_FRAMES(P, 8); break; \
+            default: AIPSTACK_LAUNCH_FRAMES(P, 4);     \
+        }                                             \
     }
     switch (tuning_frames_in_flight()) {
         case 2: AIPSTACK_LAUNCH_FRAMES_SU(2); break;
@@ -709,11 +713,11 @@ int launch_frames(const void *d_base, const uint64_t *d_offsets, uint64_t n, uin
     int st;
     if constexpr (TX) {
         if (tuning_tx_gather(SPLIT && !scatter))
-            st = launch_frames_g<true, SPLIT, true>(desc, n, d_status, d_records, stream, cus);
+            st = launch_frames_g<CsrDesc, true, SPLIT, true>(desc, n, d_status, d_records, stream, cus);
         else
-            st = launch_frames_g<true, SPLIT, false>(desc, n, d_status, d_records, stream, cus);
+            st = launch_frames_g<CsrDesc, true, SPLIT, false>(desc, n, d_status, d_records, stream, cus);
     } else {
-        st = launch_frames_g<false, SPLIT, true>(desc, n, d_status, d_records, stream, cus);
+        st = launch_frames_g<CsrDesc, false, SPLIT, true>(desc, n, d_status, d_records, stream, cus);
     }
     if (st != AIPSTACK_CHKSUM_OK) return st;
     if (SPLIT && scatter) {
@@ -726,6 +730,21 @@ int launch_frames(const void *d_base, const uint64_t *d_offsets, uint64_t n, uin
 }
 
 }  // namespace
+
+// Ring slots (SlottedDesc): per-lane header loads and the per-frame L4 loop; no stream mode,
+// so the header capture does not apply either.
+template <bool TX, bool SPLIT>
+int launch_frames_slotted(const void *d_base, uint64_t slot_stride, const uint32_t *d_len,
+                          uint64_t n, uint8_t *d_status, uint64_t *d_records, hipStream_t stream) {
+    const int cus = device_cu_count(stream);
+    if (cus <= 0) return AIPSTACK_CHKSUM_EHIP;
+    SlottedDesc desc;
+    desc.base = (uint64_t)(uintptr_t)d_base;
+    desc.stride = slot_stride;
+    desc.lens = d_len;
+    desc.cap = (uint32_t)(slot_stride < AIPSTACK_CHKSUM_MAX_LEN ? slot_stride : AIPSTACK_CHKSUM_MAX_LEN);
+    return launch_frames_g<SlottedDesc, TX, SPLIT, false>(desc, n, d_status, d_records, stream, cus);
+}
 
 int take_violations_frames(uint32_t *mask, bool clear) {
     uint32_t v = 0;
@@ -781,4 +800,35 @@ extern "C" int aipstack_chksum_tx_fill_split(void *d_base, const uint64_t *d_off
         return AIPSTACK_CHKSUM_EINVAL;
     return launch_frames<true, true>(d_base, d_offsets, n, d_status,
                                      static_cast<uint64_t *>(d_workspace), (hipStream_t)stream);
+}
+
+extern "C" int aipstack_chksum_rx_verify_slotted(const void *d_base, uint64_t slot_stride,
+                                                 const uint32_t *d_len, uint64_t n,
+                                                 uint8_t *d_verdict, void *stream) {
+    if (n == 0) return AIPSTACK_CHKSUM_OK;
+    if (!d_base || !d_len || !d_verdict || slot_stride == 0 || n > (1ull << 40))
+        return AIPSTACK_CHKSUM_EINVAL;
+    return launch_frames_slotted<false, false>(d_base, slot_stride, d_len, n, d_verdict, nullptr,
+                                               (hipStream_t)stream);
+}
+
+extern "C" int aipstack_chksum_tx_fill_slotted(void *d_base, uint64_t slot_stride,
+                                               const uint32_t *d_len, uint64_t n,
+                                               uint8_t *d_status, void *stream) {
+    if (n == 0) return AIPSTACK_CHKSUM_OK;
+    if (!d_base || !d_len || !d_status || slot_stride == 0 || n > (1ull << 40))
+        return AIPSTACK_CHKSUM_EINVAL;
+    return launch_frames_slotted<true, false>(d_base, slot_stride, d_len, n, d_status, nullptr,
+                                              (hipStream_t)stream);
+}
+
+extern "C" int aipstack_chksum_tx_fill_records_slotted(const void *d_base, uint64_t slot_stride,
+                                                       const uint32_t *d_len, uint64_t n,
+                                                       uint64_t *d_records, void *stream) {
+    if (n == 0) return AIPSTACK_CHKSUM_OK;
+    if (!d_base || !d_len || !d_records || slot_stride == 0 || n > (1ull << 40) ||
+        ((uintptr_t)d_records & 7u) != 0)
+        return AIPSTACK_CHKSUM_EINVAL;
+    return launch_frames_slotted<true, true>(d_base, slot_stride, d_len, n, nullptr, d_records,
+                                             (hipStream_t)stream);
 }

@@ -122,3 +122,23 @@ def frames_host(n: int, seed: int = SEED_DATA, max_payload: int = 1400):
     buf = np.empty(max(total, 1), dtype=np.uint8)
     lib.aipstack_synth_frames_host(buf.ctypes.data, off.ctypes.data, n, seed, max_payload)
     return buf[:total], off.astype(np.int64)
+
+
+def to_slots(buf: np.ndarray, offsets: np.ndarray, slot_stride: int, slack_seed: int = 99):
+    """Packets / frames buf[offsets[i]:offsets[i+1]] laid into a ring of fixed slots (one per
+    slot at i * slot_stride, the rest of each slot filled with splitmix64 bytes of
+    `slack_seed`, so that a kernel reading past a length would see garbage). Returns
+    (ring uint8 of n * slot_stride bytes, lens uint32)."""
+    o = np.asarray(offsets, dtype=np.int64)
+    n = o.size - 1
+    lens = np.diff(o).astype(np.int64)
+    if n and int(lens.max()) > slot_stride:
+        raise ValueError("a packet is longer than the slot")
+    ring = np.empty(n * slot_stride, dtype=np.uint8)
+    fill_host(ring, slack_seed)  # the same splitmix64 bytes as random_bytes, in C
+    if n == 0:
+        return ring, lens.astype(np.uint32)
+    so = np.arange(n, dtype=np.int64) * slot_stride
+    for d0, s0, s1 in zip(so.tolist(), o[:-1].tolist(), o[1:].tolist()):
+        ring[d0:d0 + s1 - s0] = buf[s0:s1]
+    return ring, lens.astype(np.uint32)

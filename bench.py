@@ -46,10 +46,13 @@ CONFIGS = {
     "TX": ("tx", 1 << 20, None),
     # the split fill's read pass alone (aipstack_chksum_tx_fill_records): the E2E Tx kernel
     "TXREC": ("txrec", 1 << 20, None),
+    # ring slots (one frame / packet per 2048-B slot, a length per slot; TAP receive ring)
+    "RX2K": ("rxslot", 1 << 20, None),
+    "C2K": ("csrslot", 2 << 20, None),
     # chained + seeded (TCP Tx shape)
     "CHAIN": ("chain", 1 << 20, None),
 }
-SLOT_STRIDE = {"A2K": 2048}  # strided configs whose packets do not lie back to back
+SLOT_STRIDE = {"A2K": 2048, "RX2K": 2048, "C2K": 2048}  # layouts not back to back
 WORKLOAD_NAMES = {
     "A": "1M x 1500B Ethernet-MTU packets per GPU, IP checksum (BASELINE configs[1]; x8 = configs[4])",
     "B": "256K x 9000B jumbo packets per GPU, IP checksum (BASELINE configs[2])",
@@ -63,6 +66,10 @@ WORKLOAD_NAMES = {
     "TXREC": "1M raw Ethernet frames per GPU (same mix), Tx fill records: the split fill's read "
              "pass alone (8-B record per frame: both checksums, field offset, flags, status; "
              "nothing written into the frames)",
+    "RX2K": "1M raw Ethernet frames per GPU (RX mix) in 2048B ring slots with a length per "
+            "slot, Rx verify (aipstack_chksum_rx_verify_slotted)",
+    "C2K": "2M mixed 64-1500B packets per GPU (config C's) in 2048B ring slots with a length "
+           "per slot, IP checksum (aipstack_chksum_batch_slotted)",
     "CHAIN": "1M TCP-Tx-shaped chains per GPU: IpChksumAccumulator(pseudo-header State)"
              ".getChksum(20B header node + 1460B payload in 2 chunks split at a random point)",
 }
@@ -119,6 +126,10 @@ def parse():
                         "64 slots, eager launches vs the same launches replayed from a HIP "
                         "graph. Prints its own line.")
     p.add_argument("--e2e-streams", type=int, default=4)
+    p.add_argument("--engines", type=int, default=0, metavar="N",
+                   help="with --e2e: one process drives N devices through an engine group "
+                        "(aipstack_chksum_engine_group_*; devices 0..N-1, or all "
+                        "AIPSTACK_BENCH_FORCE_DEVICE), the batch split into N ranges")
     p.add_argument("--e2e-chunk-mib", type=int, default=64)
     return p.parse_args()
 
@@ -142,13 +153,13 @@ def shard_spec(config, rank, world, n=None):
         spec["payload"] = n * plen
         spec["byte_offset"] = rank * n * stride
         spec["offsets"] = None
-    elif layout in ("rx", "tx", "txrec", "chain"):
+    elif layout in ("rx", "tx", "txrec", "rxslot", "chain"):
         # each rank synthesises its own frames / chains (seed per rank): they are independent
         spec["seed"] = synth.SEED_DATA + 1000 * rank
         spec["byte_offset"] = 0
         spec["offsets"] = None  # known after synthesis
         spec["total"] = None
-    else:
+    else:  # csr, csrslot
         off_all = synth.mixed_offsets(n * world)
         spec["offsets"] = off_all[rank * n:(rank + 1) * n + 1] - off_all[rank * n]
         spec["byte_offset"] = int(off_all[rank * n])
@@ -159,10 +170,10 @@ def shard_spec(config, rank, world, n=None):
 def host_shard(spec):
     """The shard's bytes in host memory (numpy), exactly as the device generators make them."""
     from aipstack_amd import synth
-    if spec["layout"] in ("rx", "tx", "txrec"):
+    if spec["layout"] in ("rx", "tx", "txrec", "rxslot"):
         buf, off = synth.frames_host(spec["n"], seed=spec["seed"], max_payload=1460)
         spec["offsets"], spec["total"] = off, int(off[-1])
-        if spec["layout"] == "rx":  # valid frames: fill with the oracle (test infrastructure)
+        if spec["layout"] in ("rx", "rxslot"):  # valid frames: filled by the oracle (test infra)
             lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "libchksum_oracle.so"))
             lib.oracle_tx_fill_batch.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_uint64,
                                                                          ctypes.c_void_p]
@@ -172,7 +183,7 @@ def host_shard(spec):
         return buf
     host = np.empty(spec["total"], dtype=np.uint8)
     synth.fill_host(host, synth.SEED_DATA, spec["byte_offset"])
-    if spec["layout"] == "csr":
+    if spec["layout"] in ("csr", "csrslot"):
         synth.apply_classes_host(host, spec["offsets"], first_packet=spec["first_packet"])
     return host
 
@@ -187,6 +198,10 @@ def algorithmic_bytes(layout, n, total_payload):
         return total_payload + 3 * 12 * n + 8 * (n + 1) + 4 * n + 2 * n
     if layout == "txrec":
         return total_payload + 16 * n + 8
+    if layout == "rxslot":  # frame bytes + 4 B length + 1 B verdict
+        return total_payload + 5 * n
+    if layout == "csrslot":  # packet bytes + 4 B length + 2 B result
+        return total_payload + 6 * n
     if layout in ("rx", "tx"):
         return total_payload + 9 * n + 8 + (4 * n if layout == "tx" else 0)
     b = total_payload + 2 * n
@@ -516,6 +531,15 @@ def main():
         status = torch.empty(n, dtype=torch.uint8, device=dev)
         tx_ws = torch.empty(8 * n, dtype=torch.uint8, device=dev)  # split fill's records
         records = torch.empty(n, dtype=torch.int64, device=dev)
+    if layout in ("rxslot", "csrslot"):
+        # the shard's frames / packets laid into 2048-B ring slots (slack = random bytes)
+        compact_host = host_shard(spec)
+        ring_host, lens_host = synth.to_slots(compact_host, spec["offsets"], SLOT_STRIDE[args.config])
+        buf = torch.from_numpy(ring_host).to(dev)
+        d_lens = torch.from_numpy(lens_host.view(np.int32)).to(dev)
+        status = torch.empty(n, dtype=torch.uint8, device=dev)
+        spec["total"] = int(lens_host.sum(dtype=np.uint64))
+        spec["payload"] = spec["total"]
     if layout == "chain":
         chain = make_chains(spec, dev)
         spec["total"] = chain["payload"]
@@ -541,6 +565,10 @@ def main():
             A.rx_verify(buf, d_off, out=status, stream=stream)
         elif layout == "txrec":
             A.tx_fill_records(buf, d_off, out=records, stream=stream)
+        elif layout == "rxslot":
+            A.rx_verify_slotted(buf, 2048, d_lens, out=status, stream=stream)
+        elif layout == "csrslot":
+            A.chksum_batch_slotted(buf, 2048, d_lens, out=out, stream=stream)
         elif layout == "chain" and args.chain_fill:
             A.chksum_chain_fill(chain["addr"], chain["len"], chain["index"], chain["states"],
                                 chain["fields"], out=out, stream=stream)
@@ -615,6 +643,19 @@ def main():
             parity = frames_check(spec, frames_host, buf.cpu().numpy(), status.cpu().numpy())
         if rank == 0 and not args.no_cpu_baseline:
             cpu = cpu_baseline_frames(spec, frames_host)
+    elif layout in ("rxslot", "csrslot"):
+        if not args.no_parity:
+            parity = slots_check(layout, ring_host, lens_host,
+                                 (status if layout == "rxslot" else out).cpu().numpy())
+        if rank == 0 and not args.no_cpu_baseline:
+            # the same frames / packets in their compact (CSR) form: the same host work
+            cspec = dict(spec, layout="rx" if layout == "rxslot" else "csr", total=int(spec["offsets"][-1]))
+            cspec.pop("payload", None)
+            if layout == "rxslot":
+                cpu = cpu_baseline_frames(cspec, compact_host)
+            else:
+                cpu, _ = cpu_baseline(cspec)
+            cpu["sample"] += " (the same packets in their compact CSR form)"
     elif layout == "chain":
         if not args.no_parity:
             parity = (chain_fill_check(chain) if args.chain_fill
@@ -647,6 +688,15 @@ def main():
                   else f"MISMATCH on rank(s) {bad}")
     pcis = [i["pci"] for i in infos]
 
+    slot_ceiling_fields = {}
+    if layout in ("rxslot", "csrslot") and rank == 0:
+        ceil = slot_read_ceiling(args.config, spec)
+        if ceil:
+            kernel_gbps = payload / avg_kernel_s / 1e9
+            slot_ceiling_fields = {"slot_read_ceiling": ceil,
+                                   "payload_GBps": round(kernel_gbps, 1),
+                                   "frac_of_slot_read_ceiling":
+                                       round(kernel_gbps / ceil["payload_GBps"], 4)}
     bytes_all = payload * world  # weak scaling: every rank holds the same-size shard
     value = bytes_all * args.steps / max_elapsed / 2**30
     achieved = alg / avg_kernel_s / 1e9
@@ -668,7 +718,9 @@ def main():
             "config": args.config,
             "packets_per_gpu": n,
             **({"slot_stride": stride} if layout == "strided" and stride != plen else {}),
-            "packet_bytes": plen if plen else {"csr": "64-1500 (mixed)",
+            **({"slot_stride": SLOT_STRIDE[args.config]} if layout in ("rxslot", "csrslot")
+               else {}),
+            "packet_bytes": plen if plen else {"csr": "64-1500 (mixed)", "csrslot": "64-1500 (mixed)",
                                                 "chain": "20 + 1460 in 3 chunks"}.get(
                                                     layout, "60-1514 (frames)"),
             "payload_bytes_per_gpu": payload,
@@ -691,6 +743,7 @@ def main():
                                   "median": round(per_launch[len(per_launch) // 2], 2),
                                   "max": round(per_launch[-1], 2)}} if per_launch else {}),
             "algorithmic_bytes_per_launch": alg,
+            **slot_ceiling_fields,
         },
         "per_gpu": {
             "GiB_s": [round(spec.get("payload", total) * args.steps / float(r[0]) / 2**30, 2)
@@ -846,9 +899,16 @@ def e2e(args, rank, world, local_rank, layout, n, plen):
     # every step gives the same bytes; parity compares with the oracle's fill of a copy
     orig = host.copy() if layout == "tx" and not args.no_parity else None
     out = np.empty(n, dtype=np.uint8 if frames else np.uint16)
-    eng = A.ChksumEngine(int(os.environ.get("AIPSTACK_BENCH_FORCE_DEVICE", local_rank)),
-                         chunk_bytes=args.e2e_chunk_mib << 20,
-                         nstreams=args.e2e_streams)
+    if args.engines > 0:
+        forced = os.environ.get("AIPSTACK_BENCH_FORCE_DEVICE")
+        engine_devices = ([int(forced)] * args.engines if forced is not None
+                          else list(range(args.engines)))
+        eng = A.ChksumEngineGroup(engine_devices, chunk_bytes=args.e2e_chunk_mib << 20,
+                                  nstreams=args.e2e_streams)
+    else:
+        engine_devices = [int(os.environ.get("AIPSTACK_BENCH_FORCE_DEVICE", local_rank))]
+        eng = A.ChksumEngine(engine_devices[0], chunk_bytes=args.e2e_chunk_mib << 20,
+                             nstreams=args.e2e_streams)
     if not args.e2e_pageable:
         eng.register(host)
 
@@ -938,7 +998,11 @@ def e2e(args, rank, world, local_rank, layout, n, plen):
             "config": {"workload": WORKLOAD_NAMES[args.config], "config": args.config,
                        "host_memory": "pageable (CPU copy into pinned staging)"
                        if args.e2e_pageable else "registered (hipHostRegister, DMA direct)",
-                       "streams": args.e2e_streams, "chunk_MiB": args.e2e_chunk_mib},
+                       "streams": args.e2e_streams, "chunk_MiB": args.e2e_chunk_mib,
+                       **({"engines": args.engines, "engine_devices": engine_devices,
+                           "engine_group": "one process, disjoint ranges of equal bytes, one "
+                                           "host thread per engine"}
+                          if args.engines > 0 else {})},
             "per_gpu": {"devices": pcis, "arch": [i["arch"] for i in infos],
                         "distinct_devices": len(set(pcis)) == world,
                         "parity": [i["parity"] for i in infos]},
@@ -963,6 +1027,45 @@ def frames_check(spec, frames_before, frames_after, status):
     fn(ref.ctypes.data, o.ctypes.data, n, want.ctypes.data)
     ok = np.array_equal(status, want) and np.array_equal(frames_after, ref)
     return "bit-exact (verdicts/frames vs oracle)" if ok else "MISMATCH"
+
+
+def slots_check(layout, ring, lens, got):
+    """Ring slots: every verdict / checksum vs the C oracle over the same ring."""
+    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "libchksum_oracle.so"))
+    n = lens.size
+    if layout == "rxslot":
+        want = np.empty(n, dtype=np.uint8)
+        lib.oracle_rx_verify_slotted.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                                 ctypes.c_uint64, ctypes.c_void_p]
+        lib.oracle_rx_verify_slotted(ring.ctypes.data, 2048, lens.ctypes.data, n, want.ctypes.data)
+    else:
+        want = np.empty(n, dtype=np.uint16)
+        lib.oracle_batch_slotted.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                             ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32]
+        lib.oracle_batch_slotted(ring.ctypes.data, 2048, lens.ctypes.data, n, want.ctypes.data, 0)
+    return "bit-exact (every slot vs oracle)" if np.array_equal(got, want) else "MISMATCH"
+
+
+def slot_read_ceiling(config, spec):
+    """tools/build/slot_peak on this shard's slot pattern (a child process, after the timed
+    region): the payload GB/s a pure read of just the packets' bytes from their slots reaches
+    on this GPU -- the ceiling the slotted kernels are compared with."""
+    import subprocess
+    exe = os.path.join(ROOT, "tools", "build", "slot_peak")
+    if not os.path.exists(exe):
+        return None
+    n = spec["n"]
+    args = (["frames", str(n), str(spec["seed"]), "1460", "2048"] if config == "RX2K"
+            else ["mixed", str(n), "2048"])
+    if config == "C2K" and spec["first_packet"] != 0:
+        return None  # the probe regenerates shard 0's lengths only
+    try:
+        r = subprocess.run([exe] + args, capture_output=True, text=True, timeout=120)
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+        d["source"] = "tools/build/slot_peak " + " ".join(args)
+        return d
+    except (OSError, ValueError, IndexError, subprocess.SubprocessError):
+        return None
 
 
 def records_check(spec, frames_before, frames_after, records):

@@ -75,6 +75,15 @@ int aipstack_chksum_batch_csr(const void *d_base, const uint64_t *d_offsets,
                               uint64_t n, uint16_t *d_out, uint32_t flags,
                               void *stream);
 
+/* Ring-slot batch: packet i is the d_len[i] bytes at d_base + i*slot_stride -- a receive
+ * ring that holds one frame per fixed-size slot with its length beside it (the TAP driver
+ * reads one frame per buffer, reference tap/linux/TapDeviceLinux.cpp:156-178), checksummed
+ * where it lies, without compacting it first. The buffer holds n whole slots; each
+ * d_len[i] <= min(slot_stride, 65535) (a longer one is clamped to that and reported through
+ * aipstack_chksum_contract_violations). d_out[i] as for the strided form. */
+int aipstack_chksum_batch_slotted(const void *d_base, uint64_t slot_stride, const uint32_t *d_len,
+                                  uint64_t n, uint16_t *d_out, uint32_t flags, void *stream);
+
 /* Seeded CSR batch: d_out[i] = IpChksumAccumulator(State{d_states[i]})
  *                                  .getChksum(IpBufRef{packet i})
  * i.e. a per-packet saved accumulator state (pseudo-header / header words, exported by
@@ -171,6 +180,19 @@ int aipstack_chksum_tx_fill_split(void *d_base, const uint64_t *d_offsets, uint6
 int aipstack_chksum_tx_fill_records(const void *d_base, const uint64_t *d_offsets, uint64_t n,
                                     uint64_t *d_records, void *stream);
 
+/* The frame batches on a ring of slots (layout as aipstack_chksum_batch_slotted: frame i is
+ * the d_len[i] bytes at d_base + i*slot_stride, slot_stride <= 65536, n whole slots): Rx
+ * verify, the one-pass in-place Tx fill, and the Tx records. Same results per frame as the
+ * CSR forms. */
+int aipstack_chksum_rx_verify_slotted(const void *d_base, uint64_t slot_stride,
+                                      const uint32_t *d_len, uint64_t n, uint8_t *d_verdict,
+                                      void *stream);
+int aipstack_chksum_tx_fill_slotted(void *d_base, uint64_t slot_stride, const uint32_t *d_len,
+                                    uint64_t n, uint8_t *d_status, void *stream);
+int aipstack_chksum_tx_fill_records_slotted(const void *d_base, uint64_t slot_stride,
+                                            const uint32_t *d_len, uint64_t n,
+                                            uint64_t *d_records, void *stream);
+
 /* ---- 3. host-memory streaming engine ----------------------------------------------- */
 
 /* The reference's packet path starts and ends in host memory (TAP read()/write(),
@@ -249,12 +271,71 @@ int aipstack_chksum_engine_submit_tx_fill(aipstack_chksum_engine *engine, void *
                                           const uint64_t *h_offsets, uint64_t n,
                                           uint8_t *h_status, uint64_t *ticket);
 
+/* The same three on a ring of slots in HOST memory (layout as aipstack_chksum_batch_slotted:
+ * frame i is the h_len[i] bytes at h_base + i*slot_stride; the buffer holds n whole slots;
+ * every h_len[i] <= min(slot_stride, 65535) and slot_stride <= chunk_bytes, else _EINVAL
+ * before any work). Pieces are runs of whole slots, copied as they lie (slack included). */
+int aipstack_chksum_engine_host_slotted(aipstack_chksum_engine *engine, const void *h_base,
+                                        uint64_t slot_stride, const uint32_t *h_len, uint64_t n,
+                                        uint16_t *h_out, uint32_t flags);
+int aipstack_chksum_engine_submit_slotted(aipstack_chksum_engine *engine, const void *h_base,
+                                          uint64_t slot_stride, const uint32_t *h_len, uint64_t n,
+                                          uint16_t *h_out, uint32_t flags, uint64_t *ticket);
+int aipstack_chksum_engine_host_rx_verify_slotted(aipstack_chksum_engine *engine,
+                                                  const void *h_base, uint64_t slot_stride,
+                                                  const uint32_t *h_len, uint64_t n,
+                                                  uint8_t *h_verdicts);
+int aipstack_chksum_engine_submit_rx_verify_slotted(aipstack_chksum_engine *engine,
+                                                    const void *h_base, uint64_t slot_stride,
+                                                    const uint32_t *h_len, uint64_t n,
+                                                    uint8_t *h_verdicts, uint64_t *ticket);
+int aipstack_chksum_engine_host_tx_fill_slotted(aipstack_chksum_engine *engine, void *h_base,
+                                                uint64_t slot_stride, const uint32_t *h_len,
+                                                uint64_t n, uint8_t *h_status);
+int aipstack_chksum_engine_submit_tx_fill_slotted(aipstack_chksum_engine *engine, void *h_base,
+                                                  uint64_t slot_stride, const uint32_t *h_len,
+                                                  uint64_t n, uint8_t *h_status,
+                                                  uint64_t *ticket);
+
 /* Completion of a submitted batch: 0 = done (h_out holds the results), 1 = still running
  * (poll only), negative = one of its pieces failed (the first failure's status; h_out /
  * the frames of the failed pieces are not written), or _EINVAL for a ticket never issued.
  * _wait blocks. A ticket's failure is reported once; completing it again returns 0. */
 int aipstack_chksum_engine_poll(aipstack_chksum_engine *engine, uint64_t ticket);
 int aipstack_chksum_engine_wait(aipstack_chksum_engine *engine, uint64_t ticket);
+
+/* ---- 4. several devices in one process -------------------------------------------- */
+
+/* The reference stack is one process on one event-loop thread (event_loop/event_loop.dox:
+ * 48-50); a host batch is PCIe-bound per device (~52 GiB/s). An engine group owns one engine
+ * per entry of `devices` (repeats allowed), splits every batch into contiguous ranges of about
+ * equal bytes, runs each range on its engine from its own host thread and joins: disjoint
+ * packet ranges, no data exchanged between the devices. The host_* calls mirror the single
+ * engine's; dev_status (NULL or n_devices ints) receives each engine's status, the return
+ * value is the first failure (or _OK). _register page-locks a region once for all devices
+ * (hipHostRegisterPortable). Calls on one group are serialised. */
+typedef struct aipstack_chksum_engine_group aipstack_chksum_engine_group;
+
+int aipstack_chksum_engine_group_create(const int *devices, int n_devices, uint64_t chunk_bytes,
+                                        int nstreams, aipstack_chksum_engine_group **out);
+void aipstack_chksum_engine_group_destroy(aipstack_chksum_engine_group *group);
+int aipstack_chksum_engine_group_size(const aipstack_chksum_engine_group *group);
+int aipstack_chksum_engine_group_register(aipstack_chksum_engine_group *group, void *host_ptr,
+                                          uint64_t bytes);
+int aipstack_chksum_engine_group_unregister(aipstack_chksum_engine_group *group, void *host_ptr);
+int aipstack_chksum_engine_group_host_strided(aipstack_chksum_engine_group *group,
+                                              const void *h_base, uint64_t stride, uint32_t len,
+                                              uint64_t n, uint16_t *h_out, uint32_t flags,
+                                              int *dev_status);
+int aipstack_chksum_engine_group_host_csr(aipstack_chksum_engine_group *group, const void *h_base,
+                                          const uint64_t *h_offsets, uint64_t n, uint16_t *h_out,
+                                          uint32_t flags, int *dev_status);
+int aipstack_chksum_engine_group_host_rx_verify(aipstack_chksum_engine_group *group,
+                                                const void *h_base, const uint64_t *h_offsets,
+                                                uint64_t n, uint8_t *h_verdicts, int *dev_status);
+int aipstack_chksum_engine_group_host_tx_fill(aipstack_chksum_engine_group *group, void *h_base,
+                                              const uint64_t *h_offsets, uint64_t n,
+                                              uint8_t *h_status, int *dev_status);
 
 /* ---- diagnostics ------------------------------------------------------------------ */
 

@@ -115,6 +115,18 @@ void oracle_batch_csr(const void *base, const uint64_t *offsets, uint64_t n,
     }
 }
 
+/* Ring slots: packet i = the lens[i] bytes at base + i * stride (IpChksumInverted per packet,
+ * Chksum.h:77-99, as the CSR batch). */
+void oracle_batch_slotted(const void *base, uint64_t stride, const uint32_t *lens, uint64_t n,
+                          uint16_t *out, uint32_t flags)
+{
+    const unsigned char *b = (const unsigned char *)base;
+    for (uint64_t i = 0; i < n; i++) {
+        uint16_t v = oracle_chksum_inverted(b + i * stride, lens[i]);
+        out[i] = (flags & 1u) ? (uint16_t)~v : v;
+    }
+}
+
 /* Seeded batch: IpChksumAccumulator(State{states[i]}).getChksum(IpBufRef{packet i})
  * -- one contiguous chunk per packet (reference Chksum.h:171-174, 263-269). */
 void oracle_batch_seeded_csr(const void *base, const uint64_t *offsets,

@@ -15,6 +15,8 @@ uint16_t oracle_chksum_chain(uint32_t state, const void *const *ptrs,
                              const size_t *lens, size_t nchunks);
 void oracle_batch_strided(const void *base, uint64_t stride, uint32_t len,
                           uint64_t n, uint16_t *out, uint32_t flags);
+void oracle_batch_slotted(const void *base, uint64_t stride, const uint32_t *lens, uint64_t n,
+                          uint16_t *out, uint32_t flags);
 void oracle_batch_csr(const void *base, const uint64_t *offsets, uint64_t n,
                       uint16_t *out, uint32_t flags);
 void oracle_batch_seeded_csr(const void *base, const uint64_t *offsets,

@@ -198,3 +198,20 @@ void oracle_tx_fill_batch(void *base, const uint64_t *offsets, uint64_t n, uint8
     for (uint64_t i = 0; i < n; i++)
         status[i] = (uint8_t)oracle_tx_fill(b + offsets[i], (size_t)(offsets[i + 1] - offsets[i]));
 }
+
+/* Ring slots: frame i = the lens[i] bytes at base + i * stride. */
+void oracle_rx_verify_slotted(const void *base, uint64_t stride, const uint32_t *lens,
+                              uint64_t n, uint8_t *verdict)
+{
+    const uint8_t *b = (const uint8_t *)base;
+    for (uint64_t i = 0; i < n; i++)
+        verdict[i] = (uint8_t)oracle_rx_verify(b + i * stride, lens[i]);
+}
+
+void oracle_tx_fill_slotted(void *base, uint64_t stride, const uint32_t *lens, uint64_t n,
+                            uint8_t *status)
+{
+    uint8_t *b = (uint8_t *)base;
+    for (uint64_t i = 0; i < n; i++)
+        status[i] = (uint8_t)oracle_tx_fill(b + i * stride, lens[i]);
+}

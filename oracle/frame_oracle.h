@@ -17,6 +17,10 @@ int oracle_tx_fill(void *frame, size_t len);
 void oracle_rx_verify_batch(const void *base, const uint64_t *offsets, uint64_t n,
                             uint8_t *verdict);
 void oracle_tx_fill_batch(void *base, const uint64_t *offsets, uint64_t n, uint8_t *status);
+void oracle_rx_verify_slotted(const void *base, uint64_t stride, const uint32_t *lens,
+                              uint64_t n, uint8_t *verdict);
+void oracle_tx_fill_slotted(void *base, uint64_t stride, const uint32_t *lens, uint64_t n,
+                            uint8_t *status);
 
 #ifdef __cplusplus
 }

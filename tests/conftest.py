@@ -50,7 +50,32 @@ class Oracle:
         lib.oracle_tx_fill.argtypes = [vp, sz]
         lib.oracle_rx_verify_batch.argtypes = [vp, vp, u64, vp]
         lib.oracle_tx_fill_batch.argtypes = [vp, vp, u64, vp]
+        lib.oracle_batch_slotted.argtypes = [vp, u64, vp, u64, vp, u32]
+        lib.oracle_rx_verify_slotted.argtypes = [vp, u64, vp, u64, vp]
+        lib.oracle_tx_fill_slotted.argtypes = [vp, u64, vp, u64, vp]
         self.lib = lib
+
+    def batch_slotted(self, buf, stride, lens, final=False):
+        ln = np.ascontiguousarray(lens, dtype=np.uint32)
+        out = np.empty(ln.size, dtype=np.uint16)
+        self.lib.oracle_batch_slotted(buf.ctypes.data, stride, ln.ctypes.data, ln.size,
+                                      out.ctypes.data, 1 if final else 0)
+        return out
+
+    def rx_verify_slotted(self, buf, stride, lens):
+        ln = np.ascontiguousarray(lens, dtype=np.uint32)
+        out = np.empty(ln.size, dtype=np.uint8)
+        self.lib.oracle_rx_verify_slotted(buf.ctypes.data, stride, ln.ctypes.data, ln.size,
+                                          out.ctypes.data)
+        return out
+
+    def tx_fill_slotted(self, buf, stride, lens):
+        """In place on the numpy buffer; returns statuses."""
+        ln = np.ascontiguousarray(lens, dtype=np.uint32)
+        out = np.empty(ln.size, dtype=np.uint8)
+        self.lib.oracle_tx_fill_slotted(buf.ctypes.data, stride, ln.ctypes.data, ln.size,
+                                        out.ctypes.data)
+        return out
 
     def rx_verify_batch(self, buf, offsets):
         o = np.ascontiguousarray(offsets, dtype=np.uint64)

@@ -103,6 +103,20 @@ int main() {
 
     const int dev = aipstack_chksum_device_check(0);
     CHECK(dev == 0 || dev == AIPSTACK_CHKSUM_ENODEV || dev == AIPSTACK_CHKSUM_EHIP);
+    aipstack_chksum_engine_group *grp = nullptr;
+    const int devs[3] = {0, 0, 0}, bad_devs[2] = {0, -1};
+    CHECK(aipstack_chksum_engine_group_create(nullptr, 1, 0, 2, &grp) == EINVAL_);
+    CHECK(aipstack_chksum_engine_group_create(devs, 0, 0, 2, &grp) == EINVAL_);
+    CHECK(aipstack_chksum_engine_group_create(devs, 3, 0, 2, nullptr) == EINVAL_);
+    CHECK(aipstack_chksum_engine_group_create(bad_devs, 2, 0, 2, &grp) != 0 && grp == nullptr);
+    CHECK(aipstack_chksum_engine_group_size(nullptr) == EINVAL_);
+    CHECK(aipstack_chksum_engine_group_register(nullptr, dummy, 64) == EINVAL_);
+    CHECK(aipstack_chksum_engine_group_unregister(nullptr, dummy) == EINVAL_);
+    CHECK(aipstack_chksum_engine_group_host_csr(nullptr, dummy, off, 1, out, 0, nullptr) == EINVAL_);
+    CHECK(aipstack_chksum_engine_group_host_strided(nullptr, dummy, 1, 1, 1, out, 0, nullptr) == EINVAL_);
+    CHECK(aipstack_chksum_engine_group_host_rx_verify(nullptr, dummy, off, 1, verdicts, nullptr) == EINVAL_);
+    CHECK(aipstack_chksum_engine_group_host_tx_fill(nullptr, dummy, off, 1, verdicts, nullptr) == EINVAL_);
+    aipstack_chksum_engine_group_destroy(nullptr);  // no-op
     std::uint32_t vmask = 0;
     CHECK(aipstack_chksum_contract_violations(0, nullptr, 1) == EINVAL_);
     CHECK(aipstack_chksum_contract_violations(-1, &vmask, 1) == AIPSTACK_CHKSUM_ENODEV);

@@ -1016,6 +1016,176 @@ def test_tx_fill_edge_frames(oracle, stream_mode, shift, su, split):
     assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
 
 
+# ---- ring slots: one packet / frame per fixed slot, a length per slot ---------------------
+
+@pytest.mark.parametrize("stride", [64, 1517, 2048, 9216, 65536])
+def test_slotted_checksums(oracle, stride):
+    """aipstack_chksum_batch_slotted: lengths 0..min(stride, 65535) at every slot alignment
+    an odd stride gives, slack bytes random; inverted and FINAL."""
+    rng = np.random.default_rng(stride)
+    n = {64: 50000, 1517: 20000, 2048: 20000, 9216: 3000, 65536: 300}[stride]
+    cap = min(stride, 65535)
+    lens = rng.integers(0, cap + 1, n).astype(np.uint32)
+    lens[:8] = [0, 1, 2, cap, cap - 1, 15, 16, 17][:8] if cap > 17 else lens[:8]
+    ring = synth.random_bytes(stride + 7, n * stride + 16)
+    for base in (0, 3):
+        view = ring[base:base + n * stride]
+        dring = _d(ring)
+        got = _np(A.chksum_batch_slotted(dring[base:base + n * stride], stride,
+                                         _d(lens.view(np.int32))))
+        assert np.array_equal(got, oracle.batch_slotted(np.ascontiguousarray(view), stride, lens))
+    fin = _np(A.chksum_batch_slotted(_d(ring[:n * stride]), stride, _d(lens.view(np.int32)),
+                                     final=True))
+    assert np.array_equal(fin, oracle.batch_slotted(ring[:n * stride], stride, lens, final=True))
+
+
+def test_slotted_full_size_1m(oracle):
+    """1 M config-C packets (64-1500 B, odd lengths, all-0x00/0xFF/sum-0 classes) in 2048-B
+    ring slots, and 1 M raw frames in 2048-B slots through Rx verify: whole batch vs oracle."""
+    n = 1 << 20
+    buf, off = synth.mixed_batch(n)
+    ring, lens = synth.to_slots(buf, off, 2048)
+    got = _np(A.chksum_batch_slotted(_d(ring), 2048, _d(lens.view(np.int32))))
+    assert np.array_equal(got, oracle.batch_slotted(ring, 2048, lens))
+    del ring, buf
+    fr, foff = synth.frames_host(n, seed=71, max_payload=1460)
+    oracle.tx_fill_batch(fr, foff)
+    _corrupt(fr, foff, 0.1, 3)
+    fring, flens = synth.to_slots(fr, foff, 2048)
+    v = _np(A.rx_verify_slotted(_d(fring), 2048, _d(flens.view(np.int32))))
+    want = oracle.rx_verify_slotted(fring, 2048, flens)
+    assert np.array_equal(v, want), np.nonzero(v != want)[0][:10]
+    assert np.array_equal(want, oracle.rx_verify_batch(fr, foff))  # same verdicts as CSR
+
+
+@pytest.mark.parametrize("stride", [1600, 2048, 4096])
+def test_slotted_frames_tx_fill_and_records(oracle, stride):
+    buf, off = synth.frames_host(30000, seed=stride, max_payload=1460)
+    ring, lens = synth.to_slots(buf, off, stride)
+    dl = _d(lens.view(np.int32))
+    want = ring.copy()
+    want_st = oracle.tx_fill_slotted(want, stride, lens)
+    rec = _np(A.tx_fill_records_slotted(_d(ring), stride, dl))
+    got = ring.copy()
+    st = A.apply_tx_records(got, A.slots_to_offsets(lens.size, stride), rec)
+    assert np.array_equal(st, want_st) and np.array_equal(got, want)
+    dring = _d(ring)
+    st2 = _np(A.tx_fill_slotted(dring, stride, dl))
+    assert np.array_equal(st2, want_st)
+    assert np.array_equal(_np(dring), want)  # fields written, slack untouched
+    v = _np(A.rx_verify_slotted(dring, stride, dl))
+    assert np.array_equal(v, oracle.rx_verify_slotted(want, stride, lens))
+
+
+@pytest.mark.parametrize("shift", [0, 5])
+def test_slotted_edge_frames(oracle, shift):
+    buf, off = _edge_frames(77 + shift, 3000)
+    ring, lens = synth.to_slots(buf, off, 1600)
+    big = np.zeros(ring.size + shift, dtype=np.uint8)
+    big[shift:] = ring
+    d = _d(big)
+    v = _np(A.rx_verify_slotted(d[shift:], 1600, _d(lens.view(np.int32))))
+    assert np.array_equal(v, oracle.rx_verify_slotted(ring, 1600, lens))
+    assert np.array_equal(v, oracle.rx_verify_batch(buf, off))
+
+
+def test_slotted_length_over_slot_is_clamped_and_reported(oracle):
+    n, stride = 1000, 512
+    ring = synth.random_bytes(5, n * stride)
+    lens = np.full(n, 300, dtype=np.uint32)
+    lens[7] = 600    # > the slot
+    lens[9] = 70000  # > the slot and > 65535
+    A.contract_violations(0, clear=True)
+    got = _np(A.chksum_batch_slotted(_d(ring), stride, _d(lens.view(np.int32))))
+    clamped = np.minimum(lens, stride)
+    assert np.array_equal(got, oracle.batch_slotted(ring, stride, clamped))
+    assert A.contract_violations(0, clear=True) == A.VIOLATION_PACKET_LEN
+    A.rx_verify_slotted(_d(ring), stride, _d(lens.view(np.int32)))
+    assert A.contract_violations(0, clear=True) == A.VIOLATION_PACKET_LEN
+
+
+@pytest.mark.parametrize("register", [False, True])
+def test_engine_slotted(oracle, register):
+    """The engine's ring-slot calls from host memory: checksums, Rx verify, Tx fill in place
+    (slack bytes untouched), several pieces per batch; bad lengths rejected up front."""
+    with A.ChksumEngine(0, chunk_bytes=4 << 20, nstreams=3) as eng:
+        buf, off = synth.mixed_batch(40000)
+        ring, lens = synth.to_slots(buf, off, 2048)
+        if register:
+            eng.register(ring)
+        assert np.array_equal(eng.slotted(ring, 2048, lens), oracle.batch_slotted(ring, 2048, lens))
+        fr, foff = synth.frames_host(30000, seed=72, max_payload=1460)
+        fring, flens = synth.to_slots(fr, foff, 2048)
+        if register:
+            eng.register(fring)
+        want = fring.copy()
+        want_st = oracle.tx_fill_slotted(want, 2048, flens)
+        st = eng.tx_fill_slotted(fring, 2048, flens)
+        assert np.array_equal(st, want_st) and np.array_equal(fring, want)
+        v = eng.rx_verify_slotted(fring, 2048, flens)
+        assert np.array_equal(v, oracle.rx_verify_slotted(fring, 2048, flens))
+        bad = flens.copy()
+        bad[3] = 2049
+        with pytest.raises(A.ChksumError):
+            eng.rx_verify_slotted(fring, 2048, bad)
+        t, out = eng.submit_slotted(ring, 2048, lens)
+        eng.wait(t)
+        assert np.array_equal(out, oracle.batch_slotted(ring, 2048, lens))
+
+
+# ---- several engines in one process (engine group) ----------------------------------------
+
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0, 0]])
+@pytest.mark.parametrize("register", [False, True])
+def test_engine_group(oracle, devices, register):
+    """aipstack_chksum_engine_group_*: one process, one engine per listed device (all device 0
+    on this box), the batch split into disjoint ranges of about equal bytes, one host thread
+    per engine; every result against the oracle, every engine's status 0."""
+    with A.ChksumEngineGroup(devices, chunk_bytes=8 << 20, nstreams=2) as grp:
+        n = 300000
+        buf, off = synth.mixed_batch(n)
+        if register:
+            grp.register(buf)
+        assert np.array_equal(grp.csr(buf, off), oracle.batch_csr(buf, off))
+        assert grp.last_status == [0] * len(devices)
+        sb = synth.random_bytes(3, 100000 * 1500)
+        assert np.array_equal(grp.strided(sb, 1500, 1500, 100000, final=True),
+                              oracle.batch_strided(sb, 1500, 1500, 100000, final=True))
+        fr, foff = synth.frames_host(200000, seed=81, max_payload=1460)
+        if register:
+            grp.register(fr)
+        want = fr.copy()
+        want_st = oracle.tx_fill_batch(want, foff)
+        st = grp.tx_fill(fr, foff)
+        assert np.array_equal(st, want_st) and np.array_equal(fr, want)
+        _corrupt(fr, foff, 0.1, 4)
+        assert np.array_equal(grp.rx_verify(fr, foff), oracle.rx_verify_batch(fr, foff))
+        if register:
+            grp.unregister(fr)
+            grp.unregister(buf)
+        # fewer packets than engines: the idle engines report 0
+        one = grp.csr(buf, off[:2])
+        assert one[0] == oracle.batch_csr(buf, off[:2])[0]
+        bad = off[:4].copy()
+        bad[2] = bad[1] - 1
+        with pytest.raises(A.ChksumError):
+            grp.csr(buf, bad)
+
+
+def test_bench_e2e_engine_group_line():
+    """bench.py --e2e --engines 3 (all on device 0 here): one JSON line, bit-exact, the
+    engines and their devices named."""
+    import json
+    env = dict(os.environ, AIPSTACK_BENCH_FORCE_DEVICE="0")
+    r = subprocess.run([sys.executable, "bench.py", "--e2e", "--engines", "3", "--config", "C",
+                        "--steps", "2", "--warmup", "1"], cwd=ROOT, env=env, capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.strip()][-1])
+    assert d["parity"].startswith("bit-exact") and d["value"] > 0
+    assert d["config"]["engines"] == 3 and d["config"]["engine_devices"] == [0, 0, 0]
+
+
 # ---- frame decisions pinned by the reference's own call sites (tests/golden/frame_ref.py) ---
 
 @pytest.fixture(scope="module")

@@ -6,6 +6,8 @@
 #           (AIPSTACK_CHKSUM_TX_GATHER=0), interleaved; the split fill both ways; rocprof
 #           stats and FETCH/WRITE passes of TXREC; then pytest -m gpu
 #   check   pytest -m gpu, then bench A, C, CHAIN, TXREC, RX (no CPU baseline)
+#   slots   pytest -m gpu; ring-slot lines RX2K / C2K (+ their slot-read ceilings) and A2K;
+#           a U/P sweep of the slotted checksum; e2e through an engine group of 1/2/4
 set -e
 mode=${1:?mode}
 out=gpurun_out/r03/$mode
@@ -38,6 +40,25 @@ check)
       > "$out/pytest_gpu.log" 2>&1
   for c in A C CHAIN TXREC RX; do
     bench "bench_$c" --config $c --per-launch --no-cpu-baseline
+  done
+  ;;
+slots)
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+      > "$out/pytest_gpu.log" 2>&1
+  for c in RX2K C2K A2K; do
+    bench "bench_$c" --config $c --per-launch
+  done
+  for u in 1 2 3; do
+    for p in 4 8; do
+      AIPSTACK_CHKSUM_UNROLL=$u AIPSTACK_CHKSUM_PACKETS=$p bench sweep_C2K --config C2K \
+          --per-launch --no-cpu-baseline --no-parity
+    done
+  done
+  for f in 2 4 8; do
+    AIPSTACK_CHKSUM_FRAMES=$f bench sweep_RX2K --config RX2K --per-launch --no-cpu-baseline --no-parity
+  done
+  for e in 1 2 4; do
+    AIPSTACK_BENCH_FORCE_DEVICE=0 bench e2e_group --e2e --engines $e --config C --steps 5 --warmup 1
   done
   ;;
 *)
