@@ -58,7 +58,7 @@ __device__ __forceinline__ uint32_t from_next_lane(uint32_t v, uint32_t last, in
 
 struct StridedDesc {
     static constexpr bool kCsr = false;
-    static constexpr bool kStream = true;  // chunks may lie back to back (stream mode)
+    static constexpr bool kStream = true;  // SU > 0: stream mode for back-to-back chunks
     uint64_t base;    // absolute address of packet 0
     uint64_t stride;  // bytes between packet starts
     uint32_t len;     // bytes per packet
@@ -140,7 +140,9 @@ struct CsrDesc {
 // clamped to cap (nothing outside the slot is read) and reported (note_violation).
 struct SlottedDesc {
     static constexpr bool kCsr = false;
-    static constexpr bool kStream = false;  // slots are not back to back: wave mode only
+    static constexpr bool kStream = false;  // slots are not back to back: no contiguous run,
+                                            // but the gathered stream (SU > 0) reads just the
+                                            // packets' segments as one stream
     uint64_t base;          // absolute address of slot 0
     uint64_t stride;        // slot size in bytes
     const uint32_t *lens;   // n packet lengths

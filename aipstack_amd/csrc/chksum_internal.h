@@ -28,6 +28,8 @@ int take_violations_frames(uint32_t *mask, bool clear);
 int tuning_frames_in_flight();
 // Frames per chunk of the frame kernels: 64, or fewer for a small batch (pick_shape).
 uint32_t frames_per_chunk(uint64_t n, int cus);
+// The "chunk_packets" tunable (0 = automatic).
+int tuning_chunk_packets();
 
 // Resident-wave budget per CU the grids are sized to (tunable "waves_per_cu"; 0 = each
 // kernel's default).

@@ -38,6 +38,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 #include "aipstack_amd/chksum.h"
 #include "chksum_internal.h"
@@ -70,6 +71,19 @@ __global__ __launch_bounds__(kBlock) void chksum_batch_kernel(Desc desc, uint64_
     const bool final_flag = (flags & AIPSTACK_CHKSUM_FINAL) != 0;
     const uint32_t voff = (uint32_t)lane * 16u;          // this lane's segment in a slot
     const uint32_t not_lane0 = lane == 0 ? 0u : ~0u;     // head-mask lane select
+    // Ring slots with SU > 0: the chunk's 64 packets read as ONE gathered stream of just
+    // their 16-byte segments (the chain kernel's loader, chksum_device.h), 1 KiB per wave
+    // instruction however short the packets are, instead of one packet per wave instruction.
+    constexpr bool kGathered = !Desc::kStream && SU > 0;
+    struct GatheredShared {
+        GatherLds g[kWavesPerBlock];
+        KeepTable keep;
+    };
+    __shared__ typename std::conditional<kGathered, GatheredShared, char>::type gsh;
+    if constexpr (kGathered) {
+        fill_keep_table(gsh.keep);
+        __syncthreads();
+    }
 
     for (; c < c_end; ++c) {
         const uint64_t p0 = c * cpk;
@@ -85,7 +99,11 @@ __global__ __launch_bounds__(kBlock) void chksum_batch_kernel(Desc desc, uint64_
         // lane j: exact halves-sum of packet j (0 iff all its bytes are 0)
         uint32_t sums = 0;
         bool streamed = false;
-        if constexpr (SU > 0) {
+        if constexpr (kGathered) {
+            sums = sum_gathered_chunks<SU, NT>(lS, (uint32_t)(lE - lS), lane,
+                                               &gsh.g[wave_in_block], gsh.keep);
+            streamed = true;
+        } else if constexpr (SU > 0) {
             if (stream_ok(lS, lE, lane, cnt)) {
                 // back-to-back packets: the chunk read as one contiguous run
                 sums = sum_stream_chunk<SU, NT>(lS, lE, lane, cnt, voff);
@@ -386,6 +404,8 @@ int launch_k(const Desc &desc, uint64_t n, const Shape &sh, uint16_t *d_out, uin
     const int cus = device_cu_count(stream);
     if (cus <= 0) return AIPSTACK_CHKSUM_EHIP;
     uint64_t cpw = (uint64_t)tuning().chunks_per_wave.load(std::memory_order_relaxed);
+    if (cpw == 0 && !Desc::kStream && tuning().waves_per_cu.load(std::memory_order_relaxed) == 0)
+        cpw = 1;  // ring slots: one chunk per wave, the waves scheduled as CUs free up
     if (cpw == 0) {
         int wpc = tuning().waves_per_cu.load(std::memory_order_relaxed);
         if (wpc <= 0) wpc = Desc::kCsr ? 2 * kDefaultWavesPerCu : kDefaultWavesPerCu;
@@ -405,7 +425,7 @@ int launch_k(const Desc &desc, uint64_t n, const Shape &sh, uint16_t *d_out, uin
 template <class Desc, int U, int P, bool SEEDED>
 int launch_s(const Desc &desc, uint64_t n, const Shape &sh, uint16_t *d_out, uint32_t flags,
              hipStream_t stream) {
-    if constexpr (!Desc::kStream)  // ring slots: the per-packet wave mode only
+    if constexpr (!Desc::kStream)  // ring slots, per-packet wave mode (launch: gathered)
         return launch_k<Desc, U, P, true, SEEDED, 0>(desc, n, sh, d_out, flags, stream);
     if (tuning().nontemporal.load(std::memory_order_relaxed) == 0)  // sweeps only
         return launch_k<Desc, U, P, false, SEEDED, 0>(desc, n, sh, d_out, flags, stream);
@@ -442,7 +462,18 @@ int launch(const Desc &desc, uint64_t n, uint32_t max_len, uint16_t *d_out, uint
     if (n == 0) return AIPSTACK_CHKSUM_OK;
     const int cus = device_cu_count(stream);
     if (cus <= 0) return AIPSTACK_CHKSUM_EHIP;
-    const Shape sh = pick_shape(n, cus);
+    Shape sh = pick_shape(n, cus);
+    if constexpr (!Desc::kStream) {
+        // Ring slots: the gathered stream, 4 windows per group, 16-packet chunks, one chunk
+        // per wave ("stream" tunable: 2 = 2 windows, -1 = the per-packet wave mode). C2K
+        // (profiles/r03/ssweep): 263 us against 278 with 64-packet chunks and runs of chunks
+        // per wave, and 265 for the wave mode in the same shape.
+        if (!sh.small && tuning().chunk_packets.load(std::memory_order_relaxed) == 0)
+            sh.chunk_packets = 16;
+        const int su = tuning_stream_windows(4);
+        if (su == 4) return launch_k<Desc, 1, 1, true, SEEDED, 4>(desc, n, sh, d_out, flags, stream);
+        if (su != 0) return launch_k<Desc, 1, 1, true, SEEDED, 2>(desc, n, sh, d_out, flags, stream);
+    }
     switch (pick_unroll(max_len)) {
         case 1: return launch_u<Desc, 1, SEEDED>(desc, n, sh, d_out, flags, stream);
         case 2: return launch_u<Desc, 2, SEEDED>(desc, n, sh, d_out, flags, stream);
@@ -505,6 +536,8 @@ int tuning_stream_windows(int family_default) {
 }
 
 uint32_t frames_per_chunk(uint64_t n, int cus) { return pick_shape(n, cus).chunk_packets; }
+
+int tuning_chunk_packets() { return tuning().chunk_packets.load(std::memory_order_relaxed); }
 
 bool tuning_tx_gather(bool records_only) {
     const int t = tuning().tx_gather.load(std::memory_order_relaxed);

@@ -664,11 +664,17 @@ int launch_frames_g(const Desc &desc, uint64_t n, uint8_t *d_status, uint64_t *d
                     hipStream_t stream, int cus) {
     // small batches: fewer frames per chunk, so that they spread over many waves (as the
     // checksum batches, chksum_kernels.hip pick_shape)
-    const uint32_t cpk = frames_per_chunk(n, cus);
+    uint32_t cpk = frames_per_chunk(n, cus);
+    const int wpc = tuning_waves_per_cu();
+    // Ring slots: 32-frame chunks, one per wave (RX2K, profiles/r03/ssweep: 130 us against
+    // 136 with 64-frame chunks in runs per wave; 16-frame chunks 160; 1 segment per lane up
+    // front instead of 2: 144, profiles/r03/fsweep)
+    const bool slots = !Desc::kStream && cpk == (uint32_t)kWave && tuning_chunk_packets() == 0;
+    if (slots) cpk = 32;
     const uint64_t nchunks = (n + cpk - 1) / cpk;
     const int su = tuning_stream_windows(8);  // measured: 8 > 4 > off > 2 (RX and TX)
-    const int wpc = tuning_waves_per_cu();
-    const uint64_t target_waves = (uint64_t)cus * (wpc > 0 ? wpc : 128);
+    const uint64_t target_waves =
+        (slots && wpc <= 0) ? nchunks : (uint64_t)cus * (wpc > 0 ? wpc : 128);
     uint64_t cpw = (nchunks + target_waves - 1) / target_waves;
     if (cpw == 0) cpw = 1;
     const uint64_t waves = (nchunks + cpw - 1) / cpw;

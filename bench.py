@@ -688,6 +688,7 @@ def main():
                   else f"MISMATCH on rank(s) {bad}")
     pcis = [i["pci"] for i in infos]
 
+    traffic, traffic_stale = _pmc_traffic(args.config)
     slot_ceiling_fields = {}
     if layout in ("rxslot", "csrslot") and rank == 0:
         ceil = slot_read_ceiling(args.config, spec)
@@ -737,7 +738,8 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": _pmc_traffic(args.config),
+            "traffic": traffic,
+            **({"traffic_stale": traffic_stale} if traffic_stale else {}),
             "kernel_us": round(avg_kernel_s * 1e6, 2),
             **({"per_launch_us": {"min": round(per_launch[0], 2),
                                   "median": round(per_launch[len(per_launch) // 2], 2),
@@ -1125,19 +1127,42 @@ def oracle_check(spec, got, threads=1):
     return "bit-exact (whole batch vs oracle)" if np.array_equal(got, want) else "MISMATCH"
 
 
+KERNEL_SOURCES = ("aipstack_amd/csrc/chksum_device.h", "aipstack_amd/csrc/chksum_kernels.hip",
+                  "aipstack_amd/csrc/frame_kernels.hip")
+
+
+def kernel_source_digest():
+    """sha256 (16 hex digits) of the device-code sources: identifies the kernels a PMC
+    measurement was taken on (tools/pmc_summary.py records it with every entry)."""
+    import hashlib
+    h = hashlib.sha256()
+    for rel in KERNEL_SOURCES:
+        with open(os.path.join(ROOT, rel), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
 def _pmc_traffic(config):
     """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), measured
     by tools/pmc_run.sh on the same command: (2 x FETCH_SIZE + WRITE_SIZE) KiB, the x2
-    being the gfx950 correction of MI355X_MICROARCH.md (HBM section)."""
+    being the gfx950 correction of MI355X_MICROARCH.md (HBM section). Reported only if the
+    entry was measured on these kernel sources (its kernel_sources digest equals this
+    tree's); a stale entry gives null here and its value under roofline.traffic_stale."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
             d = json.load(f)
-        v = d.get(config, {}).get("hbm_bytes_per_launch")
-        return None if v is None else int(v)
+        e = d.get(config, {})
+        v = e.get("hbm_bytes_per_launch")
+        if v is None:
+            return None, None
+        if e.get("kernel_sources") != kernel_source_digest():
+            return None, {"hbm_bytes_per_launch": int(v),
+                          "measured_on_kernel_sources": e.get("kernel_sources"),
+                          "note": "PMC entry predates the current kernel sources"}
+        return int(v), None
     except (OSError, ValueError):
-        return None
-
+        return None, None
 
 if __name__ == "__main__":
     main()

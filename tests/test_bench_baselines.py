@@ -72,3 +72,101 @@ def test_cpu_baseline_frames(layout):
     res = bench.cpu_baseline_frames(spec, frames)
     assert res["value"] > 0 and res["kind"] == "port" and res["cores"] == 1
     assert res["affinity_cores"] >= 1
+
+
+def test_oracle_check_threaded_reference_and_mismatch():
+    """Every rank's own-shard check (bench.oracle_check): the reference's IpChksumInverted over
+    several threads (or the oracle port), bit-exact on the right answers, MISMATCH on a
+    flipped one."""
+    import ctypes
+    for layout in ("strided", "csr"):
+        if layout == "strided":
+            spec = {"layout": "strided", "n": 5000, "plen": 1500, "stride": 1500,
+                    "total": 5000 * 1500, "byte_offset": 3 * 5000 * 1500, "offsets": None,
+                    "first_packet": 15000}
+        else:
+            off = synth.mixed_offsets(2 * 4000)
+            spec = {"layout": "csr", "n": 4000, "plen": None,
+                    "offsets": off[4000:] - off[4000], "byte_offset": int(off[4000]),
+                    "first_packet": 4000}
+            spec["total"] = int(spec["offsets"][-1])
+        host = bench.host_shard(spec)
+        lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "libchksum_oracle.so"))
+        want = np.empty(spec["n"], dtype=np.uint16)
+        if layout == "strided":
+            lib.oracle_batch_strided.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                                                 ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32]
+            lib.oracle_batch_strided(host.ctypes.data, 1500, 1500, spec["n"], want.ctypes.data, 0)
+        else:
+            lib.oracle_batch_csr.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                             ctypes.c_void_p, ctypes.c_uint32]
+            o = spec["offsets"].astype(np.uint64)
+            lib.oracle_batch_csr(host.ctypes.data, o.ctypes.data, spec["n"], want.ctypes.data, 0)
+        assert bench.oracle_check(spec, want, threads=4).startswith("bit-exact")
+        bad = want.copy()
+        bad[123] ^= 1
+        assert bench.oracle_check(spec, bad, threads=4) == "MISMATCH"
+
+
+def test_slots_and_records_checks():
+    """The RX2K / C2K parity check (bench.slots_check) and the TXREC one (records_check)."""
+    import ctypes
+    spec = {"layout": "rxslot", "n": 3000, "seed": synth.SEED_DATA}
+    frames = bench.host_shard(spec)
+    ring, lens = synth.to_slots(frames, spec["offsets"], 2048)
+    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "libchksum_oracle.so"))
+    want = np.empty(3000, dtype=np.uint8)
+    lib.oracle_rx_verify_batch.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_uint64, ctypes.c_void_p]
+    o = spec["offsets"].astype(np.uint64)
+    lib.oracle_rx_verify_batch(frames.ctypes.data, o.ctypes.data, 3000, want.ctypes.data)
+    assert bench.slots_check("rxslot", ring, lens, want).startswith("bit-exact")
+    want[7] ^= 1
+    assert bench.slots_check("rxslot", ring, lens, want) == "MISMATCH"
+    # records: what the device returns, built here from the oracle's fill
+    tspec = {"layout": "txrec", "n": 2000, "seed": 77}
+    fr = bench.host_shard(tspec)
+    filled = fr.copy()
+    st = np.empty(2000, dtype=np.uint8)
+    lib.oracle_tx_fill_batch.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_uint64, ctypes.c_void_p]
+    to = tspec["offsets"].astype(np.uint64)
+    lib.oracle_tx_fill_batch(filled.ctypes.data, to.ctypes.data, 2000, st.ctypes.data)
+    rec = np.zeros(2000, dtype=np.uint64)
+    for i in range(2000):
+        s = int(to[i])
+        hl = (int(filled[s + 14]) & 15) * 4 if filled[s + 12] == 8 and filled[s + 13] == 0 else 0
+        w1 = int(st[i]) << 16
+        w0 = 0
+        if fr[s + 24] != filled[s + 24] or fr[s + 25] != filled[s + 25] or st[i] in (3, 6, 8, 4):
+            if hl:
+                w0 |= (int(filled[s + 24]) << 8) | int(filled[s + 25])
+                w1 |= 1 << 8
+        if st[i] == 6:
+            proto = int(filled[s + 23])
+            fo = {6: 16, 17: 6, 1: 2}[proto]
+            fld = 14 + hl + fo
+            w0 |= ((int(filled[s + fld]) << 8) | int(filled[s + fld + 1])) << 16
+            w1 |= fld | (1 << 9)
+        rec[i] = w0 | (w1 << 32)
+    assert bench.records_check(tspec, fr, fr.copy(), rec.view(np.int64)).startswith("bit-exact")
+    rec[5] ^= np.uint64(1 << 16)
+    assert bench.records_check(tspec, fr, fr.copy(), rec.view(np.int64)) == "MISMATCH"
+
+
+def test_pmc_traffic_only_for_the_current_kernels(tmp_path, monkeypatch):
+    """roofline.traffic comes from profiles/pmc_traffic.json only while the entry's kernel
+    source digest matches this tree; otherwise null, the old value under traffic_stale."""
+    import json
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    digest = bench.kernel_source_digest()
+    (prof / "pmc_traffic.json").write_text(json.dumps({
+        "A": {"hbm_bytes_per_launch": 123, "kernel_sources": digest},
+        "C": {"hbm_bytes_per_launch": 456, "kernel_sources": "0" * 16}}))
+    for rel in bench.KERNEL_SOURCES:
+        (tmp_path / rel).parent.mkdir(parents=True, exist_ok=True)
+        (tmp_path / rel).write_bytes(open(os.path.join(ROOT, rel), "rb").read())
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    assert bench._pmc_traffic("A") == (123, None)
+    t, stale = bench._pmc_traffic("C")
+    assert t is None and stale["hbm_bytes_per_launch"] == 456
+    assert bench._pmc_traffic("B") == (None, None)

@@ -1018,10 +1018,13 @@ def test_tx_fill_edge_frames(oracle, stream_mode, shift, su, split):
 
 # ---- ring slots: one packet / frame per fixed slot, a length per slot ---------------------
 
+@pytest.mark.parametrize("su", [0, 4, -1])
 @pytest.mark.parametrize("stride", [64, 1517, 2048, 9216, 65536])
-def test_slotted_checksums(oracle, stride):
+def test_slotted_checksums(oracle, stream_mode, stride, su):
     """aipstack_chksum_batch_slotted: lengths 0..min(stride, 65535) at every slot alignment
-    an odd stride gives, slack bytes random; inverted and FINAL."""
+    an odd stride gives, slack bytes random; inverted and FINAL; the gathered stream (2 or 4
+    windows) and the per-packet wave mode (su = -1)."""
+    stream_mode(su)
     rng = np.random.default_rng(stride)
     n = {64: 50000, 1517: 20000, 2048: 20000, 9216: 3000, 65536: 300}[stride]
     cap = min(stride, 65535)

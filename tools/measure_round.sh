@@ -1,12 +1,17 @@
 #!/bin/bash
-# One round's GPU measurements, written under gpurun_out/$1 (e.g. r02). Phases (arg 2,
+# One round's GPU measurements, written under gpurun_out/$1 (e.g. r03). Phases (arg 2,
 # default "all"; each fits one gpurun call on its own):
 #   test   pytest -m gpu (the round-end gate) and smoke()
 #   bench  hbm_peak.jsonl (streaming-read ceiling + slotted-read ceiling, tools/hbm_peak.hip);
-#          bench_{A,B,C,A2K,RX,TX,CHAIN}.json (A with the CPU baseline); e2e.jsonl;
-#          prof_{A,C,A2K,RX,TX,CHAIN}/: rocprofv3 --kernel-trace --stats of the bench command
-#   pmc    pmc_{A,B,C,A2K,RX,TX,CHAIN}/: PMC passes (FETCH_SIZE, WRITE_SIZE, SQ instruction mix)
+#          bench_<CFG>.json for every config (A with the CPU baseline; RX2K / C2K with their
+#          slot-read ceilings); e2e.jsonl (single engine, and an engine group of 2);
+#          prof_<CFG>/: rocprofv3 --kernel-trace --stats of the bench command
+#   pmc    pmc_<CFG>/: PMC passes (FETCH_SIZE, WRITE_SIZE, SQ instruction mix); summarise
+#          with tools/pmc_summary.py on the same tree (entries record the kernel digest)
 #   sweep  sweep_{A,B,C,RX,TX}.jsonl: launch-parameter sweeps (tools/sweep.py)
+#   rank8  the driver's 8-rank launch rehearsed on a 1-GPU box (all ranks on device 0):
+#          control plane, per-rank parity and device ids (throughput is shared)
+#   small  small batches (bench.py --small) for A, RX and TX, eager vs graph replay
 set -e
 tag=${1:-r02}
 phase=${2:-all}
@@ -21,12 +26,8 @@ fi
 if [ "$phase" = bench ] || [ "$phase" = all ]; then
   timeout -k 10 120 tools/build/hbm_peak > "$out/hbm_peak.jsonl"
   timeout -k 10 300 python bench.py > "$out/bench_A.json" 2> "$out/bench_A.err"
-  for c in B C A2K; do
+  for c in B C A2K C2K RX RX2K TX TXREC CHAIN; do
     timeout -k 10 300 python bench.py --config $c --per-launch \
-        > "$out/bench_$c.json" 2> "$out/bench_$c.err"
-  done
-  for c in RX TX CHAIN; do
-    timeout -k 10 300 python bench.py --config $c --steps 20 --per-launch \
         > "$out/bench_$c.json" 2> "$out/bench_$c.err"
   done
   : > "$out/e2e.jsonl"
@@ -34,17 +35,33 @@ if [ "$phase" = bench ] || [ "$phase" = all ]; then
     timeout -k 10 300 python bench.py --e2e --config $c --steps 5 --warmup 1 >> "$out/e2e.jsonl" 2>> "$out/e2e.err"
     timeout -k 10 300 python bench.py --e2e --e2e-pageable --config $c --steps 3 --warmup 1 >> "$out/e2e.jsonl" 2>> "$out/e2e.err"
   done
-  for c in A C A2K RX TX CHAIN; do
+  AIPSTACK_BENCH_FORCE_DEVICE=0 timeout -k 10 300 python bench.py --e2e --engines 2 --config C \
+      --steps 5 --warmup 1 >> "$out/e2e.jsonl" 2>> "$out/e2e.err"
+  for c in A C A2K C2K RX RX2K TX TXREC CHAIN; do
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/prof_$c" -o run \
         -- python3 bench.py --config $c --no-cpu-baseline --no-parity > "$out/prof_$c.log" 2>&1
   done
 fi
 if [ "$phase" = pmc ] || [ "$phase" = all ]; then
-  for c in A B C A2K RX TX CHAIN; do tools/pmc_run.sh $c "$out/pmc_$c"; done
+  for c in A B C A2K C2K RX RX2K TX TXREC CHAIN; do tools/pmc_run.sh $c "$out/pmc_$c"; done
 fi
 if [ "$phase" = sweep ] || [ "$phase" = all ]; then
   for c in A B C A2K RX TX; do
     timeout -k 10 200 python tools/sweep.py --config $c > "$out/sweep_$c.jsonl" 2> "$out/sweep_$c.err"
+  done
+fi
+if [ "$phase" = rank8 ]; then
+  for c in A C; do
+    AIPSTACK_BENCH_FORCE_DEVICE=0 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 \
+        --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 8 \
+        --config $c --steps 5 --warmup 2 --cpu-reps 3 > "$out/bench8_$c.json" 2> "$out/bench8_$c.err"
+  done
+fi
+if [ "$phase" = small ]; then
+  for n in 64 1024 4096 16384; do
+    for c in A RX TX; do
+      timeout -k 10 120 python bench.py --config $c --small $n >> "$out/small.jsonl" 2>> "$out/small.err"
+    done
   done
 fi
 echo "measure_round: $phase done"

@@ -12,6 +12,11 @@ algorithmic bytes per launch come from the same round's bench_<CFG>.json, so
 `ratio` = measured / algorithmic HBM bytes (1.0 = no re-reads).
 
     python tools/pmc_summary.py gpurun_out/r01b profiles/pmc_traffic.json
+
+Run it on the tree the counters were taken on: every entry records the digest of the kernel
+sources (bench.kernel_source_digest), and bench.py reports an entry's traffic only while the
+sources still match (else null, with the old value under roofline.traffic_stale). Existing
+entries of other configs are kept.
 """
 import csv
 import glob
@@ -69,18 +74,28 @@ def summarise(round_dir, cfg):
 
 def main():
     round_dir, out_path = sys.argv[1], sys.argv[2]
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import kernel_source_digest  # the kernels these counters were taken on
+    digest = kernel_source_digest()
+    merge = os.path.exists(out_path)
     doc = {
         "source": f"tools/pmc_run.sh on MI355X ({round_dir}); median over dispatches "
                   "excluding the first",
         "formula": "hbm_bytes_per_launch = (2*FETCH_SIZE + WRITE_SIZE) * 1024  (FETCH_SIZE x2: "
                    "gfx950 half-count for wide streaming reads, MI355X_MICROARCH.md HBM)",
     }
+    if merge:  # keep the other configs' entries; replace the ones measured here
+        with open(out_path) as f:
+            old = json.load(f)
+        doc = {**old, "source": doc["source"], "formula": doc["formula"]}
     for d in sorted(glob.glob(os.path.join(round_dir, "pmc_*"))):
         if not os.path.isdir(d):
             continue
         cfg = os.path.basename(d)[len("pmc_"):]
         rec = summarise(round_dir, cfg)
         if rec:
+            rec["kernel_sources"] = digest
+            rec["measured_in"] = round_dir
             doc[cfg] = rec
     with open(out_path, "w") as f:
         json.dump(doc, f, indent=1)

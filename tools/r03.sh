@@ -61,6 +61,60 @@ slots)
     AIPSTACK_BENCH_FORCE_DEVICE=0 bench e2e_group --e2e --engines $e --config C --steps 5 --warmup 1
   done
   ;;
+gslot)
+  # the gathered stream for ring slots (C2K) against the wave mode, interleaved
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+      -k "slotted or slot" > "$out/pytest_slots.log" 2>&1
+  for i in 1 2; do
+    bench c2k --config C2K --per-launch --no-cpu-baseline
+    AIPSTACK_CHKSUM_STREAM=4 bench c2k_su4 --config C2K --per-launch --no-cpu-baseline --no-parity
+    AIPSTACK_CHKSUM_STREAM=-1 bench c2k_wave --config C2K --per-launch --no-cpu-baseline --no-parity
+    AIPSTACK_CHKSUM_WAVES_PER_CU=128 bench c2k_w128 --config C2K --per-launch --no-cpu-baseline --no-parity
+  done
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/prof_C2K" -o run \
+      -- python3 bench.py --config C2K --no-cpu-baseline --no-parity > "$out/prof_C2K.log" 2>&1
+  ;;
+ssweep)
+  # ring slots: chunk size, waves, gathered vs wave mode (tools/slot_sweep.py, interleaved)
+  timeout -k 10 400 python tools/slot_sweep.py --config C2K --variants \
+"stream=-1;stream=-1,chunk_packets=16,chunks_per_wave=1;stream=-1,chunk_packets=8,chunks_per_wave=1;\
+stream=-1,chunk_packets=32,chunks_per_wave=1;stream=-1,chunk_packets=16,chunks_per_wave=1,packets=4;\
+stream=-1,chunk_packets=16,chunks_per_wave=1,unroll=1;stream=-1,chunk_packets=16,chunks_per_wave=2;\
+stream=4,chunk_packets=16,chunks_per_wave=1;stream=4,chunks_per_wave=1" > "$out/c2k.jsonl" 2> "$out/c2k.err"
+  timeout -k 10 400 python tools/slot_sweep.py --config RX2K --variants \
+"frames=4;frames=8;frames=4,chunk_packets=16,waves_per_cu=100000;frames=4,chunk_packets=32,waves_per_cu=100000;\
+frames=8,chunk_packets=16,waves_per_cu=100000;frames=4,waves_per_cu=100000;frames=2,chunk_packets=16,waves_per_cu=100000;\
+frames=4,chunk_packets=8,waves_per_cu=100000" > "$out/rx2k.jsonl" 2> "$out/rx2k.err"
+  ;;
+coal)
+  # ring-slot frames: coalesced header loads + LDS transpose (product) vs per-lane header
+  # loads (tools/build/lib_nocoal.so), alternating processes; slot tests first
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+      -k "slot" > "$out/pytest_slots.log" 2>&1
+  for i in 1 2 3; do
+    timeout -k 10 300 python tools/slot_sweep.py --config RX2K --variants "frames=4;frames=8" \
+        >> "$out/rx2k_coal.jsonl" 2>> "$out/err"
+    timeout -k 10 300 python tools/slot_sweep.py --config RX2K --variants "frames=4;frames=8" \
+        --lib tools/build/lib_nocoal.so >> "$out/rx2k_nocoal.jsonl" 2>> "$out/err"
+  done
+  for c in RX2K C2K; do bench "bench_$c" --config $c --per-launch; done
+  # one-pass Tx fill: 2-byte field stores (product) vs whole 16-byte field segments
+  # (tools/build/lib_segstore.so), alternating processes; the split fill beside them
+  for i in 1 2; do
+    bench tx_inplace --config TX --tx-inplace --per-launch --no-cpu-baseline
+    AIPSTACK_AMD_LIB=tools/build/lib_segstore.so bench tx_inplace_seg --config TX --tx-inplace \
+        --per-launch --no-cpu-baseline
+    bench tx_split --config TX --per-launch --no-cpu-baseline
+  done
+  ;;
+fsweep)
+  # ring-slot frames: segments per lane up front (unroll 1/2), frames in flight, chunk size
+  timeout -k 10 600 python tools/slot_sweep.py --config RX2K --variants \
+"frames=4;frames=4,unroll=1;frames=8,unroll=1;frames=2,unroll=1;frames=8;\
+frames=4,unroll=1,chunk_packets=64,waves_per_cu=100000;frames=8,unroll=1,chunk_packets=64,waves_per_cu=100000;\
+frames=4,unroll=1,chunk_packets=16,waves_per_cu=100000" > "$out/rx2k.jsonl" 2> "$out/rx2k.err"
+  bench bench_RX2K --config RX2K --per-launch
+  ;;
 *)
   echo "unknown mode $mode" >&2; exit 2 ;;
 esac
