@@ -236,7 +236,8 @@ int drain(aipstack_chksum_engine *e, Slot &s, bool blocking = true) {
 template <class Chunker, class Launch>
 int enqueue(aipstack_chksum_engine *e, uint64_t n, void *h_out, uint32_t elem, Chunker chunker,
             Launch launch, uint64_t *ticket) {
-    if (hipSetDevice(e->device) != hipSuccess) return AIPSTACK_CHKSUM_ENODEV;
+    DeviceGuard dg(e->device);
+    if (!dg.ok) return AIPSTACK_CHKSUM_ENODEV;
     const uint64_t t = e->next_ticket++;
     *ticket = t;
     int status = AIPSTACK_CHKSUM_OK;
@@ -292,7 +293,8 @@ int enqueue(aipstack_chksum_engine *e, uint64_t n, void *h_out, uint32_t elem, C
 // only), < 0 = it failed (its first failure; the record is consumed).
 int complete(aipstack_chksum_engine *e, uint64_t ticket, bool blocking) {
     if (ticket == 0 || ticket >= e->next_ticket) return AIPSTACK_CHKSUM_EINVAL;
-    if (hipSetDevice(e->device) != hipSuccess) return AIPSTACK_CHKSUM_ENODEV;
+    DeviceGuard dg(e->device);
+    if (!dg.ok) return AIPSTACK_CHKSUM_ENODEV;
     int pending = 0;
     for (Slot &s : e->slots) {
         if (!s.busy || s.ticket != ticket) continue;
@@ -323,7 +325,8 @@ extern "C" int aipstack_chksum_engine_create(int device, uint64_t chunk_bytes, i
     if (chunk_bytes < (1u << 17)) chunk_bytes = 1u << 17;  // >= 2 max-size packets
     const int dc = aipstack_chksum_device_check(device);
     if (dc != AIPSTACK_CHKSUM_OK) return dc;
-    if (hipSetDevice(device) != hipSuccess) return AIPSTACK_CHKSUM_ENODEV;
+    DeviceGuard dg(device);
+    if (!dg.ok) return AIPSTACK_CHKSUM_ENODEV;
     auto *e = new (std::nothrow) aipstack_chksum_engine;
     if (!e) return AIPSTACK_CHKSUM_EINVAL;
     e->device = device;
@@ -355,7 +358,7 @@ extern "C" void aipstack_chksum_engine_destroy(aipstack_chksum_engine *e) {
     if (!e) return;
     {
         std::lock_guard<std::mutex> lock(e->mu);
-        (void)hipSetDevice(e->device);
+        DeviceGuard dg(e->device);
         drain_all(e);  // pieces in flight complete: results written, Tx fields applied
     }
     release(e);
@@ -374,7 +377,7 @@ void engine_drop_region(aipstack_chksum_engine *e, const void *p) {
     std::lock_guard<std::mutex> lock(e->mu);
     for (size_t i = 0; i < e->registered.size(); ++i) {
         if (e->registered[i].p == p) {
-            (void)hipSetDevice(e->device);
+            DeviceGuard dg(e->device);
             drain_all(e);
             e->registered.erase(e->registered.begin() + (long)i);
             return;
@@ -387,7 +390,8 @@ extern "C" int aipstack_chksum_engine_register(aipstack_chksum_engine *e, void *
                                                uint64_t bytes) {
     if (!e || !host_ptr || bytes == 0) return AIPSTACK_CHKSUM_EINVAL;
     std::lock_guard<std::mutex> lock(e->mu);
-    if (hipSetDevice(e->device) != hipSuccess) return AIPSTACK_CHKSUM_ENODEV;
+    DeviceGuard dg(e->device);
+    if (!dg.ok) return AIPSTACK_CHKSUM_ENODEV;
     const int st = check_hip(hipHostRegister(host_ptr, bytes, hipHostRegisterDefault));
     if (st == AIPSTACK_CHKSUM_OK)
         e->registered.push_back(Region{static_cast<char *>(host_ptr), bytes, true});
@@ -399,7 +403,7 @@ extern "C" int aipstack_chksum_engine_unregister(aipstack_chksum_engine *e, void
     std::lock_guard<std::mutex> lock(e->mu);
     for (size_t i = 0; i < e->registered.size(); ++i) {
         if (e->registered[i].p == host_ptr) {
-            (void)hipSetDevice(e->device);
+            DeviceGuard dg(e->device);
             // pieces in flight may still DMA from (or, Tx, complete into) the region
             drain_all(e);
             const int st = e->registered[i].owned ? check_hip(hipHostUnregister(host_ptr))

@@ -111,10 +111,14 @@ extern "C" int aipstack_chksum_engine_group_create(const int *devices, int n_dev
 
 extern "C" void aipstack_chksum_engine_group_destroy(aipstack_chksum_engine_group *g) {
     if (!g) return;
-    std::lock_guard<std::mutex> lock(g->mu);
-    for (aipstack_chksum_engine *e : g->engines) aipstack_chksum_engine_destroy(e);
-    for (const void *p : g->regions) (void)hipHostUnregister(const_cast<void *>(p));
-    delete g;
+    {
+        std::lock_guard<std::mutex> lock(g->mu);
+        for (aipstack_chksum_engine *e : g->engines) aipstack_chksum_engine_destroy(e);
+        for (const void *p : g->regions) (void)hipHostUnregister(const_cast<void *>(p));
+        g->regions.clear();
+        g->engines.clear();
+    }
+    delete g;  // after the lock is released (its mutex is a member)
 }
 
 extern "C" int aipstack_chksum_engine_group_size(const aipstack_chksum_engine_group *g) {
@@ -125,7 +129,8 @@ extern "C" int aipstack_chksum_engine_group_register(aipstack_chksum_engine_grou
                                                      void *host_ptr, uint64_t bytes) {
     if (!g || !host_ptr || bytes == 0) return AIPSTACK_CHKSUM_EINVAL;
     std::lock_guard<std::mutex> lock(g->mu);
-    if (hipSetDevice(g->devices[0]) != hipSuccess) return AIPSTACK_CHKSUM_ENODEV;
+    DeviceGuard dg(g->devices[0]);
+    if (!dg.ok) return AIPSTACK_CHKSUM_ENODEV;
     const int st = check_hip(hipHostRegister(host_ptr, bytes, hipHostRegisterPortable));
     if (st != AIPSTACK_CHKSUM_OK) return st;
     g->regions.push_back(host_ptr);

@@ -9,6 +9,22 @@ namespace aipstack_amd {
 // Records `e` as this thread's last HIP error and maps it to a status code.
 int check_hip(hipError_t e);
 
+// Makes `device` current for the scope and restores the caller's device after it: the
+// engine's calls must not change which device the calling thread (e.g. torch) works on.
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = false;
+    explicit DeviceGuard(int device) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        ok = hipSetDevice(device) == hipSuccess;
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+    DeviceGuard(const DeviceGuard &) = delete;
+    DeviceGuard &operator=(const DeviceGuard &) = delete;
+};
+
 // Compute units of the device `stream` belongs to (the current device for the null
 // stream), cached per device id; <= 0 on failure.
 int device_cu_count(hipStream_t stream);
