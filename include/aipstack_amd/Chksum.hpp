@@ -68,33 +68,34 @@ struct IpBufRef {
     IpBufRef subTo(std::size_t new_tot_len) const { return IpBufRef{node, offset, new_tot_len}; }
 };
 
-// BufUtils.h:129-178: visit each non-empty chunk of the first process_len bytes; moves
-// to the next node eagerly. `fn(char *ptr, size_t len)` returns how many it consumed.
+// BufUtils.h:129-178 (same contract): hands `fn(char *ptr, size_t len)` the non-empty
+// pieces of the first process_len bytes, node by node; `fn` returns how many bytes of its
+// piece it took, and taking fewer ends the walk inside that node. The returned reference
+// starts after the bytes taken and keeps everything not taken (tot_len shrinks by exactly
+// that count). A node that was used up is left behind even when nothing more is wanted,
+// as long as it has a successor -- the reference's eager advance, which also steps over
+// empty nodes.
 template <typename Fn>
 IpBufRef ipBufProcessBytes(IpBufRef buf, std::size_t process_len, Fn &&fn) {
-    std::size_t remain = buf.tot_len - process_len;
-    buf.tot_len = process_len;
+    std::size_t const untouched = buf.tot_len - process_len;
+    IpBufNode const *at = buf.node;
+    std::size_t pos = buf.offset;  // inside *at
+    std::size_t want = process_len;
     for (;;) {
-        IpBufNode const node = *buf.node;
-        std::size_t node_rem = node.len - buf.offset;
-        bool consumed = buf.tot_len >= node_rem;
-        std::size_t chunk = consumed ? node_rem : buf.tot_len;
-        if (chunk > 0) {
-            std::size_t done = fn(node.ptr + buf.offset, chunk);
-            buf.tot_len -= done;
-            buf.offset += done;
-            if (done < chunk) {
-                remain += buf.tot_len;
-                buf.tot_len = 0;
-                break;
-            }
+        std::size_t const avail = at->len - pos;
+        bool const uses_up_node = want >= avail;
+        std::size_t const piece = uses_up_node ? avail : want;
+        if (piece != 0) {
+            std::size_t const took = fn(at->ptr + pos, piece);
+            pos += took;
+            want -= took;
+            if (took != piece) break;  // the visitor stopped early
         }
-        if (!consumed || node.next == nullptr) break;
-        buf.node = node.next;
-        buf.offset = 0;
+        if (!uses_up_node || at->next == nullptr) break;
+        at = at->next;
+        pos = 0;
     }
-    buf.tot_len = remain;
-    return buf;
+    return IpBufRef{at, pos, want + untouched};
 }
 
 // Chksum.h:148-316. Same observable behaviour (State export/resume, header words added

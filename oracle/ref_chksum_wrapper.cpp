@@ -189,4 +189,6 @@ double ref_time_batch_chain(int threads, int reps, std::uint64_t addr_bias,
 using AIpStack::IpChksum;
 using AIpStack::WrapType;
 #define CS_NAME(x) ref_cs_##x
+#define CS_PROCESS_BYTES(buf, len, fn) \
+    AIpStack::ipBufProcessBytes(buf, len, AIpStack::makeTypedFunction(fn))
 #include "call_sites.inc"

@@ -23,6 +23,7 @@
 using namespace AIpStackAmd;
 
 #define CS_NAME(x) cs_##x
+#define CS_PROCESS_BYTES(buf, len, fn) ipBufProcessBytes(buf, len, fn)
 #include "call_sites.inc"
 
 namespace {

@@ -36,4 +36,5 @@ extern "C" std::uint16_t hpp_accumulate(const std::uint16_t *w16, std::size_t n1
 extern "C" std::uint16_t hpp_chksum(const char *p, std::size_t n) { return IpChksum(p, n); }
 
 #define CS_NAME(x) hpp_cs_##x
+#define CS_PROCESS_BYTES(buf, len, fn) ipBufProcessBytes(buf, len, fn)
 #include "call_sites.inc"

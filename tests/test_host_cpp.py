@@ -117,6 +117,53 @@ def test_call_sites_live_vs_reference(golden):
         assert call_sites.evaluate(hpp, "hpp", c, blob) == call_sites.evaluate(ref, "ref", c, blob), c
 
 
+def _walk(lib, prefix, blob, lens, offset, tot_len, process_len, budget):
+    fn = getattr(lib, f"{prefix}_cs_walk")
+    fn.restype = ctypes.c_size_t
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
+                   ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p,
+                   ctypes.c_size_t, ctypes.c_void_p]
+    starts = np.concatenate([[0], np.cumsum(lens)[:-1]]) if len(lens) else np.zeros(0, np.int64)
+    k = max(len(lens), 1)
+    ptrs = (ctypes.c_void_p * k)(*[blob.ctypes.data + int(o) for o in starts])
+    ln = (ctypes.c_size_t * k)(*[int(l) for l in lens])
+    pieces = np.zeros(2 * 64, dtype=np.uint64)
+    out = np.zeros(3, dtype=np.uint64)
+    cnt = fn(ptrs, ln, len(lens), offset, tot_len, process_len, budget, pieces.ctypes.data, 64,
+             out.ctypes.data)
+    rel = [(int(pieces[2 * i]) - blob.ctypes.data, int(pieces[2 * i + 1]))
+           for i in range(min(cnt, 64))]
+    return cnt, rel, [int(x) for x in out]
+
+
+@pytest.mark.skipif(not os.path.exists(REF_LIB), reason="reference library not built here")
+def test_ip_buf_process_bytes_vs_reference(golden):
+    """ipBufProcessBytes (BufUtils.h:129-178) itself, compiled from call_sites.inc against the
+    reference and against Chksum.hpp: the pieces offered, the returned node / offset /
+    tot_len, with visitors that stop early (budget), empty nodes (the eager advance steps
+    over them), process_len below tot_len and offsets inside the first node."""
+    ref = ctypes.CDLL(REF_LIB)
+    hpp = ctypes.CDLL(_built("libhpp_shim.so")[0])
+    blob = golden["blob"]
+    rng = np.random.default_rng(2024)
+    n_cases = 0
+    for _ in range(3000):
+        nn = int(rng.integers(1, 7))
+        lens = [int(x) for x in rng.integers(0, 9, size=nn)]
+        if rng.random() < 0.5:
+            lens = [l * int(rng.integers(1, 40)) for l in lens]
+        total = sum(lens)
+        offset = int(rng.integers(0, lens[0] + 1))
+        tot_len = int(rng.integers(0, total - offset + 1))
+        process_len = int(rng.integers(0, tot_len + 1))
+        budget = int(rng.integers(0, process_len + 2)) if rng.random() < 0.5 else 1 << 40
+        args = (blob, lens, offset, tot_len, process_len, budget)
+        assert _walk(hpp, "hpp", *args) == _walk(ref, "ref", *args), (lens, offset, tot_len,
+                                                                      process_len, budget)
+        n_cases += 1
+    assert n_cases == 3000
+
+
 def _write_case_files(tmp_path, cases, blob):
     blob_path = tmp_path / "blob.bin"
     blob.tofile(blob_path)
