@@ -649,6 +649,37 @@ class ChksumEngine:
             "aipstack_chksum_engine_host_rx_verify_slotted")
         return out
 
+    def submit_rx_verify_slotted(self, frames: np.ndarray, slot_stride: int, lens, *,
+                                 out=None):
+        """Enqueue an Rx verify batch of frame slots; returns (ticket, out). The slots must
+        not be refilled until the ticket completes (the receive loop of a TAP ring:
+        tap/linux/TapDeviceLinux.cpp:156-178)."""
+        ln, n = self._slot_args(frames, slot_stride, lens)
+        out = self._host_args(frames, out, n, np.uint8)
+        t = ctypes.c_uint64(0)
+        st = self._lib.aipstack_chksum_engine_submit_rx_verify_slotted(
+            self._h, frames.ctypes.data, slot_stride, ln.ctypes.data, n, out.ctypes.data,
+            ctypes.byref(t))
+        self._submitted(st, t.value, "aipstack_chksum_engine_submit_rx_verify_slotted", frames,
+                        ln, out)
+        return t.value, out
+
+    def submit_tx_fill_slotted(self, frames: np.ndarray, slot_stride: int, lens, *,
+                               status=None):
+        """Enqueue a Tx fill of frame slots, in place; returns (ticket, status). The frames
+        are filled when the ticket completes and must not be touched until then."""
+        if not frames.flags.writeable:
+            raise ValueError("frames must be writable (filled in place)")
+        ln, n = self._slot_args(frames, slot_stride, lens)
+        status = self._host_args(frames, status, n, np.uint8)
+        t = ctypes.c_uint64(0)
+        st = self._lib.aipstack_chksum_engine_submit_tx_fill_slotted(
+            self._h, frames.ctypes.data, slot_stride, ln.ctypes.data, n, status.ctypes.data,
+            ctypes.byref(t))
+        self._submitted(st, t.value, "aipstack_chksum_engine_submit_tx_fill_slotted", frames,
+                        ln, status)
+        return t.value, status
+
     def tx_fill_slotted(self, frames: np.ndarray, slot_stride: int, lens, *,
                         status=None) -> np.ndarray:
         """Tx fill, in place, of a ring of frame slots in HOST memory."""

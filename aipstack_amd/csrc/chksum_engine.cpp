@@ -31,6 +31,7 @@
 #include <atomic>
 #include <chrono>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -80,6 +81,7 @@ struct aipstack_chksum_engine {
     int device = 0;
     uint64_t chunk_bytes = 0;
     uint64_t chunk_packets = 0;
+    bool slot_rows = true;  // ring slots: copy each slot's used prefix only (2-D copy)
     std::vector<Slot> slots;
     std::vector<Region> registered;
     size_t next_slot = 0;      // round robin over the slots, across batches
@@ -229,10 +231,41 @@ int drain(aipstack_chksum_engine *e, Slot &s, bool blocking = true) {
     return st;
 }
 
-// Enqueue one batch as chunks over the slots. chunker(i0, &i1, &src, &bytes) describes
-// chunk [i0, i1) of packets and its byte range in host memory; launch(slot, i0, i1)
-// enqueues its kernel, whose results (elem bytes per packet) land in the slot's d_out.
-// Returns the status of the enqueue; *ticket identifies the batch.
+// Pageable ring slots into pinned staging: only the first `width` bytes of each `pitch`-byte
+// row (the rest of a slot is never read), by the same threads as stage_copy.
+void stage_copy_rows(void *dst, const void *src, uint64_t pitch, uint64_t width, uint64_t rows) {
+    auto run = [=](uint64_t lo, uint64_t hi) {
+        for (uint64_t r = lo; r < hi; ++r)
+            std::memcpy(static_cast<char *>(dst) + r * pitch,
+                        static_cast<const char *>(src) + r * pitch, width);
+    };
+    const unsigned hw = std::thread::hardware_concurrency();
+    const unsigned nt = (unsigned)std::min<uint64_t>(
+        std::min<uint64_t>(rows * width / (4ull << 20), 8), hw ? hw : 1);
+    if (nt <= 1) {
+        run(0, rows);
+        return;
+    }
+    const uint64_t per = (rows + nt - 1) / nt;
+    std::vector<std::thread> pool;
+    for (unsigned t = 0; t < nt && (uint64_t)t * per < rows; ++t)
+        pool.emplace_back(run, (uint64_t)t * per, std::min(rows, (uint64_t)(t + 1) * per));
+    for (std::thread &t : pool) t.join();
+}
+
+// A piece's host bytes: `bytes` from `src`, or -- when width is set -- rows of `pitch` bytes
+// of which only the first `width` travel (ring slots: the slack after the longest frame of
+// the piece stays behind; the device copy keeps the slot layout).
+struct Span {
+    const char *src = nullptr;
+    uint64_t bytes = 0;
+    uint64_t pitch = 0, width = 0;
+};
+
+// Enqueue one batch as chunks over the slots. chunker(i0, &i1, &span) describes chunk
+// [i0, i1) of packets and its bytes in host memory; launch(slot, i0, i1) enqueues its
+// kernel, whose results (elem bytes per packet) land in the slot's d_out. Returns the
+// status of the enqueue; *ticket identifies the batch.
 template <class Chunker, class Launch>
 int enqueue(aipstack_chksum_engine *e, uint64_t n, void *h_out, uint32_t elem, Chunker chunker,
             Launch launch, uint64_t *ticket) {
@@ -256,17 +289,24 @@ int enqueue(aipstack_chksum_engine *e, uint64_t n, void *h_out, uint32_t elem, C
         }
         s.tx_frames = nullptr;  // a Tx fill's launch sets it again
         uint64_t i1 = 0;
-        const char *src = nullptr;
-        uint64_t bytes = 0;
-        chunker(i0, &i1, &src, &bytes);
+        Span sp;
+        chunker(i0, &i1, &sp);
         const uint64_t cnt = i1 - i0;
-        const void *h_src = src;
-        if (bytes && !is_registered(e, src, bytes)) {  // pageable: CPU copy into pinned
-            stage_copy(s.h_stage, src, bytes);
+        const bool rows = sp.width != 0 && sp.width < sp.pitch;
+        const void *h_src = sp.src;
+        if (sp.bytes && !is_registered(e, sp.src, sp.bytes)) {  // pageable: CPU copy into pinned
+            if (rows)
+                stage_copy_rows(s.h_stage, sp.src, sp.pitch, sp.width, sp.bytes / sp.pitch);
+            else
+                stage_copy(s.h_stage, sp.src, sp.bytes);
             h_src = s.h_stage;
         }
-        if (bytes)
-            status = check_hip(hipMemcpyAsync(s.d_bytes, h_src, bytes, hipMemcpyHostToDevice,
+        if (sp.bytes && rows)
+            status = check_hip(hipMemcpy2DAsync(s.d_bytes, sp.pitch, h_src, sp.pitch, sp.width,
+                                                sp.bytes / sp.pitch, hipMemcpyHostToDevice,
+                                                s.stream));
+        else if (sp.bytes)
+            status = check_hip(hipMemcpyAsync(s.d_bytes, h_src, sp.bytes, hipMemcpyHostToDevice,
                                               s.stream));
         s.seq = ++e->pieces;
 #ifdef AIPSTACK_ENGINE_FAULT_INJECTION
@@ -333,6 +373,8 @@ extern "C" int aipstack_chksum_engine_create(int device, uint64_t chunk_bytes, i
     e->chunk_bytes = chunk_bytes;
     // results/offsets staging sized for the smallest packets (64 B, the Ethernet minimum)
     e->chunk_packets = chunk_bytes / 64 + 1;
+    // experiments: AIPSTACK_ENGINE_SLOT_ROWS=0 copies whole slots (one 1-D span per piece)
+    if (const char *v = std::getenv("AIPSTACK_ENGINE_SLOT_ROWS")) e->slot_rows = std::atoi(v) != 0;
     e->slots.resize((size_t)nstreams);
     int st = AIPSTACK_CHKSUM_OK;
     for (Slot &s : e->slots) {
@@ -426,10 +468,10 @@ extern "C" int aipstack_chksum_engine_submit_strided(aipstack_chksum_engine *e,
     per = std::min<uint64_t>(std::max<uint64_t>(per, 1), e->chunk_packets);
     if ((per - 1) * stride + len > e->chunk_bytes) return AIPSTACK_CHKSUM_EINVAL;
     const char *base = static_cast<const char *>(h_base);
-    auto chunker = [&](uint64_t i0, uint64_t *i1, const char **src, uint64_t *bytes) {
+    auto chunker = [&](uint64_t i0, uint64_t *i1, Span *sp) {
         *i1 = std::min(n, i0 + per);
-        *src = base + i0 * stride;
-        *bytes = (*i1 - i0 - 1) * stride + len;
+        sp->src = base + i0 * stride;
+        sp->bytes = (*i1 - i0 - 1) * stride + len;
     };
     auto launch = [&](Slot &s, uint64_t i0, uint64_t i1) {
         return aipstack_chksum_batch_strided(s.d_bytes, stride, len, i1 - i0, s.d_out, flags,
@@ -449,7 +491,7 @@ int submit_csr_like(aipstack_chksum_engine *e, const void *h_base, const uint64_
         if (h_offsets[i + 1] < h_offsets[i] || h_offsets[i + 1] - h_offsets[i] > AIPSTACK_CHKSUM_MAX_LEN)
             return AIPSTACK_CHKSUM_EINVAL;
     const char *base = static_cast<const char *>(h_base);
-    auto chunker = [&](uint64_t i0, uint64_t *i1, const char **src, uint64_t *bytes) {
+    auto chunker = [&](uint64_t i0, uint64_t *i1, Span *sp) {
         // whole packets while they fit the chunk (binary search on the offsets)
         const uint64_t limit = h_offsets[i0] + e->chunk_bytes;
         const uint64_t *hi = std::upper_bound(h_offsets + i0 + 1,
@@ -458,8 +500,8 @@ int submit_csr_like(aipstack_chksum_engine *e, const void *h_base, const uint64_
         uint64_t j = (uint64_t)(hi - h_offsets) - 1;  // last offset <= limit
         if (j <= i0) j = i0 + 1;
         *i1 = j;
-        *src = base + h_offsets[i0];
-        *bytes = h_offsets[j] - h_offsets[i0];
+        sp->src = base + h_offsets[i0];
+        sp->bytes = h_offsets[j] - h_offsets[i0];
     };
     auto launch = [&](Slot &s, uint64_t i0, uint64_t i1) {
         const uint64_t cnt = i1 - i0;
@@ -549,9 +591,11 @@ extern "C" int aipstack_chksum_engine_submit_csr(aipstack_chksum_engine *e, cons
 }
 
 namespace {
-// Ring-slot batches: whole slots per chunk (the piece's slots are DMA'd as one span; the
-// slack after each frame travels too), lengths staged beside them. Every length is checked
-// first: <= min(slot_stride, 65535), else _EINVAL before any work.
+// Ring-slot batches: whole slots per chunk, lengths staged beside them. Of each slot only
+// the piece's longest frame's length (rounded up to 64 bytes) crosses PCIe, as one 2-D copy
+// that keeps the slot layout on the device: a 2048-byte ring of Ethernet frames (<= 1514 B)
+// moves <= 1536 bytes per slot instead of 2048. Every length is checked first:
+// <= min(slot_stride, 65535), else _EINVAL before any work.
 template <class Kernel>
 int submit_slotted_like(aipstack_chksum_engine *e, const void *h_base, uint64_t slot_stride,
                         const uint32_t *h_len, uint64_t n, void *h_out, uint32_t elem,
@@ -562,10 +606,16 @@ int submit_slotted_like(aipstack_chksum_engine *e, const void *h_base, uint64_t 
         if (h_len[i] > cap) return AIPSTACK_CHKSUM_EINVAL;
     const uint64_t per = std::min<uint64_t>(e->chunk_bytes / slot_stride, e->chunk_packets);
     const char *base = static_cast<const char *>(h_base);
-    auto chunker = [&](uint64_t i0, uint64_t *i1, const char **src, uint64_t *bytes) {
+    auto chunker = [&](uint64_t i0, uint64_t *i1, Span *sp) {
         *i1 = std::min(n, i0 + per);
-        *src = base + i0 * slot_stride;
-        *bytes = (*i1 - i0) * slot_stride;
+        sp->src = base + i0 * slot_stride;
+        sp->bytes = (*i1 - i0) * slot_stride;
+        uint32_t longest = 0;
+        for (uint64_t i = i0; i < *i1; ++i) longest = std::max(longest, h_len[i]);
+        if (!e->slot_rows) return;
+        sp->pitch = slot_stride;
+        sp->width = std::min<uint64_t>(((uint64_t)longest + 63u) & ~63ull, slot_stride);
+        if (sp->width == 0) sp->bytes = 0;  // every frame empty: nothing to copy
     };
     auto launch = [&](Slot &s, uint64_t i0, uint64_t i1) {
         const uint64_t cnt = i1 - i0;

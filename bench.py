@@ -518,8 +518,10 @@ def main():
             raise SystemExit("--small covers configs A, RX and TX on one GPU")
         return small_batches(args, layout, plen, dev)
     if args.e2e:
-        if layout not in ("strided", "csr", "rx", "tx"):
-            raise SystemExit("--e2e covers the packet configs A, B, C, RX and TX")
+        if layout not in ("strided", "csr", "rx", "tx", "rxslot", "csrslot"):
+            raise SystemExit("--e2e covers the configs A, B, C, RX, TX, RX2K and C2K")
+        if args.engines > 0 and layout in ("rxslot", "csrslot"):
+            raise SystemExit("--engines covers the back-to-back configs")
         return e2e(args, rank, world, local_rank, layout, n, plen)
 
     # ---- this rank's shard, generated in place (global packets [rank*n, (rank+1)*n))
@@ -894,9 +896,13 @@ def e2e(args, rank, world, local_rank, layout, n, plen):
     off, total = spec["offsets"], spec.get("payload", spec["total"])
     stride = spec.get("stride", plen)
     host = host_shard(spec)
-    frames = layout in ("rx", "tx")
+    frames = layout in ("rx", "tx", "rxslot")
     if frames:  # frames: synthesised (and, for RX, made valid) on the host by host_shard
         off, total = spec["offsets"], spec["total"]
+    slot = SLOT_STRIDE.get(args.config)
+    if layout in ("rxslot", "csrslot"):  # a receive ring: one frame / packet per slot
+        host, lens = synth.to_slots(host, off, slot)
+        total = int(lens.sum(dtype=np.uint64))
     # Tx fill writes the frames in place: the fill ignores the fields' old contents, so
     # every step gives the same bytes; parity compares with the oracle's fill of a copy
     orig = host.copy() if layout == "tx" and not args.no_parity else None
@@ -921,6 +927,10 @@ def e2e(args, rank, world, local_rank, layout, n, plen):
             eng.rx_verify(host, off, out=out)
         elif layout == "tx":
             eng.tx_fill(host, off, status=out)
+        elif layout == "rxslot":
+            eng.rx_verify_slotted(host, slot, lens, out=out)
+        elif layout == "csrslot":
+            eng.slotted(host, slot, lens, out=out)
         else:
             eng.csr(host, off, out=out)
 
@@ -965,6 +975,13 @@ def e2e(args, rank, world, local_rank, layout, n, plen):
                                                                            ctypes.c_void_p]
             o = off.astype(np.uint64)
             lib.oracle_rx_verify_batch(host.ctypes.data, o.ctypes.data, n, want.ctypes.data)
+        elif layout in ("rxslot", "csrslot"):
+            fn = lib.oracle_rx_verify_slotted if layout == "rxslot" else lib.oracle_batch_slotted
+            fn.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                           ctypes.c_void_p] + ([] if layout == "rxslot" else [ctypes.c_uint32])
+            ln = np.ascontiguousarray(lens, dtype=np.uint32)
+            fn(host.ctypes.data, slot, ln.ctypes.data, n, want.ctypes.data,
+               *([] if layout == "rxslot" else [0]))
         elif layout == "strided":
             lib.oracle_batch_strided.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
                                                  ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32]
@@ -991,7 +1008,7 @@ def e2e(args, rank, world, local_rank, layout, n, plen):
     value = total * world * args.steps / max_elapsed / 2**30
     if rank == 0:
         print(json.dumps({
-            "metric": "GiB/s " + {"rx": "Rx-verified", "tx": "Tx-filled"}.get(layout, "checksummed")
+            "metric": "GiB/s " + {"rx": "Rx-verified", "rxslot": "Rx-verified", "tx": "Tx-filled"}.get(layout, "checksummed")
                       + " end-to-end (host memory in, host results out)",
             "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(max_elapsed / args.steps * 1e3, 3),
@@ -1001,6 +1018,9 @@ def e2e(args, rank, world, local_rank, layout, n, plen):
                        "host_memory": "pageable (CPU copy into pinned staging)"
                        if args.e2e_pageable else "registered (hipHostRegister, DMA direct)",
                        "streams": args.e2e_streams, "chunk_MiB": args.e2e_chunk_mib,
+                       **({"slot_stride": slot, "ring_bytes": int(host.nbytes),
+                           "value_counts": "frame/packet bytes (the lengths), not slot bytes"}
+                          if layout in ("rxslot", "csrslot") else {}),
                        **({"engines": args.engines, "engine_devices": engine_devices,
                            "engine_group": "one process, disjoint ranges of equal bytes, one "
                                            "host thread per engine"}

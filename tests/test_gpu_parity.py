@@ -1136,6 +1136,111 @@ def test_engine_slotted(oracle, register):
         assert np.array_equal(out, oracle.batch_slotted(ring, 2048, lens))
 
 
+@pytest.mark.parametrize("register", [False, True])
+def test_engine_slotted_moves_only_used_slot_prefix(oracle, register):
+    """Ring-slot pieces cross PCIe as 2-D copies of each slot's first bytes (the piece's longest
+    frame, rounded up to 64): a batch of long frames leaves its bytes in the device staging,
+    then batches of short frames (<= 60 / <= 100 B: 64- and 128-byte rows, below the
+    112-byte header window) run on the same slots -- the bytes past each row are stale, and
+    the results must still be the oracle's."""
+    stride = 2048
+    with A.ChksumEngine(0, chunk_bytes=1 << 20, nstreams=2) as eng:
+        # (max payload, seed, length cap): capped lengths cut frames short in their slots
+        for maxp, seed, cap in ((1460, 3, None), (6, 4, 60), (46, 5, 100), (1460, 6, None),
+                                (0, 7, 64), (20, 8, None)):
+            fr, foff = synth.frames_host(3000, seed=seed, max_payload=maxp)
+            ring, lens = synth.to_slots(fr, foff, stride, slack_seed=seed)
+            if cap is not None:
+                lens = np.minimum(lens, cap).astype(np.uint32)
+            if register:
+                eng.register(ring)
+            want = ring.copy()
+            want_st = oracle.tx_fill_slotted(want, stride, lens)
+            assert np.array_equal(eng.tx_fill_slotted(ring, stride, lens), want_st)
+            assert np.array_equal(ring, want)
+            assert np.array_equal(eng.rx_verify_slotted(ring, stride, lens),
+                                  oracle.rx_verify_slotted(ring, stride, lens))
+            assert np.array_equal(eng.slotted(ring, stride, lens),
+                                  oracle.batch_slotted(ring, stride, lens))
+            zero = np.zeros_like(lens)  # every frame empty: nothing crosses PCIe
+            assert np.array_equal(eng.slotted(ring, stride, zero),
+                                  oracle.batch_slotted(ring, stride, zero))
+            if register:
+                eng.unregister(ring)
+
+
+@pytest.mark.parametrize("register", [False, True])
+def test_engine_ring_receive_loop(oracle, register):
+    """A TAP-style receive/send ring driven through the engine's tickets
+    (tap/linux/TapDeviceLinux.cpp:156-178: one frame per slot, its length beside it): 8
+    regions of 2,048 slots x 2,048 B, several batches in flight; a region is refilled only
+    after its previous ticket completed (wait, or poll when it is done), so every wrap reuses
+    slots the GPU has finished with. Rx batches (a tenth of the frames corrupted) are checked
+    against the oracle's verdicts, Tx batches (filled in place) against the oracle's fill."""
+    stride, per, regions = 2048, 2048, 8
+    ring = np.zeros(regions * per * stride, dtype=np.uint8)
+    raw, soff = synth.frames_host(per * 5, seed=91, max_payload=1460)  # fields zero
+    filled = raw.copy()
+    oracle.tx_fill_batch(filled, soff)  # what a sender put on the wire
+    rng = np.random.default_rng(17)
+    with A.ChksumEngine(0, chunk_bytes=2 << 20, nstreams=3) as eng:
+        if register:
+            eng.register(ring)
+        pending = [None] * regions  # region -> (ticket, kind, out, want)
+        done = 0
+
+        def finish(r, block):
+            nonlocal done
+            t, kind, out, want = pending[r]
+            if block:
+                eng.wait(t)
+            elif not eng.poll(t):
+                return False
+            region = ring[r * per * stride:(r + 1) * per * stride]
+            if kind == "rx":
+                assert np.array_equal(out, want), f"region {r}: Rx verdicts differ"
+            else:
+                want_st, want_bytes = want
+                assert np.array_equal(out, want_st), f"region {r}: Tx statuses differ"
+                assert np.array_equal(region, want_bytes), f"region {r}: Tx fields differ"
+            pending[r] = None
+            done += 1
+            return True
+
+        for b in range(5 * regions):
+            r = b % regions
+            if pending[r] is not None:
+                finish(r, block=True)
+            for q in range(regions):  # complete whatever finished meanwhile, out of order
+                if pending[q] is not None:
+                    finish(q, block=False)
+            # the "read()"s of this region: frames of the source batch, at random rotations
+            k = int(rng.integers(0, per * 4))
+            fb, fo = (raw if b % 3 == 2 else filled), soff[k:k + per + 1]
+            region = ring[r * per * stride:(r + 1) * per * stride]
+            slots, lens = synth.to_slots(fb[int(fo[0]):int(fo[-1])], fo - fo[0], stride,
+                                         slack_seed=b)
+            region[:] = slots
+            if b % 3 == 2:
+                want_bytes = region.copy()
+                want_st = oracle.tx_fill_slotted(want_bytes, stride, lens)
+                t, out = eng.submit_tx_fill_slotted(region, stride, lens)
+                pending[r] = (t, "tx", out, (want_st, want_bytes))
+            else:
+                for i in np.nonzero(rng.random(per) < 0.1)[0]:
+                    j = int(i) * stride + int(rng.integers(12, int(lens[i])))
+                    region[j] ^= np.uint8(1 << int(rng.integers(0, 8)))
+                want = oracle.rx_verify_slotted(region, stride, lens)
+                t, out = eng.submit_rx_verify_slotted(region, stride, lens)
+                pending[r] = (t, "rx", out, want)
+        for r in range(regions):
+            if pending[r] is not None:
+                finish(r, block=True)
+        assert done == 5 * regions
+        if register:
+            eng.unregister(ring)
+
+
 # ---- several engines in one process (engine group) ----------------------------------------
 
 @pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0, 0]])
@@ -1187,6 +1292,22 @@ def test_bench_e2e_engine_group_line():
     d = json.loads([l for l in r.stdout.splitlines() if l.strip()][-1])
     assert d["parity"].startswith("bit-exact") and d["value"] > 0
     assert d["config"]["engines"] == 3 and d["config"]["engine_devices"] == [0, 0, 0]
+
+
+@pytest.mark.parametrize("config,pageable", [("RX2K", False), ("C2K", True)])
+def test_bench_e2e_ring_slots_line(config, pageable):
+    """bench.py --e2e on a receive ring (RX2K / C2K, 2048-B slots): one JSON line, bit-exact
+    against the oracle over every slot; the value counts frame bytes, not slot bytes."""
+    import json
+    cmd = [sys.executable, "bench.py", "--e2e", "--config", config, "--steps", "2", "--warmup", "1"]
+    if pageable:
+        cmd.append("--e2e-pageable")
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.strip()][-1])
+    assert d["parity"].startswith("bit-exact") and d["value"] > 0
+    assert d["config"]["slot_stride"] == 2048
+    assert d["metric"].startswith("GiB/s Rx-verified" if config == "RX2K" else "GiB/s checksummed")
 
 
 # ---- frame decisions pinned by the reference's own call sites (tests/golden/frame_ref.py) ---

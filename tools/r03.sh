@@ -6,6 +6,8 @@
 #           (AIPSTACK_CHKSUM_TX_GATHER=0), interleaved; the split fill both ways; rocprof
 #           stats and FETCH/WRITE passes of TXREC; then pytest -m gpu
 #   check   pytest -m gpu, then bench A, C, CHAIN, TXREC, RX (no CPU baseline)
+#   txnt    split Tx fill: scatter stores plain vs nontemporal (+ rocprof of each)
+#   ring    e2e receive rings (RX2K / C2K): 2-D copies of the slots' used prefix vs whole slots
 #   slots   pytest -m gpu; ring-slot lines RX2K / C2K (+ their slot-read ceilings) and A2K;
 #           a U/P sweep of the slotted checksum; e2e through an engine group of 1/2/4
 set -e
@@ -114,6 +116,35 @@ fsweep)
 frames=4,unroll=1,chunk_packets=64,waves_per_cu=100000;frames=8,unroll=1,chunk_packets=64,waves_per_cu=100000;\
 frames=4,unroll=1,chunk_packets=16,waves_per_cu=100000" > "$out/rx2k.jsonl" 2> "$out/rx2k.err"
   bench bench_RX2K --config RX2K --per-launch
+  ;;
+txnt)
+  # split Tx fill: the scatter pass's 2-byte field stores plain (product) vs nontemporal
+  # (tools/build/lib_scatter_nt.so, -DAIPSTACK_TX_STORE_MODE=1), alternating processes;
+  # then rocprof per pass for both
+  for i in 1 2 3; do
+    bench tx_split --config TX --steps 100 --per-launch --no-cpu-baseline
+    AIPSTACK_AMD_LIB=tools/build/lib_scatter_nt.so bench tx_split_nt --config TX --steps 100 \
+        --per-launch --no-cpu-baseline
+  done
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/prof_TX" -o run \
+      -- python3 bench.py --config TX --no-cpu-baseline --no-parity > "$out/prof_TX.log" 2>&1
+  AIPSTACK_AMD_LIB=tools/build/lib_scatter_nt.so timeout -k 10 300 rocprofv3 --kernel-trace \
+      --stats --output-format csv -d "$out/prof_TX_nt" -o run \
+      -- python3 bench.py --config TX --no-cpu-baseline --no-parity > "$out/prof_TX_nt.log" 2>&1
+  ;;
+ring)
+  # receive rings through the host engine (RX2K / C2K, 2048-B slots): each slot's used prefix
+  # as a 2-D copy (product) vs whole slots (AIPSTACK_ENGINE_SLOT_ROWS=0), registered and
+  # pageable; the CSR RX line beside them (same frames back to back)
+  for i in 1 2; do
+    for c in RX2K C2K; do
+      bench e2e_ring --e2e --config $c --steps 5 --warmup 1
+      AIPSTACK_ENGINE_SLOT_ROWS=0 bench e2e_ring_full --e2e --config $c --steps 5 --warmup 1
+    done
+  done
+  bench e2e_ring --e2e --e2e-pageable --config RX2K --steps 3 --warmup 1
+  AIPSTACK_ENGINE_SLOT_ROWS=0 bench e2e_ring_full --e2e --e2e-pageable --config RX2K --steps 3 --warmup 1
+  bench e2e_rx --e2e --config RX --steps 5 --warmup 1
   ;;
 *)
   echo "unknown mode $mode" >&2; exit 2 ;;
