@@ -231,31 +231,11 @@ int drain(aipstack_chksum_engine *e, Slot &s, bool blocking = true) {
     return st;
 }
 
-// Pageable ring slots into pinned staging: only the first `width` bytes of each `pitch`-byte
-// row (the rest of a slot is never read), by the same threads as stage_copy.
-void stage_copy_rows(void *dst, const void *src, uint64_t pitch, uint64_t width, uint64_t rows) {
-    auto run = [=](uint64_t lo, uint64_t hi) {
-        for (uint64_t r = lo; r < hi; ++r)
-            std::memcpy(static_cast<char *>(dst) + r * pitch,
-                        static_cast<const char *>(src) + r * pitch, width);
-    };
-    const unsigned hw = std::thread::hardware_concurrency();
-    const unsigned nt = (unsigned)std::min<uint64_t>(
-        std::min<uint64_t>(rows * width / (4ull << 20), 8), hw ? hw : 1);
-    if (nt <= 1) {
-        run(0, rows);
-        return;
-    }
-    const uint64_t per = (rows + nt - 1) / nt;
-    std::vector<std::thread> pool;
-    for (unsigned t = 0; t < nt && (uint64_t)t * per < rows; ++t)
-        pool.emplace_back(run, (uint64_t)t * per, std::min(rows, (uint64_t)(t + 1) * per));
-    for (std::thread &t : pool) t.join();
-}
-
-// A piece's host bytes: `bytes` from `src`, or -- when width is set -- rows of `pitch` bytes
-// of which only the first `width` travel (ring slots: the slack after the longest frame of
-// the piece stays behind; the device copy keeps the slot layout).
+// A piece's host bytes: `bytes` from `src`, or -- when width is set and the bytes are
+// registered -- rows of `pitch` bytes of which only the first `width` travel (ring slots:
+// the slack after the longest frame of the piece stays behind; the device copy keeps the
+// slot layout). Pageable rows are staged and sent whole: a per-row CPU copy runs slower
+// than the bulk one, and the bulk copy already keeps up with the link.
 struct Span {
     const char *src = nullptr;
     uint64_t bytes = 0;
@@ -292,13 +272,11 @@ int enqueue(aipstack_chksum_engine *e, uint64_t n, void *h_out, uint32_t elem, C
         Span sp;
         chunker(i0, &i1, &sp);
         const uint64_t cnt = i1 - i0;
-        const bool rows = sp.width != 0 && sp.width < sp.pitch;
+        const bool registered = sp.bytes && is_registered(e, sp.src, sp.bytes);
+        const bool rows = registered && sp.width != 0 && sp.width < sp.pitch;
         const void *h_src = sp.src;
-        if (sp.bytes && !is_registered(e, sp.src, sp.bytes)) {  // pageable: CPU copy into pinned
-            if (rows)
-                stage_copy_rows(s.h_stage, sp.src, sp.pitch, sp.width, sp.bytes / sp.pitch);
-            else
-                stage_copy(s.h_stage, sp.src, sp.bytes);
+        if (sp.bytes && !registered) {  // pageable: CPU copy into pinned staging
+            stage_copy(s.h_stage, sp.src, sp.bytes);
             h_src = s.h_stage;
         }
         if (sp.bytes && rows)
@@ -591,10 +569,10 @@ extern "C" int aipstack_chksum_engine_submit_csr(aipstack_chksum_engine *e, cons
 }
 
 namespace {
-// Ring-slot batches: whole slots per chunk, lengths staged beside them. Of each slot only
-// the piece's longest frame's length (rounded up to 64 bytes) crosses PCIe, as one 2-D copy
-// that keeps the slot layout on the device: a 2048-byte ring of Ethernet frames (<= 1514 B)
-// moves <= 1536 bytes per slot instead of 2048. Every length is checked first:
+// Ring-slot batches: whole slots per chunk, lengths staged beside them. From registered
+// memory only the piece's longest frame's length (rounded up to 64 bytes) of each slot
+// crosses PCIe, as one 2-D copy that keeps the slot layout on the device: a 2048-byte ring
+// of Ethernet frames (<= 1514 B) moves <= 1536 bytes per slot instead of 2048. Every length is checked first:
 // <= min(slot_stride, 65535), else _EINVAL before any work.
 template <class Kernel>
 int submit_slotted_like(aipstack_chksum_engine *e, const void *h_base, uint64_t slot_stride,
@@ -610,12 +588,12 @@ int submit_slotted_like(aipstack_chksum_engine *e, const void *h_base, uint64_t 
         *i1 = std::min(n, i0 + per);
         sp->src = base + i0 * slot_stride;
         sp->bytes = (*i1 - i0) * slot_stride;
+        if (!e->slot_rows) return;
         uint32_t longest = 0;
         for (uint64_t i = i0; i < *i1; ++i) longest = std::max(longest, h_len[i]);
-        if (!e->slot_rows) return;
         sp->pitch = slot_stride;
         sp->width = std::min<uint64_t>(((uint64_t)longest + 63u) & ~63ull, slot_stride);
-        if (sp->width == 0) sp->bytes = 0;  // every frame empty: nothing to copy
+        if (longest == 0) sp->bytes = 0;  // every frame empty: nothing to copy
     };
     auto launch = [&](Slot &s, uint64_t i0, uint64_t i1) {
         const uint64_t cnt = i1 - i0;

@@ -252,6 +252,33 @@ struct BatchChksum {
         return aipstack_chksum_tx_fill_split(d_frames, d_offsets, n, d_status, d_workspace,
                                              workspace_bytes, stream);
     }
+    // The read pass alone: one 8-byte record per frame (layout in chksum.h), frames untouched.
+    static int txFillRecords(void const *d_frames, std::uint64_t const *d_offsets,
+                             std::uint64_t n, std::uint64_t *d_records, void *stream = nullptr) {
+        return aipstack_chksum_tx_fill_records(d_frames, d_offsets, n, d_records, stream);
+    }
+    // A receive / send ring: frame or packet i = the d_len[i] bytes at d_base + i * slotStride.
+    static int slotted(void const *d_base, std::uint64_t slot_stride, std::uint32_t const *d_len,
+                       std::uint64_t n, std::uint16_t *d_out, bool final_chksum = false,
+                       void *stream = nullptr) {
+        return aipstack_chksum_batch_slotted(d_base, slot_stride, d_len, n, d_out,
+                                             final_chksum ? AIPSTACK_CHKSUM_FINAL : 0u, stream);
+    }
+    static int rxVerifySlotted(void const *d_base, std::uint64_t slot_stride,
+                               std::uint32_t const *d_len, std::uint64_t n,
+                               std::uint8_t *d_verdict, void *stream = nullptr) {
+        return aipstack_chksum_rx_verify_slotted(d_base, slot_stride, d_len, n, d_verdict, stream);
+    }
+    static int txFillSlotted(void *d_base, std::uint64_t slot_stride, std::uint32_t const *d_len,
+                             std::uint64_t n, std::uint8_t *d_status, void *stream = nullptr) {
+        return aipstack_chksum_tx_fill_slotted(d_base, slot_stride, d_len, n, d_status, stream);
+    }
+    static int txFillRecordsSlotted(void const *d_base, std::uint64_t slot_stride,
+                                    std::uint32_t const *d_len, std::uint64_t n,
+                                    std::uint64_t *d_records, void *stream = nullptr) {
+        return aipstack_chksum_tx_fill_records_slotted(d_base, slot_stride, d_len, n, d_records,
+                                                       stream);
+    }
 };
 
 // Host-memory batches (the TAP read()/write() path, tap/linux/TapDeviceLinux.cpp:122-127,
@@ -332,6 +359,40 @@ public:
                      std::uint8_t *h_status, std::uint64_t *ticket) {
         return aipstack_chksum_engine_submit_tx_fill(m_engine, h_frames, h_offsets, n,
                                                      h_status, ticket);
+    }
+    // Ring slots (the TAP ring: one frame per slot, its length beside it).
+    int slotted(void const *h_base, std::uint64_t slot_stride, std::uint32_t const *h_len,
+                std::uint64_t n, std::uint16_t *h_out, bool final_chksum = false) {
+        return aipstack_chksum_engine_host_slotted(m_engine, h_base, slot_stride, h_len, n, h_out,
+                                                   final_chksum ? AIPSTACK_CHKSUM_FINAL : 0u);
+    }
+    int rxVerifySlotted(void const *h_base, std::uint64_t slot_stride, std::uint32_t const *h_len,
+                        std::uint64_t n, std::uint8_t *h_verdict) {
+        return aipstack_chksum_engine_host_rx_verify_slotted(m_engine, h_base, slot_stride, h_len,
+                                                             n, h_verdict);
+    }
+    int txFillSlotted(void *h_base, std::uint64_t slot_stride, std::uint32_t const *h_len,
+                      std::uint64_t n, std::uint8_t *h_status) {
+        return aipstack_chksum_engine_host_tx_fill_slotted(m_engine, h_base, slot_stride, h_len, n,
+                                                           h_status);
+    }
+    int submitSlotted(void const *h_base, std::uint64_t slot_stride, std::uint32_t const *h_len,
+                      std::uint64_t n, std::uint16_t *h_out, bool final_chksum,
+                      std::uint64_t *ticket) {
+        return aipstack_chksum_engine_submit_slotted(m_engine, h_base, slot_stride, h_len, n, h_out,
+                                                     final_chksum ? AIPSTACK_CHKSUM_FINAL : 0u,
+                                                     ticket);
+    }
+    int submitRxVerifySlotted(void const *h_base, std::uint64_t slot_stride,
+                              std::uint32_t const *h_len, std::uint64_t n,
+                              std::uint8_t *h_verdict, std::uint64_t *ticket) {
+        return aipstack_chksum_engine_submit_rx_verify_slotted(m_engine, h_base, slot_stride,
+                                                               h_len, n, h_verdict, ticket);
+    }
+    int submitTxFillSlotted(void *h_base, std::uint64_t slot_stride, std::uint32_t const *h_len,
+                            std::uint64_t n, std::uint8_t *h_status, std::uint64_t *ticket) {
+        return aipstack_chksum_engine_submit_tx_fill_slotted(m_engine, h_base, slot_stride, h_len,
+                                                             n, h_status, ticket);
     }
     // 0 = complete, 1 = still running, < 0 = error of that batch
     int poll(std::uint64_t ticket) { return aipstack_chksum_engine_poll(m_engine, ticket); }

@@ -185,6 +185,27 @@ int main() {
             oracle_rx_verify_batch(want_fr.data(), foff3.data(), nf, want_v.data());
             EXPECT(eng.wait(t2) == 0 && hv == want_v, "engine rx verify differs from the oracle");
             EXPECT(eng.unregisterMemory(hf2.data()) == 0, "unregister failed");
+            // the same frames in a ring of 2048-B slots (slack bytes 0x5A): Tx fill in place,
+            // then Rx verify through submit / wait, both against the oracle's slot forms
+            const uint64_t ss = 2048;
+            std::vector<unsigned char> ring(nf * ss, 0x5A);
+            std::vector<uint32_t> lens(nf);
+            for (uint64_t i = 0; i < nf; i++) {
+                lens[i] = (uint32_t)(foff3[i + 1] - foff3[i]);
+                std::memcpy(ring.data() + i * ss, fh.data() + foff3[i], lens[i]);
+            }
+            std::vector<unsigned char> want_ring(ring);
+            std::vector<uint8_t> want_sst(nf), sst(nf, 0xEE), sv(nf), want_sv(nf);
+            oracle_tx_fill_slotted(want_ring.data(), ss, lens.data(), nf, want_sst.data());
+            EXPECT(eng.txFillSlotted(ring.data(), ss, lens.data(), nf, sst.data()) == 0,
+                   "engine slotted tx fill failed");
+            EXPECT(ring == want_ring && sst == want_sst,
+                   "engine slotted tx fill: slots or statuses differ from the oracle");
+            uint64_t t3 = 0;
+            EXPECT(eng.submitRxVerifySlotted(ring.data(), ss, lens.data(), nf, sv.data(), &t3) == 0,
+                   "engine submit slotted rx verify failed");
+            oracle_rx_verify_slotted(ring.data(), ss, lens.data(), nf, want_sv.data());
+            EXPECT(eng.wait(t3) == 0 && sv == want_sv, "engine slotted rx verify differs");
             AIpStackAmd::HostChksumEngine moved(std::move(eng));
             EXPECT(moved.valid() && !eng.valid(), "engine move");
         }
