@@ -82,6 +82,12 @@ SIGNATURES = {
     "aipstack_chksum_engine_group_host_csr": (_c_int, [_c_vp, _c_vp, _c_vp, _c_u64, _c_vp, _c_u32, _c_vp]),
     "aipstack_chksum_engine_group_host_rx_verify": (_c_int, [_c_vp, _c_vp, _c_vp, _c_u64, _c_vp, _c_vp]),
     "aipstack_chksum_engine_group_host_tx_fill": (_c_int, [_c_vp, _c_vp, _c_vp, _c_u64, _c_vp, _c_vp]),
+    "aipstack_chksum_engine_group_host_slotted": (_c_int, [_c_vp, _c_vp, _c_u64, _c_vp, _c_u64, _c_vp,
+                                                           _c_u32, _c_vp]),
+    "aipstack_chksum_engine_group_host_rx_verify_slotted": (_c_int, [_c_vp, _c_vp, _c_u64, _c_vp,
+                                                                     _c_u64, _c_vp, _c_vp]),
+    "aipstack_chksum_engine_group_host_tx_fill_slotted": (_c_int, [_c_vp, _c_vp, _c_u64, _c_vp,
+                                                                   _c_u64, _c_vp, _c_vp]),
     # synth.h
     "aipstack_synth_fill_host": (None, [_c_vp, _c_u64, _c_u64, _c_u64]),
     "aipstack_synth_mixed_offsets_host": (_c_u64, [_c_vp, _c_u64, _c_u64]),

@@ -150,31 +150,31 @@ class IpBufRef:
 
 def ipBufProcessBytes(buf: IpBufRef, processLen: int,
                       processChunk: Callable[[memoryview, int], int]) -> IpBufRef:
-    """Call ``processChunk(chunk, chunk_len)`` for each non-empty chunk of the first
-    `processLen` bytes of `buf`; returns the remaining reference. Moves to the next node
-    eagerly, as the reference does (BufUtils.h:129-178)."""
+    """BufUtils.h:129-178 (same contract): hands ``processChunk(piece, piece_len)`` the
+    non-empty pieces of the first `processLen` bytes of `buf`, node by node; it returns how
+    many bytes of its piece it took, and taking fewer ends the walk inside that node. The
+    returned reference starts after the bytes taken and keeps everything not taken. A used-up
+    node is left behind whenever it has a successor, even when nothing more is wanted (the
+    reference's eager advance, which also steps over empty nodes)."""
     assert buf.node is not None and processLen <= buf.tot_len
-    remain = buf.tot_len - processLen
-    node, offset, tot = buf.node, buf.offset, processLen
+    untouched = buf.tot_len - processLen
+    at, pos, want = buf.node, buf.offset, processLen
     while True:
-        assert offset <= node.len
-        node_rem = node.len - offset
-        consumed = tot >= node_rem
-        chunk_len = node_rem if consumed else tot
-        if chunk_len > 0:
-            proc = processChunk(node.ptr[offset:offset + chunk_len], chunk_len)
-            assert proc <= chunk_len
-            tot -= proc
-            offset += proc
-            if proc < chunk_len:
-                remain += tot
-                tot = 0
+        assert pos <= at.len
+        avail = at.len - pos
+        uses_up_node = want >= avail
+        piece = avail if uses_up_node else want
+        if piece:
+            took = processChunk(at.ptr[pos:pos + piece], piece)
+            assert 0 <= took <= piece
+            pos += took
+            want -= took
+            if took != piece:  # the visitor stopped early
                 break
-        if not consumed or node.next is None:
+        if not uses_up_node or at.next is None:
             break
-        node, offset = node.next, 0
-    assert tot == 0
-    return IpBufRef(node, offset, remain)
+        at, pos = at.next, 0
+    return IpBufRef(at, pos, want + untouched)
 
 
 # --------------------------------------------------------------------------------------
@@ -791,6 +791,33 @@ class ChksumEngineGroup:
         o, n, status = ChksumEngine._tx_args(frames, offsets, status)
         self._call("aipstack_chksum_engine_group_host_tx_fill", "engine group tx_fill",
                    frames.ctypes.data, o.ctypes.data, max(n, 0), status.ctypes.data)
+        return status
+
+    # ring slots: frame i = the lens[i] bytes at buf[i * slot_stride:]
+    def slotted(self, buf, slot_stride: int, lens, *, out=None, final=False):
+        ln, n = ChksumEngine._slot_args(buf, slot_stride, lens)
+        out = ChksumEngine._host_args(buf, out, n)
+        self._call("aipstack_chksum_engine_group_host_slotted", "engine group slotted",
+                   buf.ctypes.data, slot_stride, ln.ctypes.data, n, out.ctypes.data,
+                   AIPSTACK_CHKSUM_FINAL if final else 0)
+        return out
+
+    def rx_verify_slotted(self, frames, slot_stride: int, lens, *, out=None):
+        ln, n = ChksumEngine._slot_args(frames, slot_stride, lens)
+        out = ChksumEngine._host_args(frames, out, n, np.uint8)
+        self._call("aipstack_chksum_engine_group_host_rx_verify_slotted",
+                   "engine group rx_verify_slotted", frames.ctypes.data, slot_stride,
+                   ln.ctypes.data, n, out.ctypes.data)
+        return out
+
+    def tx_fill_slotted(self, frames, slot_stride: int, lens, *, status=None):
+        if not frames.flags.writeable:
+            raise ValueError("frames must be writable (filled in place)")
+        ln, n = ChksumEngine._slot_args(frames, slot_stride, lens)
+        status = ChksumEngine._host_args(frames, status, n, np.uint8)
+        self._call("aipstack_chksum_engine_group_host_tx_fill_slotted",
+                   "engine group tx_fill_slotted", frames.ctypes.data, slot_stride,
+                   ln.ctypes.data, n, status.ctypes.data)
         return status
 
 

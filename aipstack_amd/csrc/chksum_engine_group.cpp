@@ -208,3 +208,65 @@ extern "C" int aipstack_chksum_engine_group_host_tx_fill(aipstack_chksum_engine_
                                                    h_status + i0);
     });
 }
+
+// Ring slots (frame i = h_len[i] bytes at h_base + i * slot_stride): contiguous runs of slots
+// per device, about equal slot counts. Every length is checked before any device starts.
+namespace {
+bool slots_ok(uint64_t slot_stride, const uint32_t *h_len, uint64_t n) {
+    if (slot_stride == 0) return false;
+    const uint64_t cap = std::min<uint64_t>(slot_stride, AIPSTACK_CHKSUM_MAX_LEN);
+    for (uint64_t i = 0; i < n; ++i)
+        if (h_len[i] > cap) return false;
+    return true;
+}
+}  // namespace
+
+extern "C" int aipstack_chksum_engine_group_host_slotted(aipstack_chksum_engine_group *g,
+                                                         const void *h_base, uint64_t slot_stride,
+                                                         const uint32_t *h_len, uint64_t n,
+                                                         uint16_t *h_out, uint32_t flags,
+                                                         int *dev_status) {
+    if (!g || !h_base || !h_len || !h_out) return AIPSTACK_CHKSUM_EINVAL;
+    if (n == 0) return AIPSTACK_CHKSUM_OK;
+    if (!slots_ok(slot_stride, h_len, n)) return AIPSTACK_CHKSUM_EINVAL;
+    std::lock_guard<std::mutex> lock(g->mu);
+    const auto cut = split(n, g->engines.size(), [&](uint64_t i) { return i * slot_stride; });
+    const char *b = static_cast<const char *>(h_base);
+    return fan_out(g, cut, dev_status, [&](size_t k, uint64_t i0, uint64_t i1) {
+        return aipstack_chksum_engine_host_slotted(g->engines[k], b + i0 * slot_stride,
+                                                   slot_stride, h_len + i0, i1 - i0, h_out + i0,
+                                                   flags);
+    });
+}
+
+extern "C" int aipstack_chksum_engine_group_host_rx_verify_slotted(
+    aipstack_chksum_engine_group *g, const void *h_base, uint64_t slot_stride,
+    const uint32_t *h_len, uint64_t n, uint8_t *h_verdicts, int *dev_status) {
+    if (!g || !h_base || !h_len || !h_verdicts) return AIPSTACK_CHKSUM_EINVAL;
+    if (n == 0) return AIPSTACK_CHKSUM_OK;
+    if (!slots_ok(slot_stride, h_len, n)) return AIPSTACK_CHKSUM_EINVAL;
+    std::lock_guard<std::mutex> lock(g->mu);
+    const auto cut = split(n, g->engines.size(), [&](uint64_t i) { return i * slot_stride; });
+    const char *b = static_cast<const char *>(h_base);
+    return fan_out(g, cut, dev_status, [&](size_t k, uint64_t i0, uint64_t i1) {
+        return aipstack_chksum_engine_host_rx_verify_slotted(g->engines[k], b + i0 * slot_stride,
+                                                             slot_stride, h_len + i0, i1 - i0,
+                                                             h_verdicts + i0);
+    });
+}
+
+extern "C" int aipstack_chksum_engine_group_host_tx_fill_slotted(
+    aipstack_chksum_engine_group *g, void *h_base, uint64_t slot_stride, const uint32_t *h_len,
+    uint64_t n, uint8_t *h_status, int *dev_status) {
+    if (!g || !h_base || !h_len || !h_status) return AIPSTACK_CHKSUM_EINVAL;
+    if (n == 0) return AIPSTACK_CHKSUM_OK;
+    if (!slots_ok(slot_stride, h_len, n)) return AIPSTACK_CHKSUM_EINVAL;
+    std::lock_guard<std::mutex> lock(g->mu);
+    const auto cut = split(n, g->engines.size(), [&](uint64_t i) { return i * slot_stride; });
+    char *b = static_cast<char *>(h_base);
+    return fan_out(g, cut, dev_status, [&](size_t k, uint64_t i0, uint64_t i1) {
+        return aipstack_chksum_engine_host_tx_fill_slotted(g->engines[k], b + i0 * slot_stride,
+                                                           slot_stride, h_len + i0, i1 - i0,
+                                                           h_status + i0);
+    });
+}

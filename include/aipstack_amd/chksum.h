@@ -336,6 +336,21 @@ int aipstack_chksum_engine_group_host_rx_verify(aipstack_chksum_engine_group *gr
 int aipstack_chksum_engine_group_host_tx_fill(aipstack_chksum_engine_group *group, void *h_base,
                                               const uint64_t *h_offsets, uint64_t n,
                                               uint8_t *h_status, int *dev_status);
+/* Ring slots (frame i = h_len[i] bytes at h_base + i*slot_stride): contiguous runs of about
+ * equal slot counts per device; every length is checked (<= min(slot_stride, 65535)) before
+ * any device starts. */
+int aipstack_chksum_engine_group_host_slotted(aipstack_chksum_engine_group *group,
+                                              const void *h_base, uint64_t slot_stride,
+                                              const uint32_t *h_len, uint64_t n, uint16_t *h_out,
+                                              uint32_t flags, int *dev_status);
+int aipstack_chksum_engine_group_host_rx_verify_slotted(aipstack_chksum_engine_group *group,
+                                                        const void *h_base, uint64_t slot_stride,
+                                                        const uint32_t *h_len, uint64_t n,
+                                                        uint8_t *h_verdicts, int *dev_status);
+int aipstack_chksum_engine_group_host_tx_fill_slotted(aipstack_chksum_engine_group *group,
+                                                      void *h_base, uint64_t slot_stride,
+                                                      const uint32_t *h_len, uint64_t n,
+                                                      uint8_t *h_status, int *dev_status);
 
 /* ---- diagnostics ------------------------------------------------------------------ */
 

@@ -1280,6 +1280,35 @@ def test_engine_group(oracle, devices, register):
             grp.csr(buf, bad)
 
 
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0]])
+@pytest.mark.parametrize("register", [False, True])
+def test_engine_group_ring_slots(oracle, devices, register):
+    """The engine group on a ring of 2048-B slots: contiguous runs of slots per engine;
+    checksums, Rx verify and Tx fill in place against the oracle; a length over the slot
+    rejected before any engine starts (the ring unchanged)."""
+    with A.ChksumEngineGroup(devices, chunk_bytes=4 << 20, nstreams=2) as grp:
+        fr, foff = synth.frames_host(60000, seed=83, max_payload=1460)
+        ring, lens = synth.to_slots(fr, foff, 2048)
+        if register:
+            grp.register(ring)
+        want = ring.copy()
+        want_st = oracle.tx_fill_slotted(want, 2048, lens)
+        assert np.array_equal(grp.tx_fill_slotted(ring, 2048, lens), want_st)
+        assert np.array_equal(ring, want) and grp.last_status == [0] * len(devices)
+        assert np.array_equal(grp.rx_verify_slotted(ring, 2048, lens),
+                              oracle.rx_verify_slotted(ring, 2048, lens))
+        assert np.array_equal(grp.slotted(ring, 2048, lens, final=True),
+                              oracle.batch_slotted(ring, 2048, lens, final=True))
+        bad = lens.copy()
+        bad[-1] = 2049
+        before = ring.copy()
+        with pytest.raises(A.ChksumError):
+            grp.tx_fill_slotted(ring, 2048, bad)
+        assert np.array_equal(ring, before)
+        if register:
+            grp.unregister(ring)
+
+
 def test_bench_e2e_engine_group_line():
     """bench.py --e2e --engines 3 (all on device 0 here): one JSON line, bit-exact, the
     engines and their devices named."""

@@ -136,6 +136,25 @@ def _walk(lib, prefix, blob, lens, offset, tot_len, process_len, budget):
     return cnt, rel, [int(x) for x in out]
 
 
+def _walk_py(blob, lens, offset, tot_len, process_len, budget):
+    """The same walk through the Python mirror (aipstack_amd.ipBufProcessBytes)."""
+    import aipstack_amd as A
+    starts = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+    nodes = [A.IpBufNode(blob[int(o):int(o) + int(l)], int(l)) for o, l in zip(starts, lens)]
+    for a, b in zip(nodes, nodes[1:]):
+        a.next = b
+    offered, left = [], [budget]
+
+    def visit(mv, n):
+        addr = np.frombuffer(mv, dtype=np.uint8).ctypes.data
+        offered.append((addr - blob.ctypes.data, n))
+        took = min(n, left[0])
+        left[0] -= took
+        return took
+    r = A.ipBufProcessBytes(A.IpBufRef(nodes[0], offset, tot_len), process_len, visit)
+    return len(offered), offered[:64], [nodes.index(r.node), r.offset, r.tot_len]
+
+
 @pytest.mark.skipif(not os.path.exists(REF_LIB), reason="reference library not built here")
 def test_ip_buf_process_bytes_vs_reference(golden):
     """ipBufProcessBytes (BufUtils.h:129-178) itself, compiled from call_sites.inc against the
@@ -158,8 +177,9 @@ def test_ip_buf_process_bytes_vs_reference(golden):
         process_len = int(rng.integers(0, tot_len + 1))
         budget = int(rng.integers(0, process_len + 2)) if rng.random() < 0.5 else 1 << 40
         args = (blob, lens, offset, tot_len, process_len, budget)
-        assert _walk(hpp, "hpp", *args) == _walk(ref, "ref", *args), (lens, offset, tot_len,
-                                                                      process_len, budget)
+        want = _walk(ref, "ref", *args)
+        assert _walk(hpp, "hpp", *args) == want, (lens, offset, tot_len, process_len, budget)
+        assert _walk_py(*args) == want, ("python", lens, offset, tot_len, process_len, budget)
         n_cases += 1
     assert n_cases == 3000
 

@@ -34,7 +34,7 @@ if [ "$phase" = bench ] || [ "$phase" = all ]; then
 fi
 if [ "$phase" = e2e ] || [ "$phase" = all ]; then
   : > "$out/e2e.jsonl"
-  for c in A C RX TX; do
+  for c in A C RX TX RX2K C2K; do
     timeout -k 10 300 python bench.py --e2e --config $c --steps 5 --warmup 1 >> "$out/e2e.jsonl" 2>> "$out/e2e.err"
     timeout -k 10 300 python bench.py --e2e --e2e-pageable --config $c --steps 3 --warmup 1 >> "$out/e2e.jsonl" 2>> "$out/e2e.err"
   done

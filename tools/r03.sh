@@ -7,6 +7,7 @@
 #           stats and FETCH/WRITE passes of TXREC; then pytest -m gpu
 #   check   pytest -m gpu, then bench A, C, CHAIN, TXREC, RX (no CPU baseline)
 #   txnt    split Tx fill: scatter stores plain vs nontemporal (+ rocprof of each)
+#   asweep  launch shapes of configs A and B (robustness across boxes)
 #   ring    e2e receive rings (RX2K / C2K): 2-D copies of the slots' used prefix vs whole slots
 #   slots   pytest -m gpu; ring-slot lines RX2K / C2K (+ their slot-read ceilings) and A2K;
 #           a U/P sweep of the slotted checksum; e2e through an engine group of 1/2/4
@@ -145,6 +146,17 @@ ring)
   bench e2e_ring --e2e --e2e-pageable --config RX2K --steps 3 --warmup 1
   AIPSTACK_ENGINE_SLOT_ROWS=0 bench e2e_ring_full --e2e --e2e-pageable --config RX2K --steps 3 --warmup 1
   bench e2e_rx --e2e --config RX --steps 5 --warmup 1
+  ;;
+asweep)
+  # config A / B launch shapes, interleaved in one process per config (tools/sweep.py): the
+  # default against more windows in flight, smaller chunks (more waves), runs of chunks
+  v="stream=0;stream=4;stream=8;chunk_packets=32,stream=2;chunk_packets=32,stream=4;\
+chunk_packets=16,stream=4;waves_per_cu=32;waves_per_cu=16,stream=4"
+  for c in A B; do
+    timeout -k 10 300 python tools/sweep.py --config $c --rounds 6 --variants "$v" \
+        > "$out/sweep_$c.jsonl" 2> "$out/sweep_$c.err"
+  done
+  timeout -k 10 120 tools/build/hbm_peak > "$out/hbm_peak.jsonl"
   ;;
 *)
   echo "unknown mode $mode" >&2; exit 2 ;;

@@ -121,6 +121,11 @@ def main():
 
     variants = []
     for v in (args.variants or DEFAULT_VARIANTS[args.config]).split(";"):
+        if "=" in v:  # "key=value,...": any aipstack_chksum_tune keys (unset ones automatic)
+            d = {"unroll": 0, "packets": 0, "waves_per_cu": 0, "stream": 0, "chunk_packets": 0}
+            d.update({k: int(x) for k, x in (kv.split("=") for kv in v.split(","))})
+            variants.append(d)
+            continue
         if layout in ("rx", "tx"):
             f = [int(x) for x in v.split(",")]
             variants.append({"frames": f[0], "waves_per_cu": f[1],
@@ -133,9 +138,9 @@ def main():
                          "stream": su})
 
     def apply(v):
+        lib.aipstack_chksum_tune(b"chunks_per_wave", 0)
         for k, val in v.items():
             assert lib.aipstack_chksum_tune(k.encode(), val) == 0
-        lib.aipstack_chksum_tune(b"chunks_per_wave", 0)
 
     def check(got):
         if layout == "rx":
