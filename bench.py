@@ -520,8 +520,6 @@ def main():
     if args.e2e:
         if layout not in ("strided", "csr", "rx", "tx", "rxslot", "csrslot"):
             raise SystemExit("--e2e covers the configs A, B, C, RX, TX, RX2K and C2K")
-        if args.engines > 0 and layout in ("rxslot", "csrslot"):
-            raise SystemExit("--engines covers the back-to-back configs")
         return e2e(args, rank, world, local_rank, layout, n, plen)
 
     # ---- this rank's shard, generated in place (global packets [rank*n, (rank+1)*n))

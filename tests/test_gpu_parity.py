@@ -1323,15 +1323,20 @@ def test_bench_e2e_engine_group_line():
     assert d["config"]["engines"] == 3 and d["config"]["engine_devices"] == [0, 0, 0]
 
 
-@pytest.mark.parametrize("config,pageable", [("RX2K", False), ("C2K", True)])
-def test_bench_e2e_ring_slots_line(config, pageable):
-    """bench.py --e2e on a receive ring (RX2K / C2K, 2048-B slots): one JSON line, bit-exact
-    against the oracle over every slot; the value counts frame bytes, not slot bytes."""
+@pytest.mark.parametrize("config,pageable,engines", [("RX2K", False, 0), ("C2K", True, 0),
+                                                     ("RX2K", False, 2)])
+def test_bench_e2e_ring_slots_line(config, pageable, engines):
+    """bench.py --e2e on a receive ring (RX2K / C2K, 2048-B slots; also through an engine group
+    of 2 on the one device): one JSON line, bit-exact against the oracle over every slot; the
+    value counts frame bytes, not slot bytes."""
     import json
     cmd = [sys.executable, "bench.py", "--e2e", "--config", config, "--steps", "2", "--warmup", "1"]
     if pageable:
         cmd.append("--e2e-pageable")
-    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    if engines:
+        cmd += ["--engines", str(engines)]
+    env = dict(os.environ, AIPSTACK_BENCH_FORCE_DEVICE="0")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([l for l in r.stdout.splitlines() if l.strip()][-1])
     assert d["parity"].startswith("bit-exact") and d["value"] > 0
