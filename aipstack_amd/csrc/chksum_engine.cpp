@@ -132,6 +132,17 @@ void release(aipstack_chksum_engine *e) {
         if (r.owned) (void)hipHostUnregister(const_cast<char *>(r.p));
 }
 
+// Host threads the engine may use for one piece's Tx records / pageable staging copy
+// (AIPSTACK_ENGINE_HOST_THREADS, default 8; read once).
+unsigned host_threads_cap() {
+    static const unsigned cap = [] {
+        const char *v = std::getenv("AIPSTACK_ENGINE_HOST_THREADS");
+        const int t = v ? std::atoi(v) : 8;
+        return (unsigned)std::min(std::max(t, 1), 64);
+    }();
+    return cap;
+}
+
 // Pageable input into pinned staging: one core copies ~20 GB/s, below the PCIe link the
 // DMA then feeds, so large pieces are copied by several threads over disjoint 4 KiB-aligned
 // ranges (the previous piece's DMA runs meanwhile).
@@ -139,7 +150,8 @@ void stage_copy(void *dst, const void *src, uint64_t bytes) {
     constexpr uint64_t kPerThreadMin = 4ull << 20;
     const unsigned hw = std::thread::hardware_concurrency();
     const uint64_t want = bytes / kPerThreadMin;
-    const unsigned nt = (unsigned)std::min<uint64_t>(std::min<uint64_t>(want, 8), hw ? hw : 1);
+    const unsigned nt = (unsigned)std::min<uint64_t>(std::min<uint64_t>(want, host_threads_cap()),
+                                                     hw ? hw : 1);
     if (nt <= 1) {
         std::memcpy(dst, src, bytes);
         return;
@@ -180,13 +192,13 @@ void apply_tx_range(const uint64_t *rec, char *frames, const uint64_t *offs, uin
 }
 
 // A piece's frames are spread over up to 64 MiB of host memory: every frame is a cache miss,
-// so a large piece is applied by up to 8 threads (16 Ki frames and more each).
+// so a large piece is applied by several threads (16 Ki frames and more each).
 void apply_tx_records(const uint64_t *rec, char *frames, const uint64_t *offs, uint64_t stride,
                       uint8_t *status, uint64_t count) {
     constexpr uint64_t kPerThreadMin = 16384;
     const unsigned hw = std::thread::hardware_concurrency();
-    const unsigned nt =
-        (unsigned)std::min<uint64_t>(std::min<uint64_t>(count / kPerThreadMin, 8), hw ? hw : 1);
+    const unsigned nt = (unsigned)std::min<uint64_t>(
+        std::min<uint64_t>(count / kPerThreadMin, host_threads_cap()), hw ? hw : 1);
     if (nt <= 1) {
         apply_tx_range(rec, frames, offs, stride, status, 0, count);
         return;

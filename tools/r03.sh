@@ -8,6 +8,7 @@
 #   check   pytest -m gpu, then bench A, C, CHAIN, TXREC, RX (no CPU baseline)
 #   txnt    split Tx fill: scatter stores plain vs nontemporal (+ rocprof of each)
 #   asweep  launch shapes of configs A and B (robustness across boxes)
+#   e2ethreads  host engine Tx: apply/staging threads, piece size, streams
 #   ring    e2e receive rings (RX2K / C2K): 2-D copies of the slots' used prefix vs whole slots
 #   slots   pytest -m gpu; ring-slot lines RX2K / C2K (+ their slot-read ceilings) and A2K;
 #           a U/P sweep of the slotted checksum; e2e through an engine group of 1/2/4
@@ -157,6 +158,19 @@ chunk_packets=16,stream=4;waves_per_cu=32;waves_per_cu=16,stream=4"
         > "$out/sweep_$c.jsonl" 2> "$out/sweep_$c.err"
   done
   timeout -k 10 120 tools/build/hbm_peak > "$out/hbm_peak.jsonl"
+  ;;
+e2ethreads)
+  # host engine: threads for the Tx record apply / pageable staging (8 = default, 16, 32),
+  # and the piece size / stream count for the Tx fill, alternating
+  for i in 1 2; do
+    for t in 8 16 32; do
+      AIPSTACK_ENGINE_HOST_THREADS=$t bench tx_t$t --e2e --config TX --steps 5 --warmup 1
+      AIPSTACK_ENGINE_HOST_THREADS=$t bench txp_t$t --e2e --e2e-pageable --config TX --steps 3 --warmup 1
+    done
+    bench tx_c32 --e2e --config TX --steps 5 --warmup 1 --e2e-chunk-mib 32
+    bench tx_s8 --e2e --config TX --steps 5 --warmup 1 --e2e-streams 8
+    bench rx --e2e --config RX --steps 5 --warmup 1
+  done
   ;;
 *)
   echo "unknown mode $mode" >&2; exit 2 ;;
