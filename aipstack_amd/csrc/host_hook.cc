@@ -31,9 +31,10 @@ inline uint64_t load_le64(const unsigned char *p) {
 // (Chksum.h:90-93). Folding keeps nonzero sums nonzero, so 0 is returned only for all-zero
 // input, as by the reference.
 //
-// Three bodies, chosen once at load time by CPU feature: AVX2 (32-byte loads, 16-bit halves
-// added into 32-bit lanes), SSE2 (the x86-64 baseline, 16-byte loads), and a portable
-// 64-bit-word loop for the tail of both.
+// Four bodies, chosen once at load time by CPU feature: AVX-512 (64-byte loads, a masked
+// load for the tail), AVX2 (32-byte loads, 16-bit halves added into 32-bit lanes), SSE2 (the
+// x86-64 baseline, 16-byte loads), and a portable 64-bit-word loop (the tail of the SSE2 and
+// AVX2 bodies).
 
 namespace {
 
@@ -110,6 +111,41 @@ __attribute__((target("avx2"))) uint16_t chksum_avx2(const unsigned char *p, siz
     for (int k = 0; k < 8; ++k) s += lanes[k];
     return fold_swap(s);
 }
+
+// AVX-512: 64-byte loads, the same halves-into-32-bit-lanes sum (per lane < 2^28 for 65535
+// bytes), and the tail (< 64 bytes) as one byte-masked load: masked-off bytes read as zero
+// and are never touched, so the zero padding of an odd tail comes for free.
+__attribute__((target("avx512f,avx512bw"))) uint16_t chksum_avx512(const unsigned char *p,
+                                                                   size_t len) {
+    const __m512i lo16 = _mm512_set1_epi32(0xFFFF);
+    __m512i acc0 = _mm512_setzero_si512(), acc1 = _mm512_setzero_si512();
+    size_t i = 0;
+    for (; i + 128 <= len; i += 128) {
+        const __m512i x0 = _mm512_loadu_si512(p + i);
+        const __m512i x1 = _mm512_loadu_si512(p + i + 64);
+        acc0 = _mm512_add_epi32(acc0, _mm512_add_epi32(_mm512_and_si512(x0, lo16),
+                                                       _mm512_srli_epi32(x0, 16)));
+        acc1 = _mm512_add_epi32(acc1, _mm512_add_epi32(_mm512_and_si512(x1, lo16),
+                                                       _mm512_srli_epi32(x1, 16)));
+    }
+    if (i + 64 <= len) {
+        const __m512i x = _mm512_loadu_si512(p + i);
+        acc0 = _mm512_add_epi32(acc0, _mm512_add_epi32(_mm512_and_si512(x, lo16),
+                                                       _mm512_srli_epi32(x, 16)));
+        i += 64;
+    }
+    if (i < len) {
+        const __mmask64 m = (__mmask64)((1ull << (len - i)) - 1u);  // len - i < 64
+        const __m512i x = _mm512_maskz_loadu_epi8(m, p + i);
+        acc1 = _mm512_add_epi32(acc1, _mm512_add_epi32(_mm512_and_si512(x, lo16),
+                                                       _mm512_srli_epi32(x, 16)));
+    }
+    alignas(64) uint32_t lanes[16];
+    _mm512_store_si512(lanes, _mm512_add_epi32(acc0, acc1));
+    uint64_t s = 0;
+    for (int k = 0; k < 16; ++k) s += lanes[k];
+    return fold_swap(s);
+}
 #endif
 
 using ChksumFn = uint16_t (*)(const unsigned char *, size_t);
@@ -117,6 +153,8 @@ using ChksumFn = uint16_t (*)(const unsigned char *, size_t);
 ChksumFn pick_host_chksum() {
 #if defined(__x86_64__)
     __builtin_cpu_init();
+    if (__builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw"))
+        return chksum_avx512;
     if (__builtin_cpu_supports("avx2")) return chksum_avx2;
     return chksum_sse2;
 #else
@@ -133,10 +171,13 @@ extern "C" uint16_t IpChksumInverted(const char *data, size_t len) {
 }
 
 // Forced variants for tests / benchmarks (not in the public header): 0 portable, 1 SSE2,
-// 2 AVX2 (falls back to the best supported when the CPU lacks it).
+// 2 AVX2, 3 AVX-512 (each falls back to the next one down when the CPU lacks it).
 extern "C" uint16_t aipstack_chksum_host_variant(int variant, const char *data, size_t len) {
     const unsigned char *p = reinterpret_cast<const unsigned char *>(data);
 #if defined(__x86_64__)
+    if (variant == 3 && __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw"))
+        return chksum_avx512(p, len);
+    if (variant == 3) variant = 2;
     if (variant == 1) return chksum_sse2(p, len);
     if (variant == 2 && __builtin_cpu_supports("avx2")) return chksum_avx2(p, len);
     if (variant == 2) return chksum_sse2(p, len);

@@ -163,7 +163,8 @@ def test_chain_to_chunks_covers_tot_len(golden):
 
 
 def test_host_hook_variants_match_oracle(oracle):
-    """Portable / SSE2 / AVX2 bodies of the hook (host_hook.cc) against the oracle."""
+    """Portable / SSE2 / AVX2 / AVX-512 bodies of the hook (host_hook.cc) against the oracle
+    (a body the CPU lacks falls back to the next one down)."""
     lib = A._lib.load()
     f = lib.aipstack_chksum_host_variant
     f.restype = ctypes.c_uint16
@@ -175,5 +176,5 @@ def test_host_hook_variants_match_oracle(oracle):
         o = int(rng.integers(0, 70000 if t % 2 else 64))
         ln = min(int(rng.integers(0, 65536 if t % 50 == 0 else 3000)), 65535, buf.size - o)
         want = oracle.inverted(buf, o, ln)
-        for v in (0, 1, 2):
+        for v in (0, 1, 2, 3):
             assert f(v, buf.ctypes.data + o, ln) == want, (v, o, ln)
