@@ -633,44 +633,56 @@ def main():
         alg += 10 * n  # + the field address read and the 2-byte field written per chain
 
     # ---- parity: EVERY rank checks its own shard (after the timed region) against the
-    # oracle / the reference; rank 0 also times the CPU baseline on its shard
+    # oracle / the reference; then (after a barrier, so that no other rank's check competes
+    # for the host cores) rank 0 times the CPU baseline on its shard
     parity = None
     cpu = None
+    baseline = None  # rank 0's CPU baseline, run after every rank's check
     if layout in ("rx", "tx", "txrec"):
         if not args.no_parity and layout == "txrec":
             parity = records_check(spec, frames_host, buf.cpu().numpy(), records.cpu().numpy())
         elif not args.no_parity:
             parity = frames_check(spec, frames_host, buf.cpu().numpy(), status.cpu().numpy())
-        if rank == 0 and not args.no_cpu_baseline:
-            cpu = cpu_baseline_frames(spec, frames_host)
+        baseline = lambda: cpu_baseline_frames(spec, frames_host)
     elif layout in ("rxslot", "csrslot"):
         if not args.no_parity:
             parity = slots_check(layout, ring_host, lens_host,
                                  (status if layout == "rxslot" else out).cpu().numpy())
-        if rank == 0 and not args.no_cpu_baseline:
+
+        def baseline():
             # the same frames / packets in their compact (CSR) form: the same host work
-            cspec = dict(spec, layout="rx" if layout == "rxslot" else "csr", total=int(spec["offsets"][-1]))
+            cspec = dict(spec, layout="rx" if layout == "rxslot" else "csr",
+                         total=int(spec["offsets"][-1]))
             cspec.pop("payload", None)
-            if layout == "rxslot":
-                cpu = cpu_baseline_frames(cspec, compact_host)
-            else:
-                cpu, _ = cpu_baseline(cspec)
-            cpu["sample"] += " (the same packets in their compact CSR form)"
+            c = cpu_baseline_frames(cspec, compact_host) if layout == "rxslot" \
+                else cpu_baseline(cspec)[0]
+            c["sample"] += " (the same packets in their compact CSR form)"
+            return c
     elif layout == "chain":
         if not args.no_parity:
             parity = (chain_fill_check(chain) if args.chain_fill
                       else chain_check(chain, out.cpu().numpy()))
-        if rank == 0 and not args.no_cpu_baseline:
-            cpu = cpu_baseline_chain(chain)
+        baseline = lambda: cpu_baseline_chain(chain)
     else:
         host_out = out.cpu().numpy()
-        if rank == 0 and not args.no_cpu_baseline:
-            cpu, want = cpu_baseline(spec)
+        if world == 1 and not args.no_cpu_baseline:
+            # one rank: the baseline's own output (the reference over the whole shard) is
+            # the check
+            def baseline():
+                nonlocal parity
+                c, want = cpu_baseline(spec)
+                if not args.no_parity:
+                    parity = ("bit-exact (whole shard vs reference)"
+                              if np.array_equal(host_out, want) else "MISMATCH")
+                return c
+        else:
             if not args.no_parity:
-                parity = ("bit-exact (whole shard vs reference)" if np.array_equal(host_out, want)
-                          else "MISMATCH")
-        elif not args.no_parity:
-            parity = oracle_check(spec, host_out, threads=max(1, _affinity_cores() // world))
+                parity = oracle_check(spec, host_out, threads=max(1, _affinity_cores() // world))
+            baseline = lambda: cpu_baseline(spec)[0]
+    if world > 1:
+        dist.barrier()
+    if rank == 0 and not args.no_cpu_baseline and baseline is not None:
+        cpu = baseline()
     # which device each rank ran on, gathered on the control plane with its parity
     props = torch.cuda.get_device_properties(device)
     mine_info = {"rank": rank, "device": device,
