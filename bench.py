@@ -48,11 +48,12 @@ CONFIGS = {
     "TXREC": ("txrec", 1 << 20, None),
     # ring slots (one frame / packet per 2048-B slot, a length per slot; TAP receive ring)
     "RX2K": ("rxslot", 1 << 20, None),
+    "TX2K": ("txslot", 1 << 20, None),  # a send ring: Tx fill in place, one frame per slot
     "C2K": ("csrslot", 2 << 20, None),
     # chained + seeded (TCP Tx shape)
     "CHAIN": ("chain", 1 << 20, None),
 }
-SLOT_STRIDE = {"A2K": 2048, "RX2K": 2048, "C2K": 2048}  # layouts not back to back
+SLOT_STRIDE = {"A2K": 2048, "RX2K": 2048, "TX2K": 2048, "C2K": 2048}  # layouts not back to back
 WORKLOAD_NAMES = {
     "A": "1M x 1500B Ethernet-MTU packets per GPU, IP checksum (BASELINE configs[1]; x8 = configs[4])",
     "B": "256K x 9000B jumbo packets per GPU, IP checksum (BASELINE configs[2])",
@@ -68,6 +69,8 @@ WORKLOAD_NAMES = {
              "nothing written into the frames)",
     "RX2K": "1M raw Ethernet frames per GPU (RX mix) in 2048B ring slots with a length per "
             "slot, Rx verify (aipstack_chksum_rx_verify_slotted)",
+    "TX2K": "1M raw Ethernet frames per GPU (TX mix) in 2048B ring slots with a length per "
+            "slot, Tx fill in place (aipstack_chksum_tx_fill_slotted)",
     "C2K": "2M mixed 64-1500B packets per GPU (config C's) in 2048B ring slots with a length "
            "per slot, IP checksum (aipstack_chksum_batch_slotted)",
     "CHAIN": "1M TCP-Tx-shaped chains per GPU: IpChksumAccumulator(pseudo-header State)"
@@ -153,7 +156,7 @@ def shard_spec(config, rank, world, n=None):
         spec["payload"] = n * plen
         spec["byte_offset"] = rank * n * stride
         spec["offsets"] = None
-    elif layout in ("rx", "tx", "txrec", "rxslot", "chain"):
+    elif layout in ("rx", "tx", "txrec", "rxslot", "txslot", "chain"):
         # each rank synthesises its own frames / chains (seed per rank): they are independent
         spec["seed"] = synth.SEED_DATA + 1000 * rank
         spec["byte_offset"] = 0
@@ -170,7 +173,7 @@ def shard_spec(config, rank, world, n=None):
 def host_shard(spec):
     """The shard's bytes in host memory (numpy), exactly as the device generators make them."""
     from aipstack_amd import synth
-    if spec["layout"] in ("rx", "tx", "txrec", "rxslot"):
+    if spec["layout"] in ("rx", "tx", "txrec", "rxslot", "txslot"):
         buf, off = synth.frames_host(spec["n"], seed=spec["seed"], max_payload=1460)
         spec["offsets"], spec["total"] = off, int(off[-1])
         if spec["layout"] in ("rx", "rxslot"):  # valid frames: filled by the oracle (test infra)
@@ -200,6 +203,8 @@ def algorithmic_bytes(layout, n, total_payload):
         return total_payload + 16 * n + 8
     if layout == "rxslot":  # frame bytes + 4 B length + 1 B verdict
         return total_payload + 5 * n
+    if layout == "txslot":  # frame bytes + 4 B length + 1 B status + 4 B of checksums written
+        return total_payload + 9 * n
     if layout == "csrslot":  # packet bytes + 4 B length + 2 B result
         return total_payload + 6 * n
     if layout in ("rx", "tx"):
@@ -518,8 +523,8 @@ def main():
             raise SystemExit("--small covers configs A, RX and TX on one GPU")
         return small_batches(args, layout, plen, dev)
     if args.e2e:
-        if layout not in ("strided", "csr", "rx", "tx", "rxslot", "csrslot"):
-            raise SystemExit("--e2e covers the configs A, B, C, RX, TX, RX2K and C2K")
+        if layout not in ("strided", "csr", "rx", "tx", "rxslot", "csrslot", "txslot"):
+            raise SystemExit("--e2e covers the configs A, B, C, RX, TX, RX2K, TX2K and C2K")
         return e2e(args, rank, world, local_rank, layout, n, plen)
 
     # ---- this rank's shard, generated in place (global packets [rank*n, (rank+1)*n))
@@ -531,7 +536,7 @@ def main():
         status = torch.empty(n, dtype=torch.uint8, device=dev)
         tx_ws = torch.empty(8 * n, dtype=torch.uint8, device=dev)  # split fill's records
         records = torch.empty(n, dtype=torch.int64, device=dev)
-    if layout in ("rxslot", "csrslot"):
+    if layout in ("rxslot", "csrslot", "txslot"):
         # the shard's frames / packets laid into 2048-B ring slots (slack = random bytes)
         compact_host = host_shard(spec)
         ring_host, lens_host = synth.to_slots(compact_host, spec["offsets"], SLOT_STRIDE[args.config])
@@ -569,6 +574,8 @@ def main():
             A.rx_verify_slotted(buf, 2048, d_lens, out=status, stream=stream)
         elif layout == "csrslot":
             A.chksum_batch_slotted(buf, 2048, d_lens, out=out, stream=stream)
+        elif layout == "txslot":  # idempotent, as the CSR fill
+            A.tx_fill_slotted(buf, 2048, d_lens, out=status, stream=stream)
         elif layout == "chain" and args.chain_fill:
             A.chksum_chain_fill(chain["addr"], chain["len"], chain["index"], chain["states"],
                                 chain["fields"], out=out, stream=stream)
@@ -644,17 +651,20 @@ def main():
         elif not args.no_parity:
             parity = frames_check(spec, frames_host, buf.cpu().numpy(), status.cpu().numpy())
         baseline = lambda: cpu_baseline_frames(spec, frames_host)
-    elif layout in ("rxslot", "csrslot"):
-        if not args.no_parity:
+    elif layout in ("rxslot", "csrslot", "txslot"):
+        if not args.no_parity and layout == "txslot":
+            parity = tx_slots_check(ring_host, lens_host, buf.cpu().numpy(),
+                                    status.cpu().numpy())
+        elif not args.no_parity:
             parity = slots_check(layout, ring_host, lens_host,
                                  (status if layout == "rxslot" else out).cpu().numpy())
 
         def baseline():
             # the same frames / packets in their compact (CSR) form: the same host work
-            cspec = dict(spec, layout="rx" if layout == "rxslot" else "csr",
+            cspec = dict(spec, layout={"rxslot": "rx", "txslot": "tx"}.get(layout, "csr"),
                          total=int(spec["offsets"][-1]))
             cspec.pop("payload", None)
-            c = cpu_baseline_frames(cspec, compact_host) if layout == "rxslot" \
+            c = cpu_baseline_frames(cspec, compact_host) if layout != "csrslot" \
                 else cpu_baseline(cspec)[0]
             c["sample"] += " (the same packets in their compact CSR form)"
             return c
@@ -702,7 +712,7 @@ def main():
 
     traffic, traffic_stale = _pmc_traffic(args.config)
     slot_ceiling_fields = {}
-    if layout in ("rxslot", "csrslot") and rank == 0:
+    if layout in ("rxslot", "csrslot", "txslot") and rank == 0:
         ceil = slot_read_ceiling(args.config, spec)
         if ceil:
             kernel_gbps = payload / avg_kernel_s / 1e9
@@ -731,8 +741,8 @@ def main():
             "config": args.config,
             "packets_per_gpu": n,
             **({"slot_stride": stride} if layout == "strided" and stride != plen else {}),
-            **({"slot_stride": SLOT_STRIDE[args.config]} if layout in ("rxslot", "csrslot")
-               else {}),
+            **({"slot_stride": SLOT_STRIDE[args.config]}
+               if layout in ("rxslot", "csrslot", "txslot") else {}),
             "packet_bytes": plen if plen else {"csr": "64-1500 (mixed)", "csrslot": "64-1500 (mixed)",
                                                 "chain": "20 + 1460 in 3 chunks"}.get(
                                                     layout, "60-1514 (frames)"),
@@ -906,16 +916,16 @@ def e2e(args, rank, world, local_rank, layout, n, plen):
     off, total = spec["offsets"], spec.get("payload", spec["total"])
     stride = spec.get("stride", plen)
     host = host_shard(spec)
-    frames = layout in ("rx", "tx", "rxslot")
+    frames = layout in ("rx", "tx", "rxslot", "txslot")
     if frames:  # frames: synthesised (and, for RX, made valid) on the host by host_shard
         off, total = spec["offsets"], spec["total"]
     slot = SLOT_STRIDE.get(args.config)
-    if layout in ("rxslot", "csrslot"):  # a receive ring: one frame / packet per slot
+    if layout in ("rxslot", "csrslot", "txslot"):  # a ring: one frame / packet per slot
         host, lens = synth.to_slots(host, off, slot)
         total = int(lens.sum(dtype=np.uint64))
     # Tx fill writes the frames in place: the fill ignores the fields' old contents, so
     # every step gives the same bytes; parity compares with the oracle's fill of a copy
-    orig = host.copy() if layout == "tx" and not args.no_parity else None
+    orig = host.copy() if layout in ("tx", "txslot") and not args.no_parity else None
     out = np.empty(n, dtype=np.uint8 if frames else np.uint16)
     if args.engines > 0:
         forced = os.environ.get("AIPSTACK_BENCH_FORCE_DEVICE")
@@ -939,6 +949,8 @@ def e2e(args, rank, world, local_rank, layout, n, plen):
             eng.tx_fill(host, off, status=out)
         elif layout == "rxslot":
             eng.rx_verify_slotted(host, slot, lens, out=out)
+        elif layout == "txslot":
+            eng.tx_fill_slotted(host, slot, lens, status=out)
         elif layout == "csrslot":
             eng.slotted(host, slot, lens, out=out)
         else:
@@ -985,6 +997,13 @@ def e2e(args, rank, world, local_rank, layout, n, plen):
                                                                            ctypes.c_void_p]
             o = off.astype(np.uint64)
             lib.oracle_rx_verify_batch(host.ctypes.data, o.ctypes.data, n, want.ctypes.data)
+        elif layout == "txslot":
+            lib.oracle_tx_fill_slotted.argtypes = [ctypes.c_void_p, ctypes.c_uint64,
+                                                   ctypes.c_void_p, ctypes.c_uint64,
+                                                   ctypes.c_void_p]
+            ln = np.ascontiguousarray(lens, dtype=np.uint32)
+            lib.oracle_tx_fill_slotted(orig.ctypes.data, slot, ln.ctypes.data, n, want.ctypes.data)
+            ok_bytes = np.array_equal(host, orig)
         elif layout in ("rxslot", "csrslot"):
             fn = lib.oracle_rx_verify_slotted if layout == "rxslot" else lib.oracle_batch_slotted
             fn.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
@@ -1018,7 +1037,8 @@ def e2e(args, rank, world, local_rank, layout, n, plen):
     value = total * world * args.steps / max_elapsed / 2**30
     if rank == 0:
         print(json.dumps({
-            "metric": "GiB/s " + {"rx": "Rx-verified", "rxslot": "Rx-verified", "tx": "Tx-filled"}.get(layout, "checksummed")
+            "metric": "GiB/s " + {"rx": "Rx-verified", "rxslot": "Rx-verified", "tx": "Tx-filled",
+                                 "txslot": "Tx-filled"}.get(layout, "checksummed")
                       + " end-to-end (host memory in, host results out)",
             "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(max_elapsed / args.steps * 1e3, 3),
@@ -1030,7 +1050,7 @@ def e2e(args, rank, world, local_rank, layout, n, plen):
                        "streams": args.e2e_streams, "chunk_MiB": args.e2e_chunk_mib,
                        **({"slot_stride": slot, "ring_bytes": int(host.nbytes),
                            "value_counts": "frame/packet bytes (the lengths), not slot bytes"}
-                          if layout in ("rxslot", "csrslot") else {}),
+                          if layout in ("rxslot", "csrslot", "txslot") else {}),
                        **({"engines": args.engines, "engine_devices": engine_devices,
                            "engine_group": "one process, disjoint ranges of equal bytes, one "
                                            "host thread per engine"}
@@ -1087,7 +1107,7 @@ def slot_read_ceiling(config, spec):
     if not os.path.exists(exe):
         return None
     n = spec["n"]
-    args = (["frames", str(n), str(spec["seed"]), "1460", "2048"] if config == "RX2K"
+    args = (["frames", str(n), str(spec["seed"]), "1460", "2048"] if config in ("RX2K", "TX2K")
             else ["mixed", str(n), "2048"])
     if config == "C2K" and spec["first_packet"] != 0:
         return None  # the probe regenerates shard 0's lengths only
@@ -1098,6 +1118,19 @@ def slot_read_ceiling(config, spec):
         return d
     except (OSError, ValueError, IndexError, subprocess.SubprocessError):
         return None
+
+
+def tx_slots_check(ring_before, lens, ring_after, status):
+    """Send ring: the filled slots and the statuses vs the oracle's fill of a copy."""
+    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "libchksum_oracle.so"))
+    n = lens.size
+    want = np.empty(n, dtype=np.uint8)
+    ref = ring_before.copy()
+    lib.oracle_tx_fill_slotted.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                           ctypes.c_uint64, ctypes.c_void_p]
+    lib.oracle_tx_fill_slotted(ref.ctypes.data, 2048, lens.ctypes.data, n, want.ctypes.data)
+    ok = np.array_equal(status, want) and np.array_equal(ring_after, ref)
+    return "bit-exact (every slot filled as the oracle fills it)" if ok else "MISMATCH"
 
 
 def records_check(spec, frames_before, frames_after, records):

@@ -152,6 +152,27 @@ def test_slots_and_records_checks():
     assert bench.records_check(tspec, fr, fr.copy(), rec.view(np.int64)) == "MISMATCH"
 
 
+def test_tx_slots_check():
+    """The TX2K parity check (bench.tx_slots_check): filled slots and statuses vs the oracle's
+    fill of the ring as it was before the timed fills."""
+    import ctypes
+    spec = {"layout": "txslot", "n": 2500, "seed": 91}
+    frames = bench.host_shard(spec)
+    ring, lens = synth.to_slots(frames, spec["offsets"], 2048)
+    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "libchksum_oracle.so"))
+    filled = ring.copy()
+    st = np.empty(2500, dtype=np.uint8)
+    lib.oracle_tx_fill_slotted.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                           ctypes.c_uint64, ctypes.c_void_p]
+    lib.oracle_tx_fill_slotted(filled.ctypes.data, 2048, lens.ctypes.data, 2500, st.ctypes.data)
+    assert not np.array_equal(filled, ring)  # raw frames: the fill changes them
+    assert bench.tx_slots_check(ring, lens, filled, st).startswith("bit-exact")
+    bad = filled.copy()
+    bad[2048 * 7 + 24] ^= 1
+    assert bench.tx_slots_check(ring, lens, bad, st) == "MISMATCH"
+    assert bench.algorithmic_bytes("txslot", 10, 1000) == 1000 + 90
+
+
 def test_pmc_traffic_only_for_the_current_kernels(tmp_path, monkeypatch):
     """roofline.traffic comes from profiles/pmc_traffic.json only while the entry's kernel
     source digest matches this tree; otherwise null, the old value under traffic_stale."""

@@ -1324,7 +1324,8 @@ def test_bench_e2e_engine_group_line():
 
 
 @pytest.mark.parametrize("config,pageable,engines", [("RX2K", False, 0), ("C2K", True, 0),
-                                                     ("RX2K", False, 2)])
+                                                     ("RX2K", False, 2), ("TX2K", False, 0),
+                                                     ("TX2K", True, 2)])
 def test_bench_e2e_ring_slots_line(config, pageable, engines):
     """bench.py --e2e on a receive ring (RX2K / C2K, 2048-B slots; also through an engine group
     of 2 on the one device): one JSON line, bit-exact against the oracle over every slot; the
@@ -1341,7 +1342,21 @@ def test_bench_e2e_ring_slots_line(config, pageable, engines):
     d = json.loads([l for l in r.stdout.splitlines() if l.strip()][-1])
     assert d["parity"].startswith("bit-exact") and d["value"] > 0
     assert d["config"]["slot_stride"] == 2048
-    assert d["metric"].startswith("GiB/s Rx-verified" if config == "RX2K" else "GiB/s checksummed")
+    assert d["metric"].startswith({"RX2K": "GiB/s Rx-verified", "TX2K": "GiB/s Tx-filled"}.get(
+        config, "GiB/s checksummed"))
+
+
+def test_bench_tx2k_line():
+    """bench.py --config TX2K (a send ring filled in place on the device): one JSON line,
+    every slot filled as the oracle fills it, the slot-read ceiling beside it."""
+    import json
+    r = subprocess.run([sys.executable, "bench.py", "--config", "TX2K", "--steps", "5",
+                        "--warmup", "5", "--no-cpu-baseline"], cwd=ROOT, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.strip()][-1])
+    assert d["parity"].startswith("bit-exact") and d["config"]["slot_stride"] == 2048
+    assert d["roofline"]["frac"] > 0
 
 
 # ---- frame decisions pinned by the reference's own call sites (tests/golden/frame_ref.py) ---

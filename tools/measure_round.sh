@@ -24,7 +24,7 @@ if [ "$phase" = test ] || [ "$phase" = all ]; then
   timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > "$out/pytest_gpu.log" 2>&1
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.log" 2>&1
 fi
-CONFIGS=${CONFIGS:-A B C A2K C2K RX RX2K TX TXREC CHAIN}
+CONFIGS=${CONFIGS:-A B C A2K C2K RX RX2K TX TX2K TXREC CHAIN}
 if [ "$phase" = bench ] || [ "$phase" = all ]; then
   timeout -k 10 120 tools/build/hbm_peak > "$out/hbm_peak.jsonl"
   for c in $CONFIGS; do
@@ -34,7 +34,7 @@ if [ "$phase" = bench ] || [ "$phase" = all ]; then
 fi
 if [ "$phase" = e2e ] || [ "$phase" = all ]; then
   : > "$out/e2e.jsonl"
-  for c in A C RX TX RX2K C2K; do
+  for c in A C RX TX RX2K TX2K C2K; do
     timeout -k 10 300 python bench.py --e2e --config $c --steps 5 --warmup 1 >> "$out/e2e.jsonl" 2>> "$out/e2e.err"
     timeout -k 10 300 python bench.py --e2e --e2e-pageable --config $c --steps 3 --warmup 1 >> "$out/e2e.jsonl" 2>> "$out/e2e.err"
   done

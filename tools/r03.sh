@@ -9,6 +9,7 @@
 #   txnt    split Tx fill: scatter stores plain vs nontemporal (+ rocprof of each)
 #   asweep  launch shapes of configs A and B (robustness across boxes)
 #   e2ethreads  host engine Tx: apply/staging threads, piece size, streams
+#   tx2k    send ring: device in-place slotted Tx fill (bench + rocprof) and e2e
 #   ring    e2e receive rings (RX2K / C2K): 2-D copies of the slots' used prefix vs whole slots
 #   slots   pytest -m gpu; ring-slot lines RX2K / C2K (+ their slot-read ceilings) and A2K;
 #           a U/P sweep of the slotted checksum; e2e through an engine group of 1/2/4
@@ -171,6 +172,15 @@ e2ethreads)
     bench tx_s8 --e2e --config TX --steps 5 --warmup 1 --e2e-streams 8
     bench rx --e2e --config RX --steps 5 --warmup 1
   done
+  ;;
+tx2k)
+  # a send ring (TX2K): the in-place slotted fill on the device (+ its rocprof stats), and
+  # through the host engine (registered / pageable)
+  bench bench_TX2K --config TX2K --per-launch
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/prof_TX2K" -o run \
+      -- python3 bench.py --config TX2K --no-cpu-baseline --no-parity > "$out/prof_TX2K.log" 2>&1
+  bench e2e_tx2k --e2e --config TX2K --steps 5 --warmup 1
+  bench e2e_tx2k --e2e --e2e-pageable --config TX2K --steps 3 --warmup 1
   ;;
 *)
   echo "unknown mode $mode" >&2; exit 2 ;;
