@@ -10,6 +10,7 @@
 #   asweep  launch shapes of configs A and B (robustness across boxes)
 #   e2ethreads  host engine Tx: apply/staging threads, piece size, streams
 #   tx2k    send ring: device in-place slotted Tx fill (bench + rocprof) and e2e
+#   ringloop  the engine as a TAP receive loop from C++, per batch size
 #   ring    e2e receive rings (RX2K / C2K): 2-D copies of the slots' used prefix vs whole slots
 #   slots   pytest -m gpu; ring-slot lines RX2K / C2K (+ their slot-read ceilings) and A2K;
 #           a U/P sweep of the slotted checksum; e2e through an engine group of 1/2/4
@@ -181,6 +182,12 @@ tx2k)
       -- python3 bench.py --config TX2K --no-cpu-baseline --no-parity > "$out/prof_TX2K.log" 2>&1
   bench e2e_tx2k --e2e --config TX2K --steps 5 --warmup 1
   bench e2e_tx2k --e2e --e2e-pageable --config TX2K --steps 3 --warmup 1
+  ;;
+ringloop)
+  # the engine driven as a TAP receive loop (tools/ring_loop.cpp): 8 regions of B slots, 7
+  # batches in flight, per batch size B
+  timeout -k 10 400 tools/build/ring_loop 64 256 1024 4096 16384 65536 > "$out/ring_loop.jsonl" \
+      2> "$out/ring_loop.err"
   ;;
 *)
   echo "unknown mode $mode" >&2; exit 2 ;;
