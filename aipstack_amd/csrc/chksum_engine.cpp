@@ -54,6 +54,14 @@ struct Slot {
     void *h_stage = nullptr;       // pinned host staging (pageable inputs)
     uint64_t *h_off = nullptr;     // pinned host staging for rebased offsets
     uint16_t *h_out = nullptr;     // pinned host results
+    uint64_t *dh_off = nullptr;    // device addresses of h_off / h_out (mapped pinned memory)
+    uint16_t *dh_out = nullptr;
+    // What this piece's kernel reads its offsets / lengths from and writes its results to:
+    // d_off / d_out (copied H2D / D2H around the kernel), or, for a small piece, the pinned
+    // staging itself through dh_off / dh_out (no copies: fewer DMA ops per small batch)
+    uint64_t *k_off = nullptr;
+    uint16_t *k_out = nullptr;
+    bool zero_copy = false;
     hipEvent_t done = nullptr;
     bool busy = false;
     void *user_out = nullptr;      // where h_out goes once the slot completes
@@ -82,6 +90,7 @@ struct aipstack_chksum_engine {
     uint64_t chunk_bytes = 0;
     uint64_t chunk_packets = 0;
     bool slot_rows = true;  // ring slots: copy each slot's used prefix only (2-D copy)
+    uint64_t zero_copy_max = 0;  // pieces of at most this many packets skip the metadata copies
     std::vector<Slot> slots;
     std::vector<Region> registered;
     size_t next_slot = 0;      // round robin over the slots, across batches
@@ -284,6 +293,9 @@ int enqueue(aipstack_chksum_engine *e, uint64_t n, void *h_out, uint32_t elem, C
         Span sp;
         chunker(i0, &i1, &sp);
         const uint64_t cnt = i1 - i0;
+        s.zero_copy = cnt <= e->zero_copy_max;
+        s.k_off = s.zero_copy ? s.dh_off : s.d_off;
+        s.k_out = s.zero_copy ? s.dh_out : s.d_out;
         const bool registered = sp.bytes && is_registered(e, sp.src, sp.bytes);
         const bool rows = registered && sp.width != 0 && sp.width < sp.pitch;
         const void *h_src = sp.src;
@@ -304,7 +316,7 @@ int enqueue(aipstack_chksum_engine *e, uint64_t n, void *h_out, uint32_t elem, C
             status = AIPSTACK_CHKSUM_EHIP;
 #endif
         if (status == AIPSTACK_CHKSUM_OK) status = launch(s, i0, i1);
-        if (status == AIPSTACK_CHKSUM_OK)
+        if (status == AIPSTACK_CHKSUM_OK && !s.zero_copy)
             status = check_hip(hipMemcpyAsync(s.h_out, s.d_out, cnt * elem,
                                               hipMemcpyDeviceToHost, s.stream));
         if (status == AIPSTACK_CHKSUM_OK) status = check_hip(hipEventRecord(s.done, s.stream));
@@ -365,6 +377,8 @@ extern "C" int aipstack_chksum_engine_create(int device, uint64_t chunk_bytes, i
     e->chunk_packets = chunk_bytes / 64 + 1;
     // experiments: AIPSTACK_ENGINE_SLOT_ROWS=0 copies whole slots (one 1-D span per piece)
     if (const char *v = std::getenv("AIPSTACK_ENGINE_SLOT_ROWS")) e->slot_rows = std::atoi(v) != 0;
+    if (const char *v = std::getenv("AIPSTACK_ENGINE_ZERO_COPY_MAX"))
+        e->zero_copy_max = std::strtoull(v, nullptr, 10);
     e->slots.resize((size_t)nstreams);
     int st = AIPSTACK_CHKSUM_OK;
     for (Slot &s : e->slots) {
@@ -376,6 +390,10 @@ extern "C" int aipstack_chksum_engine_create(int device, uint64_t chunk_bytes, i
         if (st == AIPSTACK_CHKSUM_OK) st = check_hip(hipHostMalloc(reinterpret_cast<void **>(&s.h_off), (e->chunk_packets + 1) * 8, hipHostMallocDefault));
         if (st == AIPSTACK_CHKSUM_OK) st = check_hip(hipHostMalloc(reinterpret_cast<void **>(&s.h_out), e->chunk_packets * 8, hipHostMallocDefault));
         if (st == AIPSTACK_CHKSUM_OK) st = check_hip(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+        if (st == AIPSTACK_CHKSUM_OK)
+            st = check_hip(hipHostGetDevicePointer(reinterpret_cast<void **>(&s.dh_off), s.h_off, 0));
+        if (st == AIPSTACK_CHKSUM_OK)
+            st = check_hip(hipHostGetDevicePointer(reinterpret_cast<void **>(&s.dh_out), s.h_out, 0));
     }
     if (st != AIPSTACK_CHKSUM_OK) {
         release(e);
@@ -464,7 +482,7 @@ extern "C" int aipstack_chksum_engine_submit_strided(aipstack_chksum_engine *e,
         sp->bytes = (*i1 - i0 - 1) * stride + len;
     };
     auto launch = [&](Slot &s, uint64_t i0, uint64_t i1) {
-        return aipstack_chksum_batch_strided(s.d_bytes, stride, len, i1 - i0, s.d_out, flags,
+        return aipstack_chksum_batch_strided(s.d_bytes, stride, len, i1 - i0, s.k_out, flags,
                                              s.stream);
     };
     std::lock_guard<std::mutex> lock(e->mu);
@@ -497,9 +515,11 @@ int submit_csr_like(aipstack_chksum_engine *e, const void *h_base, const uint64_
         const uint64_t cnt = i1 - i0;
         const uint64_t b0 = h_offsets[i0];
         for (uint64_t i = 0; i <= cnt; ++i) s.h_off[i] = h_offsets[i0 + i] - b0;  // rebased
-        int st = check_hip(hipMemcpyAsync(s.d_off, s.h_off, (cnt + 1) * 8, hipMemcpyHostToDevice,
-                                          s.stream));
-        if (st != AIPSTACK_CHKSUM_OK) return st;
+        if (!s.zero_copy) {
+            const int st = check_hip(hipMemcpyAsync(s.d_off, s.h_off, (cnt + 1) * 8,
+                                                    hipMemcpyHostToDevice, s.stream));
+            if (st != AIPSTACK_CHKSUM_OK) return st;
+        }
         return kernel(s, i0, cnt);
     };
     std::lock_guard<std::mutex> lock(e->mu);
@@ -514,8 +534,8 @@ extern "C" int aipstack_chksum_engine_submit_rx_verify(aipstack_chksum_engine *e
     if (!e || !h_base || !h_offsets || !h_verdicts || !ticket) return AIPSTACK_CHKSUM_EINVAL;
     return submit_csr_like(e, h_base, h_offsets, n, h_verdicts, 1,
                            [&](Slot &s, uint64_t, uint64_t cnt) {
-                               return aipstack_chksum_rx_verify(s.d_bytes, s.d_off, cnt,
-                                                                reinterpret_cast<uint8_t *>(s.d_out),
+                               return aipstack_chksum_rx_verify(s.d_bytes, s.k_off, cnt,
+                                                                reinterpret_cast<uint8_t *>(s.k_out),
                                                                 s.stream);
                            },
                            ticket);
@@ -533,7 +553,7 @@ extern "C" int aipstack_chksum_engine_submit_tx_fill(aipstack_chksum_engine *e, 
                                s.tx_stride = 0;
                                s.tx_status = h_status + i0;
                                return aipstack_chksum_tx_fill_records(
-                                   s.d_bytes, s.d_off, cnt, reinterpret_cast<uint64_t *>(s.d_out),
+                                   s.d_bytes, s.k_off, cnt, reinterpret_cast<uint64_t *>(s.k_out),
                                    s.stream);
                            },
                            ticket);
@@ -574,7 +594,7 @@ extern "C" int aipstack_chksum_engine_submit_csr(aipstack_chksum_engine *e, cons
     if (!e || !h_base || !h_offsets || !h_out || !ticket) return AIPSTACK_CHKSUM_EINVAL;
     return submit_csr_like(e, h_base, h_offsets, n, h_out, 2,
                            [&](Slot &s, uint64_t, uint64_t cnt) {
-                               return aipstack_chksum_batch_csr(s.d_bytes, s.d_off, cnt, s.d_out,
+                               return aipstack_chksum_batch_csr(s.d_bytes, s.k_off, cnt, s.k_out,
                                                                 flags, s.stream);
                            },
                            ticket);
@@ -610,10 +630,12 @@ int submit_slotted_like(aipstack_chksum_engine *e, const void *h_base, uint64_t 
     auto launch = [&](Slot &s, uint64_t i0, uint64_t i1) {
         const uint64_t cnt = i1 - i0;
         std::memcpy(s.h_off, h_len + i0, cnt * sizeof(uint32_t));  // lengths -> pinned staging
-        int st = check_hip(hipMemcpyAsync(s.d_off, s.h_off, cnt * sizeof(uint32_t),
-                                          hipMemcpyHostToDevice, s.stream));
-        if (st != AIPSTACK_CHKSUM_OK) return st;
-        return kernel(s, i0, cnt, reinterpret_cast<const uint32_t *>(s.d_off));
+        if (!s.zero_copy) {
+            const int st = check_hip(hipMemcpyAsync(s.d_off, s.h_off, cnt * sizeof(uint32_t),
+                                                    hipMemcpyHostToDevice, s.stream));
+            if (st != AIPSTACK_CHKSUM_OK) return st;
+        }
+        return kernel(s, i0, cnt, reinterpret_cast<const uint32_t *>(s.k_off));
     };
     std::lock_guard<std::mutex> lock(e->mu);
     return enqueue(e, n, h_out, elem, chunker, launch, ticket);
@@ -628,7 +650,7 @@ extern "C" int aipstack_chksum_engine_submit_slotted(aipstack_chksum_engine *e, 
     return submit_slotted_like(e, h_base, slot_stride, h_len, n, h_out, 2,
                                [&](Slot &s, uint64_t, uint64_t cnt, const uint32_t *d_len) {
                                    return aipstack_chksum_batch_slotted(s.d_bytes, slot_stride,
-                                                                        d_len, cnt, s.d_out,
+                                                                        d_len, cnt, s.k_out,
                                                                         flags, s.stream);
                                },
                                ticket);
@@ -642,7 +664,7 @@ extern "C" int aipstack_chksum_engine_submit_rx_verify_slotted(
                                [&](Slot &s, uint64_t, uint64_t cnt, const uint32_t *d_len) {
                                    return aipstack_chksum_rx_verify_slotted(
                                        s.d_bytes, slot_stride, d_len, cnt,
-                                       reinterpret_cast<uint8_t *>(s.d_out), s.stream);
+                                       reinterpret_cast<uint8_t *>(s.k_out), s.stream);
                                },
                                ticket);
 }
@@ -660,7 +682,7 @@ extern "C" int aipstack_chksum_engine_submit_tx_fill_slotted(
                                    s.tx_status = h_status + i0;
                                    return aipstack_chksum_tx_fill_records_slotted(
                                        s.d_bytes, slot_stride, d_len, cnt,
-                                       reinterpret_cast<uint64_t *>(s.d_out), s.stream);
+                                       reinterpret_cast<uint64_t *>(s.k_out), s.stream);
                                },
                                ticket);
 }

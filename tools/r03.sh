@@ -11,6 +11,7 @@
 #   e2ethreads  host engine Tx: apply/staging threads, piece size, streams
 #   tx2k    send ring: device in-place slotted Tx fill (bench + rocprof) and e2e
 #   ringloop  the engine as a TAP receive loop from C++, per batch size
+#   zc      engine zero-copy metadata for small pieces: engine tests + receive loop
 #   ring    e2e receive rings (RX2K / C2K): 2-D copies of the slots' used prefix vs whole slots
 #   slots   pytest -m gpu; ring-slot lines RX2K / C2K (+ their slot-read ceilings) and A2K;
 #           a U/P sweep of the slotted checksum; e2e through an engine group of 1/2/4
@@ -188,6 +189,18 @@ ringloop)
   # batches in flight, per batch size B
   timeout -k 10 400 tools/build/ring_loop 64 256 1024 4096 16384 65536 > "$out/ring_loop.jsonl" \
       2> "$out/ring_loop.err"
+  ;;
+zc)
+  # engine pieces of at most AIPSTACK_ENGINE_ZERO_COPY_MAX packets: offsets / lengths read and
+  # results written by the kernel in the pinned staging (no metadata copies). The engine
+  # tests with every piece zero-copy, then the receive loop without / with it, alternating
+  AIPSTACK_ENGINE_ZERO_COPY_MAX=100000000 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q \
+      -k "engine" --timeout 120 --timeout-method thread > "$out/pytest_engine_zc.log" 2>&1
+  for i in 1 2; do
+    timeout -k 10 400 tools/build/ring_loop 64 256 1024 4096 16384 >> "$out/ring_loop.jsonl" 2>> "$out/err"
+    AIPSTACK_ENGINE_ZERO_COPY_MAX=65536 timeout -k 10 400 tools/build/ring_loop 64 256 1024 4096 16384 \
+        >> "$out/ring_loop_zc.jsonl" 2>> "$out/err"
+  done
   ;;
 *)
   echo "unknown mode $mode" >&2; exit 2 ;;
