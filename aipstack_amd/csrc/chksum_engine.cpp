@@ -61,6 +61,8 @@ struct Slot {
     // staging itself through dh_off / dh_out (no copies: fewer DMA ops per small batch)
     uint64_t *k_off = nullptr;
     uint16_t *k_out = nullptr;
+    void *k_bytes = nullptr;  // the packet bytes as the kernel reads them: d_bytes, or the
+                              // caller's registered memory itself (zero-copy pieces)
     bool zero_copy = false;
     hipEvent_t done = nullptr;
     bool busy = false;
@@ -81,6 +83,7 @@ struct Region {
     const char *p;
     uint64_t bytes;
     bool owned = true;  // registered by this engine (unregistered by it); else adopted
+    const char *dev = nullptr;  // the region as the device addresses it (mapped), or null
 };
 
 }  // namespace
@@ -91,6 +94,7 @@ struct aipstack_chksum_engine {
     uint64_t chunk_packets = 0;
     bool slot_rows = true;  // ring slots: copy each slot's used prefix only (2-D copy)
     uint64_t zero_copy_max = 0;  // pieces of at most this many packets skip the metadata copies
+    bool zero_copy_bytes = false;  // ... and, from registered memory, the packet-byte copy too
     std::vector<Slot> slots;
     std::vector<Region> registered;
     size_t next_slot = 0;      // round robin over the slots, across batches
@@ -104,11 +108,21 @@ struct aipstack_chksum_engine {
 
 namespace {
 
-bool is_registered(const aipstack_chksum_engine *e, const void *p, uint64_t bytes) {
+const Region *find_registered(const aipstack_chksum_engine *e, const void *p, uint64_t bytes) {
     const char *c = static_cast<const char *>(p);
     for (const Region &r : e->registered)
-        if (c >= r.p && c + bytes <= r.p + r.bytes) return true;
-    return false;
+        if (c >= r.p && c + bytes <= r.p + r.bytes) return &r;
+    return nullptr;
+}
+
+// The device address of a page-locked host region (null if the runtime gives none).
+const char *mapped_address(const void *host_ptr) {
+    void *d = nullptr;
+    if (hipHostGetDevicePointer(&d, const_cast<void *>(host_ptr), 0) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    return static_cast<const char *>(d);
 }
 
 #ifdef AIPSTACK_ENGINE_FAULT_INJECTION
@@ -296,18 +310,24 @@ int enqueue(aipstack_chksum_engine *e, uint64_t n, void *h_out, uint32_t elem, C
         s.zero_copy = cnt <= e->zero_copy_max;
         s.k_off = s.zero_copy ? s.dh_off : s.d_off;
         s.k_out = s.zero_copy ? s.dh_out : s.d_out;
-        const bool registered = sp.bytes && is_registered(e, sp.src, sp.bytes);
+        const Region *reg = sp.bytes ? find_registered(e, sp.src, sp.bytes) : nullptr;
+        const bool registered = reg != nullptr;
         const bool rows = registered && sp.width != 0 && sp.width < sp.pitch;
         const void *h_src = sp.src;
-        if (sp.bytes && !registered) {  // pageable: CPU copy into pinned staging
+        s.k_bytes = s.d_bytes;
+        if (s.zero_copy && e->zero_copy_bytes && registered && reg->dev) {
+            // the kernel reads the caller's page-locked bytes over the link itself
+            s.k_bytes = const_cast<char *>(reg->dev + (sp.src - reg->p));
+        } else if (sp.bytes && !registered) {  // pageable: CPU copy into pinned staging
             stage_copy(s.h_stage, sp.src, sp.bytes);
             h_src = s.h_stage;
         }
-        if (sp.bytes && rows)
+        const bool copy = sp.bytes && s.k_bytes == s.d_bytes;
+        if (copy && rows)
             status = check_hip(hipMemcpy2DAsync(s.d_bytes, sp.pitch, h_src, sp.pitch, sp.width,
                                                 sp.bytes / sp.pitch, hipMemcpyHostToDevice,
                                                 s.stream));
-        else if (sp.bytes)
+        else if (copy)
             status = check_hip(hipMemcpyAsync(s.d_bytes, h_src, sp.bytes, hipMemcpyHostToDevice,
                                               s.stream));
         s.seq = ++e->pieces;
@@ -379,6 +399,8 @@ extern "C" int aipstack_chksum_engine_create(int device, uint64_t chunk_bytes, i
     if (const char *v = std::getenv("AIPSTACK_ENGINE_SLOT_ROWS")) e->slot_rows = std::atoi(v) != 0;
     if (const char *v = std::getenv("AIPSTACK_ENGINE_ZERO_COPY_MAX"))
         e->zero_copy_max = std::strtoull(v, nullptr, 10);
+    if (const char *v = std::getenv("AIPSTACK_ENGINE_ZERO_COPY_BYTES"))
+        e->zero_copy_bytes = std::atoi(v) != 0;
     e->slots.resize((size_t)nstreams);
     int st = AIPSTACK_CHKSUM_OK;
     for (Slot &s : e->slots) {
@@ -421,7 +443,8 @@ namespace aipstack_amd {
 // first completes the pieces in flight (they may still read it).
 void engine_adopt_region(aipstack_chksum_engine *e, const void *p, uint64_t bytes) {
     std::lock_guard<std::mutex> lock(e->mu);
-    e->registered.push_back(Region{static_cast<const char *>(p), bytes, false});
+    DeviceGuard dg(e->device);
+    e->registered.push_back(Region{static_cast<const char *>(p), bytes, false, mapped_address(p)});
 }
 void engine_drop_region(aipstack_chksum_engine *e, const void *p) {
     std::lock_guard<std::mutex> lock(e->mu);
@@ -444,7 +467,8 @@ extern "C" int aipstack_chksum_engine_register(aipstack_chksum_engine *e, void *
     if (!dg.ok) return AIPSTACK_CHKSUM_ENODEV;
     const int st = check_hip(hipHostRegister(host_ptr, bytes, hipHostRegisterDefault));
     if (st == AIPSTACK_CHKSUM_OK)
-        e->registered.push_back(Region{static_cast<char *>(host_ptr), bytes, true});
+        e->registered.push_back(Region{static_cast<char *>(host_ptr), bytes, true,
+                                       mapped_address(host_ptr)});
     return st;
 }
 
@@ -482,7 +506,7 @@ extern "C" int aipstack_chksum_engine_submit_strided(aipstack_chksum_engine *e,
         sp->bytes = (*i1 - i0 - 1) * stride + len;
     };
     auto launch = [&](Slot &s, uint64_t i0, uint64_t i1) {
-        return aipstack_chksum_batch_strided(s.d_bytes, stride, len, i1 - i0, s.k_out, flags,
+        return aipstack_chksum_batch_strided(s.k_bytes, stride, len, i1 - i0, s.k_out, flags,
                                              s.stream);
     };
     std::lock_guard<std::mutex> lock(e->mu);
@@ -534,7 +558,7 @@ extern "C" int aipstack_chksum_engine_submit_rx_verify(aipstack_chksum_engine *e
     if (!e || !h_base || !h_offsets || !h_verdicts || !ticket) return AIPSTACK_CHKSUM_EINVAL;
     return submit_csr_like(e, h_base, h_offsets, n, h_verdicts, 1,
                            [&](Slot &s, uint64_t, uint64_t cnt) {
-                               return aipstack_chksum_rx_verify(s.d_bytes, s.k_off, cnt,
+                               return aipstack_chksum_rx_verify(s.k_bytes, s.k_off, cnt,
                                                                 reinterpret_cast<uint8_t *>(s.k_out),
                                                                 s.stream);
                            },
@@ -553,7 +577,7 @@ extern "C" int aipstack_chksum_engine_submit_tx_fill(aipstack_chksum_engine *e, 
                                s.tx_stride = 0;
                                s.tx_status = h_status + i0;
                                return aipstack_chksum_tx_fill_records(
-                                   s.d_bytes, s.k_off, cnt, reinterpret_cast<uint64_t *>(s.k_out),
+                                   s.k_bytes, s.k_off, cnt, reinterpret_cast<uint64_t *>(s.k_out),
                                    s.stream);
                            },
                            ticket);
@@ -594,7 +618,7 @@ extern "C" int aipstack_chksum_engine_submit_csr(aipstack_chksum_engine *e, cons
     if (!e || !h_base || !h_offsets || !h_out || !ticket) return AIPSTACK_CHKSUM_EINVAL;
     return submit_csr_like(e, h_base, h_offsets, n, h_out, 2,
                            [&](Slot &s, uint64_t, uint64_t cnt) {
-                               return aipstack_chksum_batch_csr(s.d_bytes, s.k_off, cnt, s.k_out,
+                               return aipstack_chksum_batch_csr(s.k_bytes, s.k_off, cnt, s.k_out,
                                                                 flags, s.stream);
                            },
                            ticket);
@@ -649,7 +673,7 @@ extern "C" int aipstack_chksum_engine_submit_slotted(aipstack_chksum_engine *e, 
     if (!e || !h_base || !h_len || !h_out || !ticket) return AIPSTACK_CHKSUM_EINVAL;
     return submit_slotted_like(e, h_base, slot_stride, h_len, n, h_out, 2,
                                [&](Slot &s, uint64_t, uint64_t cnt, const uint32_t *d_len) {
-                                   return aipstack_chksum_batch_slotted(s.d_bytes, slot_stride,
+                                   return aipstack_chksum_batch_slotted(s.k_bytes, slot_stride,
                                                                         d_len, cnt, s.k_out,
                                                                         flags, s.stream);
                                },
@@ -663,7 +687,7 @@ extern "C" int aipstack_chksum_engine_submit_rx_verify_slotted(
     return submit_slotted_like(e, h_base, slot_stride, h_len, n, h_verdicts, 1,
                                [&](Slot &s, uint64_t, uint64_t cnt, const uint32_t *d_len) {
                                    return aipstack_chksum_rx_verify_slotted(
-                                       s.d_bytes, slot_stride, d_len, cnt,
+                                       s.k_bytes, slot_stride, d_len, cnt,
                                        reinterpret_cast<uint8_t *>(s.k_out), s.stream);
                                },
                                ticket);
@@ -681,7 +705,7 @@ extern "C" int aipstack_chksum_engine_submit_tx_fill_slotted(
                                    s.tx_stride = slot_stride;
                                    s.tx_status = h_status + i0;
                                    return aipstack_chksum_tx_fill_records_slotted(
-                                       s.d_bytes, slot_stride, d_len, cnt,
+                                       s.k_bytes, slot_stride, d_len, cnt,
                                        reinterpret_cast<uint64_t *>(s.k_out), s.stream);
                                },
                                ticket);

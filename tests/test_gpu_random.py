@@ -16,7 +16,7 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 DEV = "cuda"
-SCENARIOS = 40
+SCENARIOS = 100
 
 
 def _d(a):

@@ -192,14 +192,21 @@ ringloop)
   ;;
 zc)
   # engine pieces of at most AIPSTACK_ENGINE_ZERO_COPY_MAX packets: offsets / lengths read and
-  # results written by the kernel in the pinned staging (no metadata copies). The engine
-  # tests with every piece zero-copy, then the receive loop without / with it, alternating
+  # results written by the kernel in the pinned staging (no metadata copies); with
+  # AIPSTACK_ENGINE_ZERO_COPY_BYTES=1 the kernel also reads registered packet bytes in place.
+  # The engine tests with every piece zero-copy (both levels), then the receive loop in the
+  # three modes, alternating
   AIPSTACK_ENGINE_ZERO_COPY_MAX=100000000 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q \
       -k "engine" --timeout 120 --timeout-method thread > "$out/pytest_engine_zc.log" 2>&1
+  AIPSTACK_ENGINE_ZERO_COPY_MAX=100000000 AIPSTACK_ENGINE_ZERO_COPY_BYTES=1 timeout -k 10 600 \
+      python -u -m pytest tests -m gpu -x -q -k "engine" --timeout 120 --timeout-method thread \
+      > "$out/pytest_engine_zcb.log" 2>&1
   for i in 1 2; do
     timeout -k 10 400 tools/build/ring_loop 64 256 1024 4096 16384 >> "$out/ring_loop.jsonl" 2>> "$out/err"
     AIPSTACK_ENGINE_ZERO_COPY_MAX=65536 timeout -k 10 400 tools/build/ring_loop 64 256 1024 4096 16384 \
         >> "$out/ring_loop_zc.jsonl" 2>> "$out/err"
+    AIPSTACK_ENGINE_ZERO_COPY_MAX=65536 AIPSTACK_ENGINE_ZERO_COPY_BYTES=1 timeout -k 10 400 \
+        tools/build/ring_loop 64 256 1024 4096 16384 >> "$out/ring_loop_zcb.jsonl" 2>> "$out/err"
   done
   ;;
 *)
