@@ -12,6 +12,7 @@
 #   tx2k    send ring: device in-place slotted Tx fill (bench + rocprof) and e2e
 #   ringloop  the engine as a TAP receive loop from C++, per batch size
 #   zc      engine zero-copy metadata for small pieces: engine tests + receive loop
+#   zc2     e2e from registered memory: DMA vs zero-copy pieces, every config
 #   ring    e2e receive rings (RX2K / C2K): 2-D copies of the slots' used prefix vs whole slots
 #   slots   pytest -m gpu; ring-slot lines RX2K / C2K (+ their slot-read ceilings) and A2K;
 #           a U/P sweep of the slotted checksum; e2e through an engine group of 1/2/4
@@ -207,6 +208,17 @@ zc)
         >> "$out/ring_loop_zc.jsonl" 2>> "$out/err"
     AIPSTACK_ENGINE_ZERO_COPY_MAX=65536 AIPSTACK_ENGINE_ZERO_COPY_BYTES=1 timeout -k 10 400 \
         tools/build/ring_loop 64 256 1024 4096 16384 >> "$out/ring_loop_zcb.jsonl" 2>> "$out/err"
+  done
+  ;;
+zc2)
+  # whole batches from registered memory: DMA (default) vs every piece zero-copy (the kernel
+  # reads the caller's bytes over the link), alternating
+  for i in 1 2; do
+    for c in A C RX TX RX2K TX2K C2K; do
+      bench e2e_dma --e2e --config $c --steps 5 --warmup 1
+      AIPSTACK_ENGINE_ZERO_COPY_MAX=100000000 AIPSTACK_ENGINE_ZERO_COPY_BYTES=1 \
+          bench e2e_zcb --e2e --config $c --steps 5 --warmup 1
+    done
   done
   ;;
 *)
