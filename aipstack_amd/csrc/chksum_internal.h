@@ -54,6 +54,10 @@ int tuning_waves_per_cu();
 // Stream-mode windows a wave issues together (tunable "stream": 2, 4, 8; 0 = stream mode
 // off), with the default of the given kernel family when the tunable is automatic.
 int tuning_stream_windows(int family_default);
+// Host engine: kernels read registered input in place (1) or the engine DMAs it (0); pieces of
+// at most tuning_engine_zero_copy_small() packets keep offsets / results in pinned staging.
+int tuning_engine_zero_copy();
+int tuning_engine_zero_copy_small();
 
 }  // namespace aipstack_amd
 

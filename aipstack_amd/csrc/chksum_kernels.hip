@@ -308,6 +308,10 @@ struct Tuning {
                                           // batch size (pick_shape)
     std::atomic<int> tx_gather{-1};       // Tx header segments from the stream: 0 never,
                                           // 1 always, else for the records-only read pass
+    // host engine (read when an engine is created, chksum_engine.cpp):
+    std::atomic<int> engine_zero_copy{1};         // kernels read registered input in place
+    std::atomic<int> engine_zero_copy_small{65536};  // pieces of at most this many packets
+                                                     // keep offsets / results in pinned staging
 
     Tuning() {
         auto env = [](const char *k, std::atomic<int> &v) {
@@ -322,6 +326,8 @@ struct Tuning {
         env("AIPSTACK_CHKSUM_STREAM", stream);
         env("AIPSTACK_CHKSUM_CHUNK_PACKETS", chunk_packets);
         env("AIPSTACK_CHKSUM_TX_GATHER", tx_gather);
+        env("AIPSTACK_ENGINE_ZERO_COPY", engine_zero_copy);
+        env("AIPSTACK_ENGINE_ZERO_COPY_SMALL", engine_zero_copy_small);
 
     }
 };
@@ -528,6 +534,11 @@ int tuning_waves_per_cu() {
     return tuning().waves_per_cu.load(std::memory_order_relaxed);
 }
 
+int tuning_engine_zero_copy() { return tuning().engine_zero_copy.load(std::memory_order_relaxed); }
+int tuning_engine_zero_copy_small() {
+    return tuning().engine_zero_copy_small.load(std::memory_order_relaxed);
+}
+
 int tuning_stream_windows(int family_default) {
     const int t = tuning().stream.load(std::memory_order_relaxed);
     if (t < 0) return 0;
@@ -618,6 +629,8 @@ extern "C" int aipstack_chksum_tune(const char *key, int value) {
     else if (!std::strcmp(key, "stream")) t.stream = value;
     else if (!std::strcmp(key, "chunk_packets")) t.chunk_packets = value;
     else if (!std::strcmp(key, "tx_gather")) t.tx_gather = value;
+    else if (!std::strcmp(key, "engine_zero_copy")) t.engine_zero_copy = value;
+    else if (!std::strcmp(key, "engine_zero_copy_small")) t.engine_zero_copy_small = value;
     else return AIPSTACK_CHKSUM_EINVAL;
     return AIPSTACK_CHKSUM_OK;
 }

@@ -200,8 +200,11 @@ int aipstack_chksum_tx_fill_records_slotted(const void *d_base, uint64_t slot_st
  * HOST memory and writes the results to HOST memory, pipelining H2D copies, kernels and
  * D2H copies over `nstreams` HIP streams in chunks of at most `chunk_bytes` (0 = 64 MiB)
  * of whole packets. Host buffers registered with aipstack_chksum_engine_register()
- * (page-locked once, e.g. a receive ring) are DMA'd directly; other host memory is first
- * copied into the engine's pinned staging. The host_* calls are synchronous; the submit_*
+ * (page-locked once, e.g. a receive ring) are read by the kernels where they lie, over the
+ * link (only the bytes the packets cover cross it: for ring slots not the slack); with
+ * aipstack_chksum_tune("engine_zero_copy", 0) before the engine is created they are DMA'd
+ * to the device first instead. Other host memory is first copied into the engine's pinned
+ * staging. The host_* calls are synchronous; the submit_*
  * calls enqueue a batch and return a ticket at once, so the caller can fill its next batch
  * (e.g. read() frames into its ring) while the GPU works; _poll / _wait complete it. Calls
  * on one engine from several threads are serialised, except that _wait waits for the GPU

@@ -37,6 +37,20 @@ def _np(t):
     return t.cpu().numpy()
 
 
+class _engine_copy_mode:
+    """Engines created inside read registered input in place (zero_copy=1, the default) or
+    DMA it first (0: the 2-D slot copies, whole spans); restored on exit."""
+
+    def __init__(self, zero_copy):
+        self.zc = int(zero_copy)
+
+    def __enter__(self):
+        assert A._lib.load().aipstack_chksum_tune(b"engine_zero_copy", self.zc) == 0
+
+    def __exit__(self, *exc):
+        A._lib.load().aipstack_chksum_tune(b"engine_zero_copy", 1)
+
+
 def test_native_library_loaded_in_process():
     maps = open("/proc/self/maps").read()
     assert os.path.join("aipstack_amd", "lib", "libaipstack_chksum.so") in maps
@@ -441,11 +455,12 @@ def test_bench_e2e_tx_two_ranks_one_gpu():
 
 # ---- host-memory streaming engine ------------------------------------
 
+@pytest.mark.parametrize("zero_copy", [1, 0])
 @pytest.mark.parametrize("register", [False, True])
-def test_engine_host_strided(oracle, register):
+def test_engine_host_strided(oracle, register, zero_copy):
     n, plen = 300000, 1500
     host = synth.random_bytes(21, n * plen + 3)
-    with A.ChksumEngine(0, chunk_bytes=16 << 20, nstreams=3) as eng:
+    with _engine_copy_mode(zero_copy), A.ChksumEngine(0, chunk_bytes=16 << 20, nstreams=3) as eng:
         if register:
             eng.register(host)
         got = eng.strided(host[3:], plen, plen, n) if not register else \
@@ -456,10 +471,11 @@ def test_engine_host_strided(oracle, register):
         assert np.array_equal(fin, oracle.batch_strided(host, 1501, 1499, 1000, final=True))
 
 
+@pytest.mark.parametrize("zero_copy", [1, 0])
 @pytest.mark.parametrize("register", [False, True])
-def test_engine_host_csr(oracle, register):
+def test_engine_host_csr(oracle, register, zero_copy):
     buf, off = synth.mixed_batch(400000)
-    with A.ChksumEngine(0, chunk_bytes=8 << 20, nstreams=2) as eng:
+    with _engine_copy_mode(zero_copy), A.ChksumEngine(0, chunk_bytes=8 << 20, nstreams=2) as eng:
         if register:
             eng.register(buf)
         got = eng.csr(buf, off)
@@ -522,15 +538,16 @@ def test_engine_async_frames_in_flight(oracle):
         assert np.array_equal(ob, oracle.batch_csr(b_buf, b_off))
 
 
+@pytest.mark.parametrize("zero_copy", [1, 0])
 @pytest.mark.parametrize("register", [False, True])
-def test_engine_host_rx_verify(oracle, register):
+def test_engine_host_rx_verify(oracle, register, zero_copy):
     """Raw frames in host memory (the TAP receive path batched): verdicts as the device
     batch and the frame oracle give, over several engine chunks; also through submit/wait."""
     buf, off = synth.frames_host(60000, seed=41)
     oracle.tx_fill_batch(buf, off)
     _corrupt(buf, off, 0.2, 3)
     want = oracle.rx_verify_batch(buf, off)
-    with A.ChksumEngine(0, chunk_bytes=4 << 20, nstreams=3) as eng:
+    with _engine_copy_mode(zero_copy), A.ChksumEngine(0, chunk_bytes=4 << 20, nstreams=3) as eng:
         if register:
             eng.register(buf)
         got = eng.rx_verify(buf, off)
@@ -542,8 +559,9 @@ def test_engine_host_rx_verify(oracle, register):
             eng.rx_verify(buf, np.array([0, 100, 50], dtype=np.uint64))
 
 
+@pytest.mark.parametrize("zero_copy", [1, 0])
 @pytest.mark.parametrize("register", [False, True])
-def test_engine_host_tx_fill(oracle, register):
+def test_engine_host_tx_fill(oracle, register, zero_copy):
     """Raw frames in host memory (the TAP send path batched), filled IN PLACE: frames and
     statuses byte-identical to the frame oracle's, over several engine chunks; also through
     submit/wait, on frames whose fields hold garbage."""
@@ -553,7 +571,7 @@ def test_engine_host_tx_fill(oracle, register):
     want = buf.copy()
     want_st = oracle.tx_fill_batch(want, off)
     assert len(set(want_st.tolist())) > 1
-    with A.ChksumEngine(0, chunk_bytes=4 << 20, nstreams=3) as eng:
+    with _engine_copy_mode(zero_copy), A.ChksumEngine(0, chunk_bytes=4 << 20, nstreams=3) as eng:
         if register:
             eng.register(buf)
         st = eng.tx_fill(buf, off)
@@ -1107,11 +1125,13 @@ def test_slotted_length_over_slot_is_clamped_and_reported(oracle):
     assert A.contract_violations(0, clear=True) == A.VIOLATION_PACKET_LEN
 
 
+@pytest.mark.parametrize("zero_copy", [1, 0])
 @pytest.mark.parametrize("register", [False, True])
-def test_engine_slotted(oracle, register):
+def test_engine_slotted(oracle, register, zero_copy):
     """The engine's ring-slot calls from host memory: checksums, Rx verify, Tx fill in place
-    (slack bytes untouched), several pieces per batch; bad lengths rejected up front."""
-    with A.ChksumEngine(0, chunk_bytes=4 << 20, nstreams=3) as eng:
+    (slack bytes untouched), several pieces per batch; bad lengths rejected up front. Both
+    copy modes of registered input (read in place, or DMA'd first)."""
+    with _engine_copy_mode(zero_copy), A.ChksumEngine(0, chunk_bytes=4 << 20, nstreams=3) as eng:
         buf, off = synth.mixed_batch(40000)
         ring, lens = synth.to_slots(buf, off, 2048)
         if register:
@@ -1136,15 +1156,16 @@ def test_engine_slotted(oracle, register):
         assert np.array_equal(out, oracle.batch_slotted(ring, 2048, lens))
 
 
+@pytest.mark.parametrize("zero_copy", [0, 1])
 @pytest.mark.parametrize("register", [False, True])
-def test_engine_slotted_moves_only_used_slot_prefix(oracle, register):
+def test_engine_slotted_moves_only_used_slot_prefix(oracle, register, zero_copy):
     """Ring-slot pieces cross PCIe as 2-D copies of each slot's first bytes (the piece's longest
     frame, rounded up to 64): a batch of long frames leaves its bytes in the device staging,
     then batches of short frames (<= 60 / <= 100 B: 64- and 128-byte rows, below the
     112-byte header window) run on the same slots -- the bytes past each row are stale, and
     the results must still be the oracle's."""
     stride = 2048
-    with A.ChksumEngine(0, chunk_bytes=1 << 20, nstreams=2) as eng:
+    with _engine_copy_mode(zero_copy), A.ChksumEngine(0, chunk_bytes=1 << 20, nstreams=2) as eng:
         # (max payload, seed, length cap): capped lengths cut frames short in their slots
         for maxp, seed, cap in ((1460, 3, None), (6, 4, 60), (46, 5, 100), (1460, 6, None),
                                 (0, 7, 64), (20, 8, None)):
@@ -1169,8 +1190,9 @@ def test_engine_slotted_moves_only_used_slot_prefix(oracle, register):
                 eng.unregister(ring)
 
 
+@pytest.mark.parametrize("zero_copy", [1, 0])
 @pytest.mark.parametrize("register", [False, True])
-def test_engine_ring_receive_loop(oracle, register):
+def test_engine_ring_receive_loop(oracle, register, zero_copy):
     """A TAP-style receive/send ring driven through the engine's tickets
     (tap/linux/TapDeviceLinux.cpp:156-178: one frame per slot, its length beside it): 8
     regions of 2,048 slots x 2,048 B, several batches in flight; a region is refilled only
@@ -1183,7 +1205,7 @@ def test_engine_ring_receive_loop(oracle, register):
     filled = raw.copy()
     oracle.tx_fill_batch(filled, soff)  # what a sender put on the wire
     rng = np.random.default_rng(17)
-    with A.ChksumEngine(0, chunk_bytes=2 << 20, nstreams=3) as eng:
+    with _engine_copy_mode(zero_copy), A.ChksumEngine(0, chunk_bytes=2 << 20, nstreams=3) as eng:
         if register:
             eng.register(ring)
         pending = [None] * regions  # region -> (ticket, kind, out, want)

@@ -11,7 +11,8 @@
 #   e2ethreads  host engine Tx: apply/staging threads, piece size, streams
 #   tx2k    send ring: device in-place slotted Tx fill (bench + rocprof) and e2e
 #   ringloop  the engine as a TAP receive loop from C++, per batch size
-#   zc      engine zero-copy metadata for small pieces: engine tests + receive loop
+#   zc      engine zero-copy (metadata / packet bytes read in place) vs DMA: engine tests +
+#           receive loop (round-3 experiment; zero copy is the default since)
 #   zc2     e2e from registered memory: DMA vs zero-copy pieces, every config
 #   ring    e2e receive rings (RX2K / C2K): 2-D copies of the slots' used prefix vs whole slots
 #   slots   pytest -m gpu; ring-slot lines RX2K / C2K (+ their slot-read ceilings) and A2K;
@@ -192,21 +193,22 @@ ringloop)
       2> "$out/ring_loop.err"
   ;;
 zc)
-  # engine pieces of at most AIPSTACK_ENGINE_ZERO_COPY_MAX packets: offsets / lengths read and
+  # engine pieces of at most AIPSTACK_ENGINE_ZERO_COPY_SMALL packets: offsets / lengths read and
   # results written by the kernel in the pinned staging (no metadata copies); with
-  # AIPSTACK_ENGINE_ZERO_COPY_BYTES=1 the kernel also reads registered packet bytes in place.
+  # AIPSTACK_ENGINE_ZERO_COPY=1 the kernel also reads registered packet bytes in place.
   # The engine tests with every piece zero-copy (both levels), then the receive loop in the
   # three modes, alternating
-  AIPSTACK_ENGINE_ZERO_COPY_MAX=100000000 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q \
+  AIPSTACK_ENGINE_ZERO_COPY=0 AIPSTACK_ENGINE_ZERO_COPY_SMALL=100000000 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q \
       -k "engine" --timeout 120 --timeout-method thread > "$out/pytest_engine_zc.log" 2>&1
-  AIPSTACK_ENGINE_ZERO_COPY_MAX=100000000 AIPSTACK_ENGINE_ZERO_COPY_BYTES=1 timeout -k 10 600 \
+  AIPSTACK_ENGINE_ZERO_COPY=1 AIPSTACK_ENGINE_ZERO_COPY_SMALL=100000000 timeout -k 10 600 \
       python -u -m pytest tests -m gpu -x -q -k "engine" --timeout 120 --timeout-method thread \
       > "$out/pytest_engine_zcb.log" 2>&1
   for i in 1 2; do
-    timeout -k 10 400 tools/build/ring_loop 64 256 1024 4096 16384 >> "$out/ring_loop.jsonl" 2>> "$out/err"
-    AIPSTACK_ENGINE_ZERO_COPY_MAX=65536 timeout -k 10 400 tools/build/ring_loop 64 256 1024 4096 16384 \
+    AIPSTACK_ENGINE_ZERO_COPY=0 AIPSTACK_ENGINE_ZERO_COPY_SMALL=0 timeout -k 10 400 \
+        tools/build/ring_loop 64 256 1024 4096 16384 >> "$out/ring_loop.jsonl" 2>> "$out/err"
+    AIPSTACK_ENGINE_ZERO_COPY=0 AIPSTACK_ENGINE_ZERO_COPY_SMALL=65536 timeout -k 10 400 tools/build/ring_loop 64 256 1024 4096 16384 \
         >> "$out/ring_loop_zc.jsonl" 2>> "$out/err"
-    AIPSTACK_ENGINE_ZERO_COPY_MAX=65536 AIPSTACK_ENGINE_ZERO_COPY_BYTES=1 timeout -k 10 400 \
+    AIPSTACK_ENGINE_ZERO_COPY=1 AIPSTACK_ENGINE_ZERO_COPY_SMALL=65536 timeout -k 10 400 \
         tools/build/ring_loop 64 256 1024 4096 16384 >> "$out/ring_loop_zcb.jsonl" 2>> "$out/err"
   done
   ;;
@@ -215,8 +217,9 @@ zc2)
   # reads the caller's bytes over the link), alternating
   for i in 1 2; do
     for c in A C RX TX RX2K TX2K C2K; do
-      bench e2e_dma --e2e --config $c --steps 5 --warmup 1
-      AIPSTACK_ENGINE_ZERO_COPY_MAX=100000000 AIPSTACK_ENGINE_ZERO_COPY_BYTES=1 \
+      AIPSTACK_ENGINE_ZERO_COPY=0 AIPSTACK_ENGINE_ZERO_COPY_SMALL=0 \
+          bench e2e_dma --e2e --config $c --steps 5 --warmup 1
+      AIPSTACK_ENGINE_ZERO_COPY=1 AIPSTACK_ENGINE_ZERO_COPY_SMALL=100000000 \
           bench e2e_zcb --e2e --config $c --steps 5 --warmup 1
     done
   done
