@@ -451,7 +451,8 @@ class ChksumEngine:
             pass
 
     def register(self, arr: np.ndarray) -> None:
-        """Page-lock `arr` (kept alive by the engine) so batches in it are DMA'd directly."""
+        """Page-lock `arr` (kept alive by the engine) so that the kernels read batches in it
+        where they lie (zero copy; or DMA'd directly with tune("engine_zero_copy", 0))."""
         _check(self._lib.aipstack_chksum_engine_register(self._h, arr.ctypes.data, arr.nbytes),
                "aipstack_chksum_engine_register")
         self._registered.append(arr)

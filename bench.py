@@ -1046,7 +1046,10 @@ def e2e(args, rank, world, local_rank, layout, n, plen):
             "data": "synthetic (splitmix64 bytes, seed 42; host memory)",
             "config": {"workload": WORKLOAD_NAMES[args.config], "config": args.config,
                        "host_memory": "pageable (CPU copy into pinned staging)"
-                       if args.e2e_pageable else "registered (hipHostRegister, DMA direct)",
+                       if args.e2e_pageable else
+                       ("registered (hipHostRegister; kernels read it in place, zero copy)"
+                        if os.environ.get("AIPSTACK_ENGINE_ZERO_COPY", "1") != "0"
+                        else "registered (hipHostRegister, DMA direct)"),
                        "streams": args.e2e_streams, "chunk_MiB": args.e2e_chunk_mib,
                        **({"slot_stride": slot, "ring_bytes": int(host.nbytes),
                            "value_counts": "frame/packet bytes (the lengths), not slot bytes"}
