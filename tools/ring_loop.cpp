@@ -6,7 +6,8 @@
 // checks the verdicts of every region of the last lap against the frame oracle. Prints one
 // JSON line per B: batches/s, frames/s, GiB/s of frame bytes, us per batch.
 //
-//   tools/build/ring_loop [B ...]        (default B = 256 1024 4096 16384 65536)
+//   tools/build/ring_loop [-r R] [B ...]   (default R = 8, B = 256 1024 4096 16384 65536;
+//                                         R = 1: one batch at a time, the round-trip latency)
 #include <chrono>
 #include <cstdint>
 #include <cstdio>
@@ -18,8 +19,8 @@
 #include "aipstack_amd/synth.h"
 #include "frame_oracle.h"
 
-static int run(uint64_t B) {
-    const uint64_t R = 8, slot = 2048;
+static int run(uint64_t B, uint64_t R) {
+    const uint64_t slot = 2048;
     const uint64_t nfr = R * B;
     // frames: the RX mix, filled as a sender would, laid one per slot
     std::vector<uint64_t> off(nfr + 1);
@@ -82,9 +83,17 @@ static int run(uint64_t B) {
 
 int main(int argc, char **argv) {
     std::vector<uint64_t> sizes;
-    for (int i = 1; i < argc; ++i) sizes.push_back(std::strtoull(argv[i], nullptr, 10));
+    uint64_t regions = 8;
+    for (int i = 1; i < argc; ++i) {
+        if (!std::strcmp(argv[i], "-r") && i + 1 < argc) {
+            regions = std::strtoull(argv[++i], nullptr, 10);
+            if (regions < 1) regions = 1;
+            continue;
+        }
+        sizes.push_back(std::strtoull(argv[i], nullptr, 10));
+    }
     if (sizes.empty()) sizes = {256, 1024, 4096, 16384, 65536};
     int rc = 0;
-    for (uint64_t b : sizes) rc |= run(b);
+    for (uint64_t b : sizes) rc |= run(b, regions);
     return rc;
 }
