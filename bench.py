@@ -762,6 +762,7 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
             **({"traffic_stale": traffic_stale} if traffic_stale else {}),
+            "device_code": device_code_digest(),
             "kernel_us": round(avg_kernel_s * 1e6, 2),
             **({"per_launch_us": {"min": round(per_launch[0], 2),
                                   "median": round(per_launch[len(per_launch) // 2], 2),
@@ -1197,6 +1198,35 @@ KERNEL_SOURCES = ("aipstack_amd/csrc/chksum_device.h", "aipstack_amd/csrc/chksum
                   "aipstack_amd/csrc/frame_kernels.hip")
 
 
+def device_code_digest(lib_path=None):
+    """sha256 (16 hex digits) of the device code objects in libaipstack_chksum.so (its
+    .hip_fatbin section, read with a minimal ELF64 section-table parser): identifies the
+    kernels a PMC measurement was taken on, and changes only when device code does (host-side
+    edits of the .hip files leave it alone). None if the section cannot be read."""
+    import hashlib
+    import struct
+    path = lib_path or os.path.join(ROOT, "aipstack_amd", "lib", "libaipstack_chksum.so")
+    try:
+        with open(path, "rb") as f:
+            data = f.read()
+        if data[:4] != b"\x7fELF" or data[4] != 2:
+            return None
+        shoff, = struct.unpack_from("<Q", data, 0x28)
+        shentsize, shnum, shstrndx = struct.unpack_from("<HHH", data, 0x3A)
+        def sec(i):
+            name, _, _, _, off, size = struct.unpack_from("<IIQQQQ", data, shoff + i * shentsize)
+            return name, off, size
+        _, stroff, _ = sec(shstrndx)
+        for i in range(shnum):
+            name, off, size = sec(i)
+            end = data.index(b"\0", stroff + name)
+            if data[stroff + name:end] == b".hip_fatbin":
+                return hashlib.sha256(data[off:off + size]).hexdigest()[:16]
+    except (OSError, ValueError, struct.error):
+        return None
+    return None
+
+
 def kernel_source_digest():
     """sha256 (16 hex digits) of the device-code sources: identifies the kernels a PMC
     measurement was taken on (tools/pmc_summary.py records it with every entry)."""
@@ -1212,8 +1242,9 @@ def _pmc_traffic(config):
     """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), measured
     by tools/pmc_run.sh on the same command: (2 x FETCH_SIZE + WRITE_SIZE) KiB, the x2
     being the gfx950 correction of MI355X_MICROARCH.md (HBM section). Reported only if the
-    entry was measured on these kernel sources (its kernel_sources digest equals this
-    tree's); a stale entry gives null here and its value under roofline.traffic_stale."""
+    entry was measured on this library's device code (its device_code digest equals
+    device_code_digest() of the loaded .so); a stale entry gives null here and its value
+    under roofline.traffic_stale."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
@@ -1222,10 +1253,10 @@ def _pmc_traffic(config):
         v = e.get("hbm_bytes_per_launch")
         if v is None:
             return None, None
-        if e.get("kernel_sources") != kernel_source_digest():
+        if e.get("device_code") is None or e.get("device_code") != device_code_digest():
             return None, {"hbm_bytes_per_launch": int(v),
-                          "measured_on_kernel_sources": e.get("kernel_sources"),
-                          "note": "PMC entry predates the current kernel sources"}
+                          "measured_on_device_code": e.get("device_code"),
+                          "note": "PMC entry predates the current device code"}
         return int(v), None
     except (OSError, ValueError):
         return None, None

@@ -174,20 +174,36 @@ def test_tx_slots_check():
 
 
 def test_pmc_traffic_only_for_the_current_kernels(tmp_path, monkeypatch):
-    """roofline.traffic comes from profiles/pmc_traffic.json only while the entry's kernel
-    source digest matches this tree; otherwise null, the old value under traffic_stale."""
+    """roofline.traffic comes from profiles/pmc_traffic.json only while the entry's device-code
+    digest (the .hip_fatbin of libaipstack_chksum.so) matches the loaded library's; otherwise
+    null, the old value under traffic_stale."""
     import json
     prof = tmp_path / "profiles"
     prof.mkdir()
-    digest = bench.kernel_source_digest()
     (prof / "pmc_traffic.json").write_text(json.dumps({
-        "A": {"hbm_bytes_per_launch": 123, "kernel_sources": digest},
-        "C": {"hbm_bytes_per_launch": 456, "kernel_sources": "0" * 16}}))
-    for rel in bench.KERNEL_SOURCES:
-        (tmp_path / rel).parent.mkdir(parents=True, exist_ok=True)
-        (tmp_path / rel).write_bytes(open(os.path.join(ROOT, rel), "rb").read())
+        "A": {"hbm_bytes_per_launch": 123, "device_code": "abcd" * 4},
+        "C": {"hbm_bytes_per_launch": 456, "device_code": "0" * 16},
+        "B": {"hbm_bytes_per_launch": 789, "kernel_sources": "f" * 16}}))
     monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    monkeypatch.setattr(bench, "device_code_digest", lambda lib_path=None: "abcd" * 4)
     assert bench._pmc_traffic("A") == (123, None)
     t, stale = bench._pmc_traffic("C")
     assert t is None and stale["hbm_bytes_per_launch"] == 456
-    assert bench._pmc_traffic("B") == (None, None)
+    t, stale = bench._pmc_traffic("B")  # an entry without a device-code digest: stale
+    assert t is None and stale["hbm_bytes_per_launch"] == 789
+    assert bench._pmc_traffic("A2K") == (None, None)
+
+
+def test_device_code_digest_reads_the_fatbin():
+    """The digest is the .hip_fatbin section's hash: stable for the built library, None for a
+    file that is not an ELF with that section."""
+    import tempfile
+    lib = os.path.join(ROOT, "aipstack_amd", "lib", "libaipstack_chksum.so")
+    d = bench.device_code_digest(lib)
+    assert d is not None and len(d) == 16 and d == bench.device_code_digest(lib)
+    hook = os.path.join(ROOT, "aipstack_amd", "lib", "libaipstack_chksum_hook.so")
+    assert bench.device_code_digest(hook) is None  # host-only library: no device code
+    with tempfile.NamedTemporaryFile() as f:
+        f.write(b"not an elf")
+        f.flush()
+        assert bench.device_code_digest(f.name) is None

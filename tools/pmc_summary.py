@@ -14,7 +14,9 @@ algorithmic bytes per launch come from the same round's bench_<CFG>.json, so
     python tools/pmc_summary.py gpurun_out/r01b profiles/pmc_traffic.json
 
 Run it on the tree the counters were taken on: every entry records the digest of the kernel
-sources (bench.kernel_source_digest), and bench.py reports an entry's traffic only while the
+sources (bench.kernel_source_digest) and of the library's device code (bench.device_code_digest:
+the .hip_fatbin section of libaipstack_chksum.so), and bench.py reports an entry's traffic only
+while the device code still matches; before that, while the
 sources still match (else null, with the old value under roofline.traffic_stale). Existing
 entries of other configs are kept.
 """
@@ -75,8 +77,9 @@ def summarise(round_dir, cfg):
 def main():
     round_dir, out_path = sys.argv[1], sys.argv[2]
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    from bench import kernel_source_digest  # the kernels these counters were taken on
+    from bench import device_code_digest, kernel_source_digest  # the kernels measured
     digest = kernel_source_digest()
+    code = device_code_digest()
     merge = os.path.exists(out_path)
     doc = {
         "source": f"tools/pmc_run.sh on MI355X ({round_dir}); median over dispatches "
@@ -95,6 +98,7 @@ def main():
         rec = summarise(round_dir, cfg)
         if rec:
             rec["kernel_sources"] = digest
+            rec["device_code"] = code
             rec["measured_in"] = round_dir
             doc[cfg] = rec
     with open(out_path, "w") as f:
