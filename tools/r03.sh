@@ -14,6 +14,7 @@
 #   zc      engine zero-copy (metadata / packet bytes read in place) vs DMA: engine tests +
 #           receive loop (round-3 experiment; zero copy is the default since)
 #   zc2     e2e from registered memory: DMA vs zero-copy pieces, every config
+#   txtouch split Tx fill with captured headers + field lines touched up front (experiment)
 #   ring    e2e receive rings (RX2K / C2K): 2-D copies of the slots' used prefix vs whole slots
 #   slots   pytest -m gpu; ring-slot lines RX2K / C2K (+ their slot-read ceilings) and A2K;
 #           a U/P sweep of the slotted checksum; e2e through an engine group of 1/2/4
@@ -223,6 +224,20 @@ zc2)
           bench e2e_zcb --e2e --config $c --steps 5 --warmup 1
     done
   done
+  ;;
+txtouch)
+  # split Tx fill: per-lane header loads (product) vs headers captured from the stream with
+  # the field lines loaded up front at the default policy (tools/build/lib_txtouch.so,
+  # tools/experiments/tx_touch_field_lines.patch) vs captured without them; alternating
+  for i in 1 2 3; do
+    bench tx_split --config TX --steps 100 --per-launch --no-cpu-baseline
+    AIPSTACK_AMD_LIB=tools/build/lib_txtouch.so AIPSTACK_CHKSUM_TX_GATHER=1 bench tx_touch \
+        --config TX --steps 100 --per-launch --no-cpu-baseline
+    AIPSTACK_CHKSUM_TX_GATHER=1 bench tx_gather --config TX --steps 100 --per-launch --no-cpu-baseline
+  done
+  AIPSTACK_AMD_LIB=tools/build/lib_txtouch.so AIPSTACK_CHKSUM_TX_GATHER=1 timeout -k 10 300 \
+      rocprofv3 --kernel-trace --stats --output-format csv -d "$out/prof_touch" -o run \
+      -- python3 bench.py --config TX --no-cpu-baseline --no-parity > "$out/prof_touch.log" 2>&1
   ;;
 *)
   echo "unknown mode $mode" >&2; exit 2 ;;
