@@ -29,10 +29,10 @@ struct DeviceGuard {
 // stream), cached per device id; <= 0 on failure.
 int device_cu_count(hipStream_t stream);
 
-// Whether a Tx frame launch takes its header segments from the stream (as Rx does) instead
-// of per-lane header loads (tunable "tx_gather": 0 never, 1 always, else automatic = for
-// the records-only read pass, whose output is not followed by in-place field stores).
-bool tuning_tx_gather(bool records_only);
+// Where a Tx frame launch takes its header segments from (frame_kernels.hip kHdr*): the
+// tunable "tx_gather" (0 per-lane loads, 1 captured from the stream, 2 captured + the field
+// lines touched up front), else `family_default` for the kind of launch.
+int tuning_tx_header_mode(int family_default);
 
 // The contract-violation word of each kernel translation unit on the current device:
 // OR it into *mask, clear it if `clear`.

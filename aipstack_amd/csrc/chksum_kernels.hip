@@ -306,8 +306,9 @@ struct Tuning {
                                           // issued together (2, 4, 8); -1 = off
     std::atomic<int> chunk_packets{0};    // packets per chunk (1, 2, 4, ..., 64); 0 = by
                                           // batch size (pick_shape)
-    std::atomic<int> tx_gather{-1};       // Tx header segments from the stream: 0 never,
-                                          // 1 always, else for the records-only read pass
+    std::atomic<int> tx_gather{-1};       // Tx header segments: 0 per-lane loads, 1 captured
+                                          // from the stream, 2 captured + field lines
+                                          // touched up front; else by kind of Tx launch
     // host engine (read when an engine is created, chksum_engine.cpp):
     std::atomic<int> engine_zero_copy{1};         // kernels read registered input in place
     std::atomic<int> engine_zero_copy_small{65536};  // pieces of at most this many packets
@@ -550,9 +551,9 @@ uint32_t frames_per_chunk(uint64_t n, int cus) { return pick_shape(n, cus).chunk
 
 int tuning_chunk_packets() { return tuning().chunk_packets.load(std::memory_order_relaxed); }
 
-bool tuning_tx_gather(bool records_only) {
+int tuning_tx_header_mode(int family_default) {
     const int t = tuning().tx_gather.load(std::memory_order_relaxed);
-    return t == 0 ? false : t == 1 ? true : records_only;
+    return (t >= 0 && t <= 2) ? t : family_default;
 }
 
 int tuning_frames_in_flight() {

@@ -404,9 +404,15 @@ __device__ __forceinline__ uint32_t l4s_below(const u32x4 (&seg)[kHdrSegs], uint
 #ifndef AIPSTACK_FRAME_PREFETCH
 #define AIPSTACK_FRAME_PREFETCH(SU) ((SU) / 2)
 #endif
-// GATHER: header segments captured from the stream (Rx always; Tx when no in-place field
-// stores follow the pass -- the records-only read pass, launch_frames).
-template <class Desc, bool TX, int U, int P, bool NT, int SU, bool GATHER>
+// GATHER: where the parse's header segments come from (launch_frames picks it):
+//   kHdrLoads    per-lane loads before the stream (default policy);
+//   kHdrCapture  copied out of the stream windows as they pass (Rx, the records-only pass);
+//   kHdrCaptureTouch  the same, plus two dword loads per frame at the default policy before
+//                the stream, on the lines holding the IPv4 and (usually) the L4 checksum
+//                field, so that the split fill's scatter pass finds those lines in the caches
+//                (168 vs 178 us for the whole split fill).
+constexpr int kHdrLoads = 0, kHdrCapture = 1, kHdrCaptureTouch = 2;
+template <class Desc, bool TX, int U, int P, bool NT, int SU, int GATHER>
 __device__ __forceinline__ FrameOut process_chunk(const Desc &desc, uint64_t p0, uint64_t n,
                                                   uint32_t cpk, int lane, uint32_t voff,
                                                   uint32_t not_lane0, FrameLds *lds,
@@ -457,7 +463,7 @@ __device__ __forceinline__ FrameOut process_chunk(const Desc &desc, uint64_t p0,
              << 32) |
             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)E, lastl);
         const uint32_t nseg = ((uint32_t)(X1 - base) + 15u) >> 4;
-        if (GATHER && ((nseg + 63u) >> 6) <= kGatherWindows) {
+        if (GATHER != kHdrLoads && ((nseg + 63u) >> 6) <= kGatherWindows) {
             // (B'+C') one pass: the stream gives H at every frame's aligned start A0_j and
             // hands the header segments to LDS; the parse runs on them after the stream.
             const uint64_t A0 = S & ~(uint64_t)15;
@@ -482,6 +488,16 @@ __device__ __forceinline__ FrameOut process_chunk(const Desc &desc, uint64_t p0,
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
+            // the field lines (frame bytes 24 and 50: IPv4, and TCP / UDP / ICMP behind a
+            // 20-byte IPv4 header) into the caches before the nontemporal stream passes them
+            uint32_t touch0 = 0, touch1 = 0;
+            if constexpr (TX && GATHER == kHdrCaptureTouch) {
+                const uint32_t fo = (uint32_t)(S - base);
+                touch0 = __builtin_amdgcn_raw_buffer_load_b32(
+                    hrsrc, act ? (fo + 24u) & ~3u : 0xFFFFFFF0u, 0u, 0);
+                touch1 = __builtin_amdgcn_raw_buffer_load_b32(
+                    hrsrc, act ? (fo + 50u) & ~3u : 0xFFFFFFF0u, 0u, 0);
+            }
             StreamRun<SU, NT> run;
             run.begin(base, X1, voff);
             // compact slot of r0: the union segments below it. Regions start and end in
@@ -540,6 +556,8 @@ __device__ __forceinline__ FrameOut process_chunk(const Desc &desc, uint64_t p0,
                 r = fold16(h_e - h_s - fl.fhalf);  // exact halves-sum, < 2^32
                 streamed = true;
             }
+            if constexpr (TX && GATHER == kHdrCaptureTouch)
+                asm volatile("" ::"v"(touch0), "v"(touch1));  // loaded, never used
             have_headers = true;  // the parse's inputs are the loaded header blocks
         } else {
             // (C') long runs: header blocks loaded per lane, stream prefixes at each frame's
@@ -623,7 +641,7 @@ __device__ __forceinline__ FrameOut process_chunk(const Desc &desc, uint64_t p0,
 #ifndef AIPSTACK_FRAME_WAVES_PER_SIMD  // occupancy the register budget is fitted to
 #define AIPSTACK_FRAME_WAVES_PER_SIMD 4
 #endif
-template <class Desc, bool TX, int U, int P, bool NT, int SU, bool SPLIT, bool GATHER>
+template <class Desc, bool TX, int U, int P, bool NT, int SU, bool SPLIT, int GATHER>
 __global__ __launch_bounds__(kBlock, AIPSTACK_FRAME_WAVES_PER_SIMD) void frame_kernel(Desc desc, uint64_t n,
                                                        uint32_t chunks_per_wave,
                                                        uint32_t chunk_packets,
@@ -638,7 +656,7 @@ __global__ __launch_bounds__(kBlock, AIPSTACK_FRAME_WAVES_PER_SIMD) void frame_k
     const uint64_t c_end = min(c + chunks_per_wave, nchunks);
     const uint32_t voff = (uint32_t)lane * 16u;
     const uint32_t not_lane0 = lane == 0 ? 0u : ~0u;
-    constexpr bool kGather = SU > 0 && GATHER;
+    constexpr bool kGather = SU > 0 && GATHER != kHdrLoads;
     __shared__ FrameLds lds[kGather ? kWavesPerBlock : 1];  // 9 KiB per wave (gathered stream)
     FrameLds *my = &lds[kGather ? wave_in_block : 0];
     for (; c < c_end; ++c) {
@@ -659,7 +677,7 @@ __global__ __launch_bounds__(kBlock, AIPSTACK_FRAME_WAVES_PER_SIMD) void frame_k
     }
 }
 
-template <class Desc, bool TX, bool SPLIT, bool GATHER>
+template <class Desc, bool TX, bool SPLIT, int GATHER>
 int launch_frames_g(const Desc &desc, uint64_t n, uint8_t *d_status, uint64_t *d_records,
                     hipStream_t stream, int cus) {
     // small batches: fewer frames per chunk, so that they spread over many waves (as the
@@ -707,9 +725,10 @@ int launch_frames_g(const Desc &desc, uint64_t n, uint8_t *d_status, uint64_t *d
 
 // Rx verify; Tx fill in one pass; the split fill's read pass (SPLIT), followed by the
 // scatter pass unless `scatter` is false (the records-only call). Where the header segments
-// come from (GATHER): Rx and the records-only pass capture them from the stream; a fill
-// that writes the fields in place keeps per-lane header loads, whose default cache policy
-// leaves the field lines in the Infinity Cache for the in-place stores.
+// come from (GATHER): Rx and the records-only pass capture them from the stream; the split
+// fill captures them too and touches the field lines up front, so that its scatter pass finds
+// them in the caches; the one-pass fill keeps per-lane header loads, whose default cache
+// policy does the same for its in-place stores.
 template <bool TX, bool SPLIT = false>
 int launch_frames(const void *d_base, const uint64_t *d_offsets, uint64_t n, uint8_t *d_status,
                   uint64_t *d_records, hipStream_t stream, bool scatter = true) {
@@ -718,12 +737,20 @@ int launch_frames(const void *d_base, const uint64_t *d_offsets, uint64_t n, uin
     CsrDesc desc{(uint64_t)(uintptr_t)d_base, d_offsets};
     int st;
     if constexpr (TX) {
-        if (tuning_tx_gather(SPLIT && !scatter))
-            st = launch_frames_g<CsrDesc, true, SPLIT, true>(desc, n, d_status, d_records, stream, cus);
+        const int mode = tuning_tx_header_mode(
+            !SPLIT ? kHdrLoads : scatter ? kHdrCaptureTouch : kHdrCapture);
+        if (mode == kHdrCaptureTouch)
+            st = launch_frames_g<CsrDesc, true, SPLIT, kHdrCaptureTouch>(desc, n, d_status, d_records,
+                                                                        stream, cus);
+        else if (mode == kHdrCapture)
+            st = launch_frames_g<CsrDesc, true, SPLIT, kHdrCapture>(desc, n, d_status, d_records,
+                                                                   stream, cus);
         else
-            st = launch_frames_g<CsrDesc, true, SPLIT, false>(desc, n, d_status, d_records, stream, cus);
+            st = launch_frames_g<CsrDesc, true, SPLIT, kHdrLoads>(desc, n, d_status, d_records,
+                                                                 stream, cus);
     } else {
-        st = launch_frames_g<CsrDesc, false, SPLIT, true>(desc, n, d_status, d_records, stream, cus);
+        st = launch_frames_g<CsrDesc, false, SPLIT, kHdrCapture>(desc, n, d_status, d_records,
+                                                                stream, cus);
     }
     if (st != AIPSTACK_CHKSUM_OK) return st;
     if (SPLIT && scatter) {
@@ -749,7 +776,8 @@ int launch_frames_slotted(const void *d_base, uint64_t slot_stride, const uint32
     desc.stride = slot_stride;
     desc.lens = d_len;
     desc.cap = (uint32_t)(slot_stride < AIPSTACK_CHKSUM_MAX_LEN ? slot_stride : AIPSTACK_CHKSUM_MAX_LEN);
-    return launch_frames_g<SlottedDesc, TX, SPLIT, false>(desc, n, d_status, d_records, stream, cus);
+    return launch_frames_g<SlottedDesc, TX, SPLIT, kHdrLoads>(desc, n, d_status, d_records, stream,
+                                                             cus);
 }
 
 int take_violations_frames(uint32_t *mask, bool clear) {

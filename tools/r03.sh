@@ -15,6 +15,7 @@
 #           receive loop (round-3 experiment; zero copy is the default since)
 #   zc2     e2e from registered memory: DMA vs zero-copy pieces, every config
 #   txtouch split Tx fill with captured headers + field lines touched up front (experiment)
+#   txmode  split / one-pass Tx fill by header mode, then the GPU suite
 #   ring    e2e receive rings (RX2K / C2K): 2-D copies of the slots' used prefix vs whole slots
 #   slots   pytest -m gpu; ring-slot lines RX2K / C2K (+ their slot-read ceilings) and A2K;
 #           a U/P sweep of the slotted checksum; e2e through an engine group of 1/2/4
@@ -238,6 +239,20 @@ txtouch)
   AIPSTACK_AMD_LIB=tools/build/lib_txtouch.so AIPSTACK_CHKSUM_TX_GATHER=1 timeout -k 10 300 \
       rocprofv3 --kernel-trace --stats --output-format csv -d "$out/prof_touch" -o run \
       -- python3 bench.py --config TX --no-cpu-baseline --no-parity > "$out/prof_touch.log" 2>&1
+  ;;
+txmode)
+  # the split fill's header modes (tune tx_gather: 0 per-lane loads = round 2's product,
+  # 2 captured + field lines touched = the product now), and the one-pass fill both ways;
+  # then the GPU suite
+  for i in 1 2 3; do
+    bench tx_split --config TX --steps 100 --per-launch --no-cpu-baseline
+    AIPSTACK_CHKSUM_TX_GATHER=0 bench tx_split_loads --config TX --steps 100 --per-launch --no-cpu-baseline
+    bench tx_inplace --config TX --tx-inplace --steps 100 --per-launch --no-cpu-baseline
+    AIPSTACK_CHKSUM_TX_GATHER=2 bench tx_inplace_touch --config TX --tx-inplace --steps 100 \
+        --per-launch --no-cpu-baseline
+  done
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+      > "$out/pytest_gpu.log" 2>&1
   ;;
 *)
   echo "unknown mode $mode" >&2; exit 2 ;;
