@@ -66,7 +66,9 @@ struct Slot {
     uint64_t *k_off = nullptr;
     uint16_t *k_out = nullptr;
     void *k_bytes = nullptr;  // the packet bytes as the kernel reads them: d_bytes, or the
-                              // caller's registered memory itself (zero-copy pieces)
+                              // caller's registered memory itself (zero-copy pieces), or the
+                              // pinned staging (pageable ring slots, frame bytes only)
+    char *dh_stage = nullptr;  // device address of h_stage
     bool zero_copy = false;
     hipEvent_t done = nullptr;
     bool busy = false;
@@ -104,6 +106,7 @@ struct aipstack_chksum_engine {
     // staging too; so they do for small pieces of pageable input.
     bool zero_copy_bytes = true;
     uint64_t zero_copy_max = 65536;  // metadata in pinned staging for pieces up to this
+    bool pageable_rows = true;  // pageable ring slots: frame bytes staged, read in place
     std::vector<Slot> slots;
     std::vector<Region> registered;
     size_t next_slot = 0;      // round robin over the slots, across batches
@@ -284,7 +287,32 @@ struct Span {
     const char *src = nullptr;
     uint64_t bytes = 0;
     uint64_t pitch = 0, width = 0;
+    const uint32_t *row_len = nullptr;  // ring slots: each row's frame length
 };
+
+// Pageable ring slots into pinned staging: each slot's frame bytes only (row r's first
+// row_len[r] bytes, at the same pitch), by up to host_threads_cap() threads; the kernel then
+// reads the staging in place, so neither the CPU nor the link moves any slack.
+void stage_copy_frames(void *dst, const void *src, uint64_t pitch, const uint32_t *row_len,
+                       uint64_t rows) {
+    auto run = [=](uint64_t lo, uint64_t hi) {
+        for (uint64_t r = lo; r < hi; ++r)
+            std::memcpy(static_cast<char *>(dst) + r * pitch,
+                        static_cast<const char *>(src) + r * pitch, row_len[r]);
+    };
+    const unsigned hw = std::thread::hardware_concurrency();
+    const unsigned nt = (unsigned)std::min<uint64_t>(
+        std::min<uint64_t>(rows / 2048, host_threads_cap()), hw ? hw : 1);
+    if (nt <= 1) {
+        run(0, rows);
+        return;
+    }
+    const uint64_t per = (rows + nt - 1) / nt;
+    std::vector<std::thread> pool;
+    for (unsigned t = 0; t < nt && (uint64_t)t * per < rows; ++t)
+        pool.emplace_back(run, (uint64_t)t * per, std::min(rows, (uint64_t)(t + 1) * per));
+    for (std::thread &t : pool) t.join();
+}
 
 // Enqueue one batch as chunks over the slots. chunker(i0, &i1, &span) describes chunk
 // [i0, i1) of packets and its bytes in host memory; launch(slot, i0, i1) enqueues its
@@ -319,7 +347,8 @@ int enqueue(aipstack_chksum_engine *e, uint64_t n, void *h_out, uint32_t elem, C
         const Region *reg = sp.bytes ? find_registered(e, sp.src, sp.bytes) : nullptr;
         const bool registered = reg != nullptr;
         const bool in_place = e->zero_copy_bytes && registered && reg->dev;
-        s.zero_copy = in_place || cnt <= e->zero_copy_max;
+        const bool staged_rows = !registered && sp.bytes && sp.row_len && e->pageable_rows;
+        s.zero_copy = in_place || staged_rows || cnt <= e->zero_copy_max;
         s.k_off = s.zero_copy ? s.dh_off : s.d_off;
         s.k_out = s.zero_copy ? s.dh_out : s.d_out;
         const bool rows = registered && sp.width != 0 && sp.width < sp.pitch;
@@ -328,6 +357,10 @@ int enqueue(aipstack_chksum_engine *e, uint64_t n, void *h_out, uint32_t elem, C
         if (in_place) {
             // the kernel reads the caller's page-locked bytes over the link itself
             s.k_bytes = const_cast<char *>(reg->dev + (sp.src - reg->p));
+        } else if (staged_rows) {
+            // the frames' bytes into pinned staging, read there by the kernel
+            stage_copy_frames(s.h_stage, sp.src, sp.pitch, sp.row_len, sp.bytes / sp.pitch);
+            s.k_bytes = s.dh_stage;
         } else if (sp.bytes && !registered) {  // pageable: CPU copy into pinned staging
             stage_copy(s.h_stage, sp.src, sp.bytes);
             h_src = s.h_stage;
@@ -409,6 +442,7 @@ extern "C" int aipstack_chksum_engine_create(int device, uint64_t chunk_bytes, i
     if (const char *v = std::getenv("AIPSTACK_ENGINE_SLOT_ROWS")) e->slot_rows = std::atoi(v) != 0;
     e->zero_copy_bytes = tuning_engine_zero_copy() != 0;
     e->zero_copy_max = (uint64_t)std::max(tuning_engine_zero_copy_small(), 0);
+    e->pageable_rows = tuning_engine_pageable_rows() != 0;
     e->slots.resize((size_t)nstreams);
     int st = AIPSTACK_CHKSUM_OK;
     for (Slot &s : e->slots) {
@@ -424,6 +458,8 @@ extern "C" int aipstack_chksum_engine_create(int device, uint64_t chunk_bytes, i
             st = check_hip(hipHostGetDevicePointer(reinterpret_cast<void **>(&s.dh_off), s.h_off, 0));
         if (st == AIPSTACK_CHKSUM_OK)
             st = check_hip(hipHostGetDevicePointer(reinterpret_cast<void **>(&s.dh_out), s.h_out, 0));
+        if (st == AIPSTACK_CHKSUM_OK)
+            st = check_hip(hipHostGetDevicePointer(reinterpret_cast<void **>(&s.dh_stage), s.h_stage, 0));
     }
     if (st != AIPSTACK_CHKSUM_OK) {
         release(e);
@@ -652,10 +688,11 @@ int submit_slotted_like(aipstack_chksum_engine *e, const void *h_base, uint64_t 
         *i1 = std::min(n, i0 + per);
         sp->src = base + i0 * slot_stride;
         sp->bytes = (*i1 - i0) * slot_stride;
+        sp->pitch = slot_stride;
+        sp->row_len = h_len + i0;
         if (!e->slot_rows) return;
         uint32_t longest = 0;
         for (uint64_t i = i0; i < *i1; ++i) longest = std::max(longest, h_len[i]);
-        sp->pitch = slot_stride;
         sp->width = std::min<uint64_t>(((uint64_t)longest + 63u) & ~63ull, slot_stride);
         if (longest == 0) sp->bytes = 0;  // every frame empty: nothing to copy
     };

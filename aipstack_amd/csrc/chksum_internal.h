@@ -58,6 +58,7 @@ int tuning_stream_windows(int family_default);
 // at most tuning_engine_zero_copy_small() packets keep offsets / results in pinned staging.
 int tuning_engine_zero_copy();
 int tuning_engine_zero_copy_small();
+int tuning_engine_pageable_rows();  // pageable ring slots: frame bytes staged, read in place
 
 }  // namespace aipstack_amd
 

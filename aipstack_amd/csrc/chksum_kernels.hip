@@ -313,6 +313,8 @@ struct Tuning {
     std::atomic<int> engine_zero_copy{1};         // kernels read registered input in place
     std::atomic<int> engine_zero_copy_small{65536};  // pieces of at most this many packets
                                                      // keep offsets / results in pinned staging
+    std::atomic<int> engine_pageable_rows{1};  // pageable ring slots: frame bytes staged
+                                               // and read in place (0: whole slots DMA'd)
 
     Tuning() {
         auto env = [](const char *k, std::atomic<int> &v) {
@@ -329,6 +331,7 @@ struct Tuning {
         env("AIPSTACK_CHKSUM_TX_GATHER", tx_gather);
         env("AIPSTACK_ENGINE_ZERO_COPY", engine_zero_copy);
         env("AIPSTACK_ENGINE_ZERO_COPY_SMALL", engine_zero_copy_small);
+        env("AIPSTACK_ENGINE_PAGEABLE_ROWS", engine_pageable_rows);
 
     }
 };
@@ -539,6 +542,9 @@ int tuning_engine_zero_copy() { return tuning().engine_zero_copy.load(std::memor
 int tuning_engine_zero_copy_small() {
     return tuning().engine_zero_copy_small.load(std::memory_order_relaxed);
 }
+int tuning_engine_pageable_rows() {
+    return tuning().engine_pageable_rows.load(std::memory_order_relaxed);
+}
 
 int tuning_stream_windows(int family_default) {
     const int t = tuning().stream.load(std::memory_order_relaxed);
@@ -632,6 +638,7 @@ extern "C" int aipstack_chksum_tune(const char *key, int value) {
     else if (!std::strcmp(key, "tx_gather")) t.tx_gather = value;
     else if (!std::strcmp(key, "engine_zero_copy")) t.engine_zero_copy = value;
     else if (!std::strcmp(key, "engine_zero_copy_small")) t.engine_zero_copy_small = value;
+    else if (!std::strcmp(key, "engine_pageable_rows")) t.engine_pageable_rows = value;
     else return AIPSTACK_CHKSUM_EINVAL;
     return AIPSTACK_CHKSUM_OK;
 }

@@ -16,6 +16,7 @@
 #   zc2     e2e from registered memory: DMA vs zero-copy pieces, every config
 #   txtouch split Tx fill with captured headers + field lines touched up front (experiment)
 #   txmode  split / one-pass Tx fill by header mode, then the GPU suite
+#   prows   pageable rings staged frame-bytes-only vs whole slots; a third field-line touch
 #   ring    e2e receive rings (RX2K / C2K): 2-D copies of the slots' used prefix vs whole slots
 #   slots   pytest -m gpu; ring-slot lines RX2K / C2K (+ their slot-read ceilings) and A2K;
 #           a U/P sweep of the slotted checksum; e2e through an engine group of 1/2/4
@@ -253,6 +254,24 @@ txmode)
   done
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
       > "$out/pytest_gpu.log" 2>&1
+  ;;
+prows)
+  # pageable rings: frame bytes staged and read in place (product) vs whole slots staged and
+  # DMA'd (AIPSTACK_ENGINE_PAGEABLE_ROWS=0); then the split Tx fill with a third field-line
+  # touch (tools/build/lib_touch3.so) vs the product; the engine tests
+  for i in 1 2; do
+    for c in RX2K TX2K C2K; do
+      bench e2e_prows --e2e --e2e-pageable --config $c --steps 3 --warmup 1
+      AIPSTACK_ENGINE_PAGEABLE_ROWS=0 bench e2e_pwhole --e2e --e2e-pageable --config $c --steps 3 --warmup 1
+    done
+  done
+  for i in 1 2 3; do
+    bench tx_split --config TX --steps 100 --per-launch --no-cpu-baseline
+    AIPSTACK_AMD_LIB=tools/build/lib_touch3.so bench tx_touch3 --config TX --steps 100 --per-launch \
+        --no-cpu-baseline
+  done
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -k "engine" --timeout 120 \
+      --timeout-method thread > "$out/pytest_engine.log" 2>&1
   ;;
 *)
   echo "unknown mode $mode" >&2; exit 2 ;;
