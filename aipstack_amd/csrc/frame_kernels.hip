@@ -314,9 +314,6 @@ __device__ __forceinline__ uint32_t hdr_below(const u32x4 (&seg)[kHdrSegs],
 // Which lanes of window w hold header segments is bit (w & 31) of word (w >> 5) of an LDS
 // bit table per lane slot, so runs of at most kGatherWindows windows take this path.
 constexpr uint32_t kGatherWindows = 128;
-#ifndef AIPSTACK_EXP_TOUCH3  // experiments only (tools/build_variant.sh): a third field-line touch
-#define AIPSTACK_EXP_TOUCH3 0
-#endif
 #ifndef AIPSTACK_FRAME_NT  // experiments: 0 = the frame stream loads with the default policy
 #define AIPSTACK_FRAME_NT 1
 #endif
@@ -493,17 +490,13 @@ __device__ __forceinline__ FrameOut process_chunk(const Desc &desc, uint64_t p0,
             __builtin_amdgcn_wave_barrier();
             // the field lines (frame bytes 24 and 50: IPv4, and TCP / UDP / ICMP behind a
             // 20-byte IPv4 header) into the caches before the nontemporal stream passes them
-            uint32_t touch0 = 0, touch1 = 0, touch2 = 0;
+            uint32_t touch0 = 0, touch1 = 0;
             if constexpr (TX && GATHER == kHdrCaptureTouch) {
                 const uint32_t fo = (uint32_t)(S - base);
                 touch0 = __builtin_amdgcn_raw_buffer_load_b32(
                     hrsrc, act ? (fo + 24u) & ~3u : 0xFFFFFFF0u, 0u, 0);
                 touch1 = __builtin_amdgcn_raw_buffer_load_b32(
                     hrsrc, act ? (fo + 50u) & ~3u : 0xFFFFFFF0u, 0u, 0);
-#if AIPSTACK_EXP_TOUCH3  // experiment: also the line of byte 90 (L4 field behind IPv4 options)
-                touch2 = __builtin_amdgcn_raw_buffer_load_b32(
-                    hrsrc, act ? (fo + 90u) & ~3u : 0xFFFFFFF0u, 0u, 0);
-#endif
             }
             StreamRun<SU, NT> run;
             run.begin(base, X1, voff);
@@ -564,7 +557,7 @@ __device__ __forceinline__ FrameOut process_chunk(const Desc &desc, uint64_t p0,
                 streamed = true;
             }
             if constexpr (TX && GATHER == kHdrCaptureTouch)
-                asm volatile("" ::"v"(touch0), "v"(touch1), "v"(touch2));  // loaded, never used
+                asm volatile("" ::"v"(touch0), "v"(touch1));  // loaded, never used
             have_headers = true;  // the parse's inputs are the loaded header blocks
         } else {
             // (C') long runs: header blocks loaded per lane, stream prefixes at each frame's
