@@ -204,7 +204,8 @@ int aipstack_chksum_tx_fill_records_slotted(const void *d_base, uint64_t slot_st
  * link (only the bytes the packets cover cross it: for ring slots not the slack); with
  * aipstack_chksum_tune("engine_zero_copy", 0) before the engine is created they are DMA'd
  * to the device first instead. Other host memory is first copied into the engine's pinned
- * staging. The host_* calls are synchronous; the submit_*
+ * staging (a ring of slots: each frame's bytes only, read there by the kernel; tune
+ * "engine_pageable_rows" 0 = whole slots, DMA'd). The host_* calls are synchronous; the submit_*
  * calls enqueue a batch and return a ticket at once, so the caller can fill its next batch
  * (e.g. read() frames into its ring) while the GPU works; _poll / _wait complete it. Calls
  * on one engine from several threads are serialised, except that _wait waits for the GPU
