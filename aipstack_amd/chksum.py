@@ -414,6 +414,23 @@ def chksum_batch_seeded_csr(buf, offsets, states, *, out=None, stream=None):
     return out
 
 
+def _host_u64(a):
+    """Host offsets as the C-ABI's uint64: a contiguous int64 array is passed as it is (a
+    view; the engine rejects the huge values a negative entry becomes, as non-decreasing
+    offsets within the frames), anything else is converted (a copy)."""
+    if isinstance(a, np.ndarray) and a.dtype == np.int64 and a.flags.c_contiguous:
+        return a.view(np.uint64)
+    return np.ascontiguousarray(a, dtype=np.uint64)
+
+
+def _host_u32(a):
+    """Host lengths as the C-ABI's uint32 (int32 viewed, as _host_u64; the engine rejects
+    lengths above the slot stride)."""
+    if isinstance(a, np.ndarray) and a.dtype == np.int32 and a.flags.c_contiguous:
+        return a.view(np.uint32)
+    return np.ascontiguousarray(a, dtype=np.uint32)
+
+
 class ChksumEngine:
     """Host-memory streaming engine (C-ABI ``aipstack_chksum_engine_*``): checksums
     batches held in HOST memory (numpy arrays) and returns results in host memory,
@@ -504,7 +521,7 @@ class ChksumEngine:
     def submit_csr(self, buf: np.ndarray, offsets: np.ndarray, *, out=None,
                    final: bool = False):
         """Enqueue a CSR batch; returns (ticket, out) (see submit_strided)."""
-        o = np.ascontiguousarray(offsets, dtype=np.uint64)
+        o = _host_u64(offsets)
         n = o.size - 1
         if n > 0 and int(o[-1]) > buf.nbytes:
             raise ValueError("offsets exceed buf")
@@ -550,7 +567,7 @@ class ChksumEngine:
         """Rx verify of raw Ethernet frames in HOST memory (frame i =
         ``frames[offsets[i]:offsets[i+1]]``): one AIPSTACK_RX_* verdict per frame (uint8),
         as :func:`rx_verify` on the device."""
-        o = np.ascontiguousarray(offsets, dtype=np.uint64)
+        o = _host_u64(offsets)
         n = o.size - 1
         if n > 0 and int(o[-1]) > frames.nbytes:
             raise ValueError("offsets exceed frames")
@@ -562,7 +579,7 @@ class ChksumEngine:
 
     def submit_rx_verify(self, frames: np.ndarray, offsets: np.ndarray, *, out=None):
         """Enqueue an Rx verify batch; returns (ticket, out) (see submit_strided)."""
-        o = np.ascontiguousarray(offsets, dtype=np.uint64)
+        o = _host_u64(offsets)
         n = o.size - 1
         if n > 0 and int(o[-1]) > frames.nbytes:
             raise ValueError("offsets exceed frames")
@@ -578,7 +595,7 @@ class ChksumEngine:
     def _tx_args(frames, offsets, status):
         if not isinstance(frames, np.ndarray) or not frames.flags.writeable:
             raise ValueError("frames must be a writable numpy array (filled in place)")
-        o = np.ascontiguousarray(offsets, dtype=np.uint64)
+        o = _host_u64(offsets)
         n = o.size - 1
         if n > 0 and int(o[-1]) > frames.nbytes:
             raise ValueError("offsets exceed frames")
@@ -612,7 +629,7 @@ class ChksumEngine:
 
     @staticmethod
     def _slot_args(buf, slot_stride: int, lens):
-        ln = np.ascontiguousarray(lens, dtype=np.uint32)
+        ln = _host_u32(lens)
         n = ln.size
         if slot_stride <= 0 or n * slot_stride > buf.nbytes:
             raise ValueError("the buffer must hold n whole slots of slot_stride bytes")
@@ -695,7 +712,7 @@ class ChksumEngine:
 
     def csr(self, buf: np.ndarray, offsets: np.ndarray, *, out=None,
             final: bool = False) -> np.ndarray:
-        o = np.ascontiguousarray(offsets, dtype=np.uint64)
+        o = _host_u64(offsets)
         n = o.size - 1
         if n > 0 and int(o[-1]) > buf.nbytes:
             raise ValueError("offsets exceed buf")
@@ -769,7 +786,7 @@ class ChksumEngineGroup:
         return out
 
     def csr(self, buf, offsets, *, out=None, final=False):
-        o = np.ascontiguousarray(offsets, dtype=np.uint64)
+        o = _host_u64(offsets)
         n = o.size - 1
         if n > 0 and int(o[-1]) > buf.nbytes:
             raise ValueError("offsets exceed buf")
@@ -779,7 +796,7 @@ class ChksumEngineGroup:
         return out
 
     def rx_verify(self, frames, offsets, *, out=None):
-        o = np.ascontiguousarray(offsets, dtype=np.uint64)
+        o = _host_u64(offsets)
         n = o.size - 1
         if n > 0 and int(o[-1]) > frames.nbytes:
             raise ValueError("offsets exceed frames")

@@ -36,6 +36,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
@@ -116,6 +117,38 @@ struct Applier {
     std::map<uint64_t, int> pending;  // ticket -> pieces queued or being applied
     bool stop = false;
     std::thread thread;
+    std::atomic<uint64_t> *busy_ns = nullptr;  // engine stats (AIPSTACK_ENGINE_STATS), or null
+};
+
+// Where an engine's host time goes (AIPSTACK_ENGINE_STATS=1: one JSON line on stderr at
+// destroy; the counters cost nothing otherwise). Nanoseconds, summed over the engine's life.
+struct Stats {
+    bool on = false;
+    std::atomic<uint64_t> enqueue{0};     // inside the submit calls
+    std::atomic<uint64_t> slot_wait{0};   // of which: waiting for a slot's previous piece
+    std::atomic<uint64_t> rec_copy{0};    // of which: Tx records copied out of a slot
+    std::atomic<uint64_t> stage{0};       // of which: pageable input staged by the CPU
+    std::atomic<uint64_t> apply{0};       // applier thread: Tx records applied
+    std::atomic<uint64_t> apply_wait{0};  // completion calls waiting for the applier
+    std::atomic<uint64_t> complete{0};    // inside the poll / wait calls
+    uint64_t created = 0;
+    std::atomic<uint64_t> pieces{0};
+};
+
+uint64_t now_ns() {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
+// Adds the time since construction to a counter, when stats are on.
+struct Span_ns {
+    std::atomic<uint64_t> *to;
+    uint64_t t0;
+    Span_ns(const Stats &st, std::atomic<uint64_t> &c) : to(st.on ? &c : nullptr), t0(to ? now_ns() : 0) {}
+    ~Span_ns() {
+        if (to) to->fetch_add(now_ns() - t0, std::memory_order_relaxed);
+    }
 };
 
 }  // namespace
@@ -143,6 +176,7 @@ struct aipstack_chksum_engine {
     std::map<uint64_t, int> failed;
     std::mutex mu;  // serialises the calls on one engine
     std::unique_ptr<Applier> applier;  // Tx record apply, off the submitting thread
+    Stats stats;
 };
 
 namespace {
@@ -240,7 +274,15 @@ void stage_copy(void *dst, const void *src, uint64_t bytes) {
 // aipstack_chksum_tx_fill_records).
 void apply_tx_range(const uint64_t *rec, char *frames, const uint64_t *offs, uint64_t stride,
                     uint8_t *status, uint64_t lo, uint64_t hi) {
+    // every frame's field line is a cache miss (the device read the frames, not this core):
+    // the lines a few frames ahead are requested while this one is written
+    constexpr uint64_t kAhead = 16;
     for (uint64_t i = lo; i < hi; ++i) {
+        if (i + kAhead < hi) {
+            const char *g = frames + (offs ? offs[i + kAhead] : (i + kAhead) * stride);
+            __builtin_prefetch(g + 24, 1, 0);  // the IPv4 checksum
+            __builtin_prefetch(g + 51, 1, 0);  // TCP's (UDP's and ICMP's share a line with one)
+        }
         const uint64_t x = rec[i];
         char *f = frames + (offs ? offs[i] : i * stride);
         status[i] = (uint8_t)(x >> 48);
@@ -288,8 +330,10 @@ void applier_loop(Applier *a) {
         ApplyJob job = std::move(a->queue.front());
         a->queue.pop_front();
         lock.unlock();
+        const uint64_t t0 = a->busy_ns ? now_ns() : 0;
         apply_tx_records(job.rec.data(), job.frames, job.offs, job.stride, job.status,
                          job.rec.size());
+        if (a->busy_ns) a->busy_ns->fetch_add(now_ns() - t0, std::memory_order_relaxed);
         lock.lock();
         if (--a->pending[job.ticket] == 0) a->pending.erase(job.ticket);
         a->done.notify_all();
@@ -299,6 +343,7 @@ void applier_loop(Applier *a) {
 void queue_apply(aipstack_chksum_engine *e, ApplyJob &&job) {
     if (!e->applier) {
         e->applier.reset(new Applier);
+        if (e->stats.on) e->applier->busy_ns = &e->stats.apply;
         e->applier->thread = std::thread(applier_loop, e->applier.get());
     }
     Applier *a = e->applier.get();
@@ -313,6 +358,7 @@ void queue_apply(aipstack_chksum_engine *e, ApplyJob &&job) {
 bool applies_pending(aipstack_chksum_engine *e, uint64_t ticket, bool blocking) {
     Applier *a = e->applier.get();
     if (!a) return false;
+    Span_ns timed(e->stats, e->stats.apply_wait);
     std::unique_lock<std::mutex> lock(a->mu);
     auto busy = [a, ticket] {
         return ticket == 0 ? !a->pending.empty() : a->pending.count(ticket) != 0;
@@ -340,6 +386,7 @@ int drain(aipstack_chksum_engine *e, Slot &s, bool blocking = true) {
     if (!s.busy) return AIPSTACK_CHKSUM_OK;
     hipError_t r;
     if (blocking) {
+        Span_ns timed(e->stats, e->stats.slot_wait);
         r = hipEventSynchronize(s.done);
     } else {
         r = hipEventQuery(s.done);
@@ -352,6 +399,7 @@ int drain(aipstack_chksum_engine *e, Slot &s, bool blocking = true) {
     if (st == AIPSTACK_CHKSUM_OK && s.tx_frames) {
         // the records leave the slot (copied), the applier writes the fields
         const uint64_t *rec = reinterpret_cast<const uint64_t *>(s.h_out);
+        Span_ns timed(e->stats, e->stats.rec_copy);
         queue_apply(e, ApplyJob{std::vector<uint64_t>(rec, rec + s.count), s.tx_frames,
                                 s.tx_offs, s.tx_stride, s.tx_status, s.ticket});
     } else if (st == AIPSTACK_CHKSUM_OK) {
@@ -406,6 +454,7 @@ void stage_copy_frames(void *dst, const void *src, uint64_t pitch, const uint32_
 template <class Chunker, class Launch>
 int enqueue(aipstack_chksum_engine *e, uint64_t n, void *h_out, uint32_t elem, Chunker chunker,
             Launch launch, uint64_t *ticket) {
+    Span_ns timed(e->stats, e->stats.enqueue);
     DeviceGuard dg(e->device);
     if (!dg.ok) return AIPSTACK_CHKSUM_ENODEV;
     const uint64_t t = e->next_ticket++;
@@ -444,9 +493,11 @@ int enqueue(aipstack_chksum_engine *e, uint64_t n, void *h_out, uint32_t elem, C
             s.k_bytes = const_cast<char *>(reg->dev + (sp.src - reg->p));
         } else if (staged_rows) {
             // the frames' bytes into pinned staging, read there by the kernel
+            Span_ns staged(e->stats, e->stats.stage);
             stage_copy_frames(s.h_stage, sp.src, sp.pitch, sp.row_len, sp.bytes / sp.pitch);
             s.k_bytes = s.dh_stage;
         } else if (sp.bytes && !registered) {  // pageable: CPU copy into pinned staging
+            Span_ns staged(e->stats, e->stats.stage);
             stage_copy(s.h_stage, sp.src, sp.bytes);
             h_src = s.h_stage;
         }
@@ -459,6 +510,7 @@ int enqueue(aipstack_chksum_engine *e, uint64_t n, void *h_out, uint32_t elem, C
             status = check_hip(hipMemcpyAsync(s.d_bytes, h_src, sp.bytes, hipMemcpyHostToDevice,
                                               s.stream));
         s.seq = ++e->pieces;
+        e->stats.pieces.fetch_add(1, std::memory_order_relaxed);
 #ifdef AIPSTACK_ENGINE_FAULT_INJECTION
         if (status == AIPSTACK_CHKSUM_OK && injected(g_fail_at_launch, s.seq))
             status = AIPSTACK_CHKSUM_EHIP;
@@ -483,6 +535,7 @@ int enqueue(aipstack_chksum_engine *e, uint64_t n, void *h_out, uint32_t elem, C
 // only), < 0 = it failed (its first failure; the record is consumed).
 int complete(aipstack_chksum_engine *e, uint64_t ticket, bool blocking) {
     if (ticket == 0 || ticket >= e->next_ticket) return AIPSTACK_CHKSUM_EINVAL;
+    Span_ns timed(e->stats, e->stats.complete);
     DeviceGuard dg(e->device);
     if (!dg.ok) return AIPSTACK_CHKSUM_ENODEV;
     int pending = 0;
@@ -530,6 +583,8 @@ extern "C" int aipstack_chksum_engine_create(int device, uint64_t chunk_bytes, i
     e->zero_copy_bytes = tuning_engine_zero_copy() != 0;
     e->zero_copy_max = (uint64_t)std::max(tuning_engine_zero_copy_small(), 0);
     e->pageable_rows = tuning_engine_pageable_rows() != 0;
+    if (const char *v = std::getenv("AIPSTACK_ENGINE_STATS")) e->stats.on = std::atoi(v) != 0;
+    e->stats.created = now_ns();
     e->slots.resize((size_t)nstreams);
     int st = AIPSTACK_CHKSUM_OK;
     for (Slot &s : e->slots) {
@@ -565,6 +620,18 @@ extern "C" void aipstack_chksum_engine_destroy(aipstack_chksum_engine *e) {
         drain_all(e);  // pieces in flight complete: results written, Tx fields applied
     }
     release(e);
+    if (e->stats.on) {
+        const Stats &t = e->stats;
+        auto ms = [](const std::atomic<uint64_t> &v) { return (double)v.load() / 1e6; };
+        std::fprintf(stderr,
+                     "{\"engine_stats\": {\"device\": %d, \"pieces\": %llu, \"life_ms\": %.3f, "
+                     "\"enqueue_ms\": %.3f, \"slot_wait_ms\": %.3f, \"rec_copy_ms\": %.3f, "
+                     "\"stage_ms\": %.3f, \"complete_ms\": %.3f, \"apply_wait_ms\": %.3f, "
+                     "\"applier_busy_ms\": %.3f}}\n",
+                     e->device, (unsigned long long)t.pieces.load(),
+                     (double)(now_ns() - t.created) / 1e6, ms(t.enqueue), ms(t.slot_wait),
+                     ms(t.rec_copy), ms(t.stage), ms(t.complete), ms(t.apply_wait), ms(t.apply));
+    }
     delete e;
 }
 

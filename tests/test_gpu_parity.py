@@ -593,6 +593,16 @@ def test_engine_rejects_bad_offsets():
         with pytest.raises(A.ChksumError):
             eng.csr(buf, np.array([0, 70000], dtype=np.uint64))
         assert eng.csr(buf, np.array([0], dtype=np.uint64)).size == 0
+        # int64 offsets / int32 lengths are passed to the C-ABI as views (no copy): a
+        # negative entry becomes a huge unsigned value, which the engine rejects
+        with pytest.raises((A.ChksumError, ValueError)):
+            eng.csr(buf, np.array([0, -100, 200], dtype=np.int64))
+        with pytest.raises((A.ChksumError, ValueError)):
+            eng.rx_verify(buf, np.array([-64, 0], dtype=np.int64))
+        with pytest.raises(A.ChksumError):
+            eng.slotted(buf[:2048 * 4], 2048, np.array([60, -1, 60, 60], dtype=np.int32))
+        good = np.array([0, 100, 1500], dtype=np.int64)
+        assert np.array_equal(eng.csr(buf, good), eng.csr(buf, good.astype(np.uint64)))
 
 
 # ---- chained scatter-gather batches ---------------------------------

@@ -8,6 +8,7 @@
 #   check   pytest -m gpu, then bench A, C, CHAIN, TXREC, RX (no CPU baseline)
 #   txnt    split Tx fill: scatter stores plain vs nontemporal (+ rocprof of each)
 #   asweep  launch shapes of configs A and B (robustness across boxes)
+#   estats  engine host-time counters, e2e RX / TX / TX2K
 #   e2ethreads  host engine Tx: apply/staging threads, piece size, streams
 #   tx2k    send ring: device in-place slotted Tx fill (bench + rocprof) and e2e
 #   ringloop  the engine as a TAP receive loop from C++, per batch size
@@ -45,6 +46,17 @@ txrec)
   tools/pmc_run.sh TXREC "$out/pmc_TXREC"
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
       > "$out/pytest_gpu.log" 2>&1
+  ;;
+estats)
+  # where the engine's host time goes, Tx vs Rx e2e (AIPSTACK_ENGINE_STATS: stderr JSON)
+  export AIPSTACK_ENGINE_STATS=1
+  for c in RX TX TX2K; do
+    bench "e2e_$c" --e2e --config $c --steps 5 --warmup 1
+    bench "e2ep_$c" --e2e --e2e-pageable --config $c --steps 3 --warmup 1
+  done
+  AIPSTACK_ENGINE_HOST_THREADS=16 bench e2ep_TX2K_t16 --e2e --e2e-pageable --config TX2K --steps 3 --warmup 1
+  AIPSTACK_ENGINE_HOST_THREADS=16 bench e2ep_RX2K_t16 --e2e --e2e-pageable --config RX2K --steps 3 --warmup 1
+  bench e2ep_RX2K --e2e --e2e-pageable --config RX2K --steps 3 --warmup 1
   ;;
 check)
   # the GPU suite, then the timed configs the last change could move
