@@ -178,3 +178,24 @@ def test_host_hook_variants_match_oracle(oracle):
         want = oracle.inverted(buf, o, ln)
         for v in (0, 1, 2, 3):
             assert f(v, buf.ctypes.data + o, ln) == want, (v, o, ln)
+
+
+def test_engine_host_arrays_view_or_convert():
+    """The engine wrappers hand offsets / lengths to the C-ABI as uint64 / uint32: contiguous
+    int64 / int32 arrays as views (no per-call copy of a 1 M-entry array), the rest converted;
+    the bit patterns are those of the conversion either way."""
+    from aipstack_amd.chksum import _host_u32, _host_u64
+    o = np.arange(0, 10 * 1500, 1500, dtype=np.int64)
+    v = _host_u64(o)
+    assert v.dtype == np.uint64 and np.shares_memory(v, o)
+    assert np.array_equal(v, o.astype(np.uint64))
+    neg = np.array([0, -1], dtype=np.int64)
+    assert int(_host_u64(neg)[1]) == 2**64 - 1  # rejected by the engine's offset check
+    for src in (o.astype(np.int32), o.astype(np.uint64), o[::2], list(o)):
+        c = _host_u64(src)
+        assert c.dtype == np.uint64 and c.flags.c_contiguous
+        assert np.array_equal(c, np.asarray(src, dtype=np.int64).astype(np.uint64))
+    ln = np.array([60, 1514, 0], dtype=np.int32)
+    assert _host_u32(ln).dtype == np.uint32 and np.shares_memory(_host_u32(ln), ln)
+    assert int(_host_u32(np.array([-1], dtype=np.int32))[0]) == 2**32 - 1
+    assert np.array_equal(_host_u32([60, 1514]), np.array([60, 1514], dtype=np.uint32))

@@ -48,7 +48,10 @@ txrec)
       > "$out/pytest_gpu.log" 2>&1
   ;;
 estats)
-  # where the engine's host time goes, Tx vs Rx e2e (AIPSTACK_ENGINE_STATS: stderr JSON)
+  # where the engine's host time goes, Tx vs Rx e2e (AIPSTACK_ENGINE_STATS: stderr JSON),
+  # after the GPU suite
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+      > "$out/pytest_gpu.log" 2>&1
   export AIPSTACK_ENGINE_STATS=1
   for c in RX TX TX2K; do
     bench "e2e_$c" --e2e --config $c --steps 5 --warmup 1
