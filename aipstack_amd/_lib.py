@@ -55,6 +55,8 @@ SIGNATURES = {
     "aipstack_chksum_batch_slotted": (_c_int, [_c_vp, _c_u64, _c_vp, _c_u64, _c_vp, _c_u32, _c_vp]),
     "aipstack_chksum_rx_verify_slotted": (_c_int, [_c_vp, _c_u64, _c_vp, _c_u64, _c_vp, _c_vp]),
     "aipstack_chksum_tx_fill_slotted": (_c_int, [_c_vp, _c_u64, _c_vp, _c_u64, _c_vp, _c_vp]),
+    "aipstack_chksum_tx_fill_slotted_split": (_c_int, [_c_vp, _c_u64, _c_vp, _c_u64, _c_vp, _c_vp,
+                                                       _c_u64, _c_vp]),
     "aipstack_chksum_tx_fill_records_slotted": (_c_int, [_c_vp, _c_u64, _c_vp, _c_u64, _c_vp, _c_vp]),
     "aipstack_chksum_engine_submit_rx_verify": (_c_int, [_c_vp, _c_vp, _c_vp, _c_u64, _c_vp, _c_vp]),
     "aipstack_chksum_engine_submit_strided": (_c_int, [_c_vp, _c_vp, _c_u64, _c_u32, _c_u64, _c_vp,

@@ -369,14 +369,23 @@ def rx_verify_slotted(frames, slot_stride: int, lens, *, out=None, stream=None):
     return out
 
 
-def tx_fill_slotted(frames, slot_stride: int, lens, *, out=None, stream=None):
-    """Tx fill, in place, of a ring of frame slots on the GPU; one status per frame."""
+def tx_fill_slotted(frames, slot_stride: int, lens, *, out=None, stream=None, split=False,
+                    workspace=None):
+    """Tx fill, in place, of a ring of frame slots on the GPU; one status per frame.
+    ``split=True`` runs ``aipstack_chksum_tx_fill_slotted_split`` (records pass + scatter pass
+    through a workspace of 8 bytes per frame, as :func:`tx_fill`); both write the same bytes."""
     _require_device(frames, "frames")
     n = _require_lens(lens, frames.numel() * frames.element_size(), slot_stride, frames)
     out = _u8_out(out, n, frames)
-    _check(_lib.load().aipstack_chksum_tx_fill_slotted(
-        frames.data_ptr(), slot_stride, lens.data_ptr(), n, out.data_ptr(),
-        _stream_handle(stream, frames)), "aipstack_chksum_tx_fill_slotted")
+    lib = _lib.load()
+    if not split:
+        _check(lib.aipstack_chksum_tx_fill_slotted(
+            frames.data_ptr(), slot_stride, lens.data_ptr(), n, out.data_ptr(),
+            _stream_handle(stream, frames)), "aipstack_chksum_tx_fill_slotted")
+        return out
+    _split_call(lib, "aipstack_chksum_tx_fill_slotted_split", frames, n, stream, workspace,
+                lambda ws, ws_bytes, h: (frames.data_ptr(), slot_stride, lens.data_ptr(), n,
+                                         out.data_ptr(), ws, ws_bytes, h))
     return out
 
 
@@ -956,6 +965,15 @@ def tx_fill(frames, offsets, *, out=None, stream=None, split=None, workspace=Non
                                            out.data_ptr(), _stream_handle(stream, frames)),
                "aipstack_chksum_tx_fill")
         return out
+    _split_call(lib, "aipstack_chksum_tx_fill_split", frames, n, stream, workspace,
+                lambda ws, ws_bytes, h: (frames.data_ptr(), offsets.data_ptr(), n,
+                                         out.data_ptr(), ws, ws_bytes, h))
+    return out
+
+
+def _split_call(lib, name, frames, n, stream, workspace, args):
+    """A split Tx fill (read pass + scatter pass through a workspace of 8 bytes per frame):
+    ``args(workspace_ptr, workspace_bytes, stream_handle)`` gives the entry point's arguments."""
     torch = _torch()
     need = int(lib.aipstack_chksum_tx_fill_workspace_bytes(max(n, 0)))
     if workspace is None:
@@ -967,14 +985,11 @@ def tx_fill(frames, offsets, *, out=None, stream=None, split=None, workspace=Non
     launch_stream = torch.cuda.current_stream(frames.device) if stream is None else stream
     if not hasattr(launch_stream, "cuda_stream"):  # a raw hipStream_t handle
         launch_stream = torch.cuda.ExternalStream(int(launch_stream), device=frames.device)
-    _check(lib.aipstack_chksum_tx_fill_split(frames.data_ptr(), offsets.data_ptr(), n,
-                                             out.data_ptr(), workspace.data_ptr(), ws_bytes,
-                                             _stream_handle(launch_stream)),
-           "aipstack_chksum_tx_fill_split")
+    _check(getattr(lib, name)(*args(workspace.data_ptr(), ws_bytes,
+                                    _stream_handle(launch_stream))), name)
     # The caching allocator must not hand the workspace out again before both passes on
     # the launch stream are done with it (it may not be torch's current stream).
     workspace.record_stream(launch_stream)
-    return out
 
 
 def tx_fill_records(frames, offsets, *, out=None, stream=None):

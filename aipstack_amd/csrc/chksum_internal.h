@@ -34,6 +34,11 @@ int device_cu_count(hipStream_t stream);
 // lines touched up front), else `family_default` for the kind of launch.
 int tuning_tx_header_mode(int family_default);
 
+// How the in-place Tx fills store the checksum fields (frame_kernels.hip FieldSectors): the
+// tunable "tx_store" (0 = 2-byte field stores, 1 = whole sectors), else `family_default`.
+constexpr int kTxStoreFields = 0, kTxStoreSectors = 1;
+int tuning_tx_store(int family_default);
+
 // The contract-violation word of each kernel translation unit on the current device:
 // OR it into *mask, clear it if `clear`.
 int take_violations_batch(uint32_t *mask, bool clear);

@@ -309,6 +309,8 @@ struct Tuning {
     std::atomic<int> tx_gather{-1};       // Tx header segments: 0 per-lane loads, 1 captured
                                           // from the stream, 2 captured + field lines
                                           // touched up front; else by kind of Tx launch
+    std::atomic<int> tx_store{-1};        // in-place Tx fills: 0 = 2-byte field stores, 1 =
+                                          // whole sectors; else the default
     // host engine (read when an engine is created, chksum_engine.cpp):
     std::atomic<int> engine_zero_copy{1};         // kernels read registered input in place
     std::atomic<int> engine_zero_copy_small{65536};  // pieces of at most this many packets
@@ -329,6 +331,7 @@ struct Tuning {
         env("AIPSTACK_CHKSUM_STREAM", stream);
         env("AIPSTACK_CHKSUM_CHUNK_PACKETS", chunk_packets);
         env("AIPSTACK_CHKSUM_TX_GATHER", tx_gather);
+        env("AIPSTACK_CHKSUM_TX_STORE", tx_store);
         env("AIPSTACK_ENGINE_ZERO_COPY", engine_zero_copy);
         env("AIPSTACK_ENGINE_ZERO_COPY_SMALL", engine_zero_copy_small);
         env("AIPSTACK_ENGINE_PAGEABLE_ROWS", engine_pageable_rows);
@@ -562,6 +565,11 @@ int tuning_tx_header_mode(int family_default) {
     return (t >= 0 && t <= 2) ? t : family_default;
 }
 
+int tuning_tx_store(int family_default) {
+    const int t = tuning().tx_store.load(std::memory_order_relaxed);
+    return (t == kTxStoreFields || t == kTxStoreSectors) ? t : family_default;
+}
+
 int tuning_frames_in_flight() {
     const int f = tuning().frames.load(std::memory_order_relaxed);
     return (f == 2 || f == 4 || f == 8) ? f : 4;
@@ -636,6 +644,7 @@ extern "C" int aipstack_chksum_tune(const char *key, int value) {
     else if (!std::strcmp(key, "stream")) t.stream = value;
     else if (!std::strcmp(key, "chunk_packets")) t.chunk_packets = value;
     else if (!std::strcmp(key, "tx_gather")) t.tx_gather = value;
+    else if (!std::strcmp(key, "tx_store")) t.tx_store = value;
     else if (!std::strcmp(key, "engine_zero_copy")) t.engine_zero_copy = value;
     else if (!std::strcmp(key, "engine_zero_copy_small")) t.engine_zero_copy_small = value;
     else if (!std::strcmp(key, "engine_pageable_rows")) t.engine_pageable_rows = value;

@@ -30,6 +30,12 @@ namespace {
 constexpr int kHdrSegs = 8;
 constexpr int kHdrDwords = 23;  // frame bytes [0, 92) realigned to the frame start
 constexpr uint32_t kHdrNeed = 97;
+constexpr uint64_t kMaxSlotStride = AIPSTACK_CHKSUM_MAX_SLOT_STRIDE;
+// The in-place Tx fills' field stores by default (tunable "tx_store", FieldSectors below).
+#ifndef AIPSTACK_TX_STORE_DEFAULT
+#define AIPSTACK_TX_STORE_DEFAULT 0
+#endif
+constexpr int kTxStoreDefault = AIPSTACK_TX_STORE_DEFAULT;
 
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) {
@@ -63,6 +69,21 @@ __device__ __forceinline__ void store_be16(uint64_t addr, uint32_t v) {
 #endif
 }
 
+// Sector stores (round 4, the in-place Tx fills' `SECT` form). A 2-byte field store makes a
+// partial 32-byte sector that the memory side has to merge with the bytes around it; the
+// lane holds those bytes already (its header blocks), so it writes each field's whole
+// sector instead -- the sector's bytes as read, the field patched in -- as two 16-byte
+// stores. Only sectors inside the frame's own bytes [S, E) are written whole (no byte of
+// another frame or of a slot's slack is ever rewritten). Every written field that overlaps a
+// whole-written sector, even by one byte, is patched into it; a field that no written sector
+// holds whole keeps its 2-byte store as well (the same value, so their order is free).
+// sec[0..1] = sector A (holding frame byte 24, the IPv4 checksum field's first), sec[2..3] =
+// sector B (holding the L4 field's first byte; not written when it is A).
+struct FieldSectors {
+    u32x4 sec[4];
+    uint32_t mode;  // bit 0: write A whole; bit 1: write B whole
+};
+
 // One frame's result, as the finish step produces it (lane j <-> frame j of the chunk):
 //   w0 = IPv4 header checksum (bits 0-15) | L4 checksum (16-31)
 //   w1 = L4 field offset from the frame start (0-7) | write the IPv4 field (8) | write the
@@ -71,6 +92,7 @@ __device__ __forceinline__ void store_be16(uint64_t addr, uint32_t v) {
 struct FrameOut {
     uint64_t S;  // frame start (absolute address)
     uint32_t w0, w1;
+    FieldSectors fs;  // SECT launches only
 };
 
 __device__ __forceinline__ uint32_t frame_w1(int fld, bool ip, bool l4, int status) {
@@ -89,6 +111,60 @@ __device__ __forceinline__ void store_frame(uint64_t S, uint32_t w0, uint32_t w1
     }
 }
 
+// The 16-bit value v written big-endian at byte b of a sector held as 8 little-endian
+// dwords (d[k] = sector bytes [4k, 4k + 4)); b = -1 or 31: only the byte inside the sector.
+// Branch-free over the 8 dwords.
+__device__ __forceinline__ void patch_be16(u32x4 &lo, u32x4 &hi, int b, uint32_t v) {
+    const uint32_t w = bswap16(v);  // low byte = the byte at b
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int p = b - 4 * k;  // the field's first byte within dword k (-1: its 2nd)
+        const uint32_t m = dword_keep(p, p + 2);
+        const uint32_t val = p >= 0 ? w << ((8 * p) & 31) : w >> 8;
+        if (k < 4)
+            lo[k] = (lo[k] & ~m) | (val & m);
+        else
+            hi[k - 4] = (hi[k - 4] & ~m) | (val & m);
+    }
+}
+
+// Sector stores of one frame (FieldSectors above): the written sectors whole, each with
+// every written field overlapping it patched in, and 2-byte stores of the fields no written
+// sector holds whole. The sector addresses are recomputed from S and fld.
+__device__ __forceinline__ void store_frame_sectors(uint64_t S, uint32_t w0, uint32_t w1,
+                                                    FieldSectors fs, uint8_t *__restrict__ status,
+                                                    uint64_t i) {
+    status[i] = (uint8_t)(w1 >> 16);
+    const bool wi = (w1 & 0x100u) != 0, wl = (w1 & 0x200u) != 0;
+    const uint64_t xi = S + 24, xl = S + (w1 & 0xFFu);
+    const uint64_t sa = xi & ~(uint64_t)31, sb = xl & ~(uint64_t)31;
+    // field positions relative to each sector (the first byte; -1 .. 31 = overlaps it)
+    const int ia = (int)(xi - sa), la = (int)(int64_t)(xl - sa);
+    const int ib = (int)(int64_t)(xi - sb), lb = (int)(xl - sb);
+    const bool wa = (fs.mode & 1u) != 0, wb = (fs.mode & 2u) != 0;
+    bool ci = false, cl = false;  // held whole by a written sector
+    if (wa) {
+        if (wi) patch_be16(fs.sec[0], fs.sec[1], ia, w0);
+        if (wl && la >= -1 && la <= 31) patch_be16(fs.sec[0], fs.sec[1], la, w0 >> 16);
+        ci = ia <= 30;
+        cl = la >= 0 && la <= 30;
+        u32x4 *p = reinterpret_cast<u32x4 *>(sa);
+        p[0] = fs.sec[0];
+        p[1] = fs.sec[1];
+    }
+    if (wb) {
+        if (wl) patch_be16(fs.sec[2], fs.sec[3], lb, w0 >> 16);
+        if (wi && ib >= -1 && ib <= 31) patch_be16(fs.sec[2], fs.sec[3], ib, w0);
+        cl = cl || lb <= 30;
+        ci = ci || (ib >= 0 && ib <= 30);
+        u32x4 *p = reinterpret_cast<u32x4 *>(sb);
+        p[0] = fs.sec[2];
+        p[1] = fs.sec[3];
+    }
+    if (wi && !ci) store_be16(xi, w0);
+    if (wl && !cl) store_be16(xl, w0 >> 16);
+}
+
 // Second pass of the split Tx fill: one frame per thread, the stores of every frame after
 // the whole read pass (stream-ordered behind frame_kernel<TX, ..., SPLIT>).
 __global__ __launch_bounds__(kBlock) void tx_scatter_kernel(uint64_t base,
@@ -100,6 +176,18 @@ __global__ __launch_bounds__(kBlock) void tx_scatter_kernel(uint64_t base,
     for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
         const uint64_t rec = records[i];
         store_frame<true>(base + offsets[i], (uint32_t)rec, (uint32_t)(rec >> 32), status, i);
+    }
+}
+
+// The same for ring slots: frame i starts at base + i * stride.
+__global__ __launch_bounds__(kBlock) void tx_scatter_slotted_kernel(uint64_t base, uint64_t stride,
+                                                                    const uint64_t *__restrict__ records,
+                                                                    uint8_t *__restrict__ status,
+                                                                    uint64_t n) {
+    const uint64_t step = (uint64_t)gridDim.x * kBlock;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += step) {
+        const uint64_t rec = records[i];
+        store_frame<true>(base + i * stride, (uint32_t)rec, (uint32_t)(rec >> 32), status, i);
     }
 }
 
@@ -386,6 +474,43 @@ __device__ __forceinline__ uint32_t l4s_below(const u32x4 (&seg)[kHdrSegs], uint
     return acc;
 }
 
+// The sectors of a frame's two checksum fields, taken from its header blocks right after
+// the parse (FieldSectors): sector A holds frame byte 24, B frame byte fld; A0 = S & ~15, so
+// A lies at segment 0..2 and B at segment 1..6 of the blocks, and both end inside them (the
+// blocks end on the first 32-byte boundary at or past frame byte 97).
+__device__ __forceinline__ FieldSectors pick_sectors(const u32x4 (&seg)[kHdrSegs], uint64_t S,
+                                                     uint64_t E, const FrameLane &fl) {
+    const uint64_t A0 = S & ~(uint64_t)15;
+    const uint64_t xi = S + 24, xl = S + (uint64_t)fl.fld;
+    const uint64_t ai = xi & ~(uint64_t)31, al = xl & ~(uint64_t)31;
+    const bool in_i = fl.ip_ok && ai >= S && ai + 32 <= E;
+    const bool in_l = fl.l4 && al >= S && al + 32 <= E && !(in_i && al == ai);
+    FieldSectors fs;
+    fs.mode = (in_i ? 1u : 0u) | (in_l ? 2u : 0u);
+    const uint32_t ia = (uint32_t)(ai - A0) >> 4, il = (uint32_t)(al - A0) >> 4;
+    fs.sec[0] = seg[0];
+    fs.sec[1] = seg[1];
+    fs.sec[2] = seg[1];
+    fs.sec[3] = seg[2];
+#pragma unroll
+    for (int i = 1; i <= 6; ++i) {
+        const uint32_t ma = i <= 2 && ia == (uint32_t)i ? ~0u : 0u;
+        const uint32_t mb = i >= 2 && il == (uint32_t)i ? ~0u : 0u;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            if (i <= 2) {
+                fs.sec[0][d] = blend(ma, fs.sec[0][d], seg[i][d]);
+                fs.sec[1][d] = blend(ma, fs.sec[1][d], seg[i + 1][d]);
+            }
+            if (i >= 2) {
+                fs.sec[2][d] = blend(mb, fs.sec[2][d], seg[i][d]);
+                fs.sec[3][d] = blend(mb, fs.sec[3][d], seg[i + 1][d]);
+            }
+        }
+    }
+    return fs;
+}
+
 // Rx verify / Tx fill of one 64-frame chunk (CSR offsets), lane j <-> frame j:
 //   (B) lane j loads frame j's first 112 aligned bytes (one buffer descriptor per chunk)
 //       and parses its headers (parse_lane): the L4 byte range, pseudo-header words and
@@ -412,7 +537,7 @@ __device__ __forceinline__ uint32_t l4s_below(const u32x4 (&seg)[kHdrSegs], uint
 //                field, so that the in-place field stores find those lines in the caches
 //                (split fill 168 vs 178 us, one pass 174 vs 186).
 constexpr int kHdrLoads = 0, kHdrCapture = 1, kHdrCaptureTouch = 2;
-template <class Desc, bool TX, int U, int P, bool NT, int SU, int GATHER>
+template <class Desc, bool TX, int U, int P, bool NT, int SU, int GATHER, bool SECT>
 __device__ __forceinline__ FrameOut process_chunk(const Desc &desc, uint64_t p0, uint64_t n,
                                                   uint32_t cpk, int lane, uint32_t voff,
                                                   uint32_t not_lane0, FrameLds *lds,
@@ -453,6 +578,8 @@ __device__ __forceinline__ FrameOut process_chunk(const Desc &desc, uint64_t p0,
                 hrsrc, 16u * i < hb_end && lane < cnt ? hoff + 16u * i : 0xFFFFFFF0u, 0u);
     };
     FrameLane fl;
+    FieldSectors fsec;
+    fsec.mode = 0;
     uint32_t r;
     bool streamed = false, have_headers = false;
     if constexpr (SU > 0) {
@@ -529,6 +656,7 @@ __device__ __forceinline__ FrameOut process_chunk(const Desc &desc, uint64_t p0,
             const uint32_t pn =
                 nm_n ? halves_below(lds->slots[min(cs_n, kHdrSlots - 1u)], (uint32_t)E & 15u) : 0u;
             fl = parse_lane<TX, true>(seg, S, len, hb_end);
+            if constexpr (SECT) fsec = pick_sectors(seg, S, E, fl);
             const bool use = act && fl.l4;
             // H(l4s): l4s lies in the own header blocks (l4s - A0 <= 89 < hb_end)
             const uint32_t h_s = hA[0] + l4s_below(seg, (uint32_t)(fl.l4s - A0));
@@ -568,6 +696,7 @@ __device__ __forceinline__ FrameOut process_chunk(const Desc &desc, uint64_t p0,
             StreamRun<SU, NT, AIPSTACK_FRAME_PREFETCH(SU)> run;
             run.begin(base, X1, voff);
             fl = parse_lane<TX, true>(seg, S, len, hb_end);
+            // (no sector stores here: their 16 VGPRs would live through the stream)
             // frames without an L4 sum (and lanes past the batch) put both at X1
             const bool use = lane < cnt && fl.l4;
             const uint64_t bs[2] = {use ? fl.l4s : X1, use ? fl.l4e : X1};
@@ -608,6 +737,9 @@ __device__ __forceinline__ FrameOut process_chunk(const Desc &desc, uint64_t p0,
     if (!streamed) {
         if (!have_headers) load_headers();
         fl = parse_lane<TX, false>(seg, S, len, hb_end);
+        // sector stores: ring slots (this is their only path), not the rare CSR chunks that
+        // are not back to back (16 more VGPRs through the per-frame loop)
+        if constexpr (SECT && !Desc::kStream) fsec = pick_sectors(seg, S, E, fl);
         const bool need = fl.ce != fl.cs;
         const LaneMeta meta = lane_meta(fl.cs, fl.ce);
         // (C) the remaining L4 bytes, one frame per wave, P frames' loads in flight
@@ -632,6 +764,7 @@ __device__ __forceinline__ FrameOut process_chunk(const Desc &desc, uint64_t p0,
     o.S = S;
     o.w0 = (fl.hchk & 0xFFFFu) | chk << 16;
     o.w1 = frame_w1(fl.fld, TX && fl.ip_ok, TX && fl.l4, v);
+    o.fs = fsec;
     return o;
 }
 
@@ -641,7 +774,7 @@ __device__ __forceinline__ FrameOut process_chunk(const Desc &desc, uint64_t p0,
 #ifndef AIPSTACK_FRAME_WAVES_PER_SIMD  // occupancy the register budget is fitted to
 #define AIPSTACK_FRAME_WAVES_PER_SIMD 4
 #endif
-template <class Desc, bool TX, int U, int P, bool NT, int SU, bool SPLIT, int GATHER>
+template <class Desc, bool TX, int U, int P, bool NT, int SU, bool SPLIT, int GATHER, bool SECT>
 __global__ __launch_bounds__(kBlock, AIPSTACK_FRAME_WAVES_PER_SIMD) void frame_kernel(Desc desc, uint64_t n,
                                                        uint32_t chunks_per_wave,
                                                        uint32_t chunk_packets,
@@ -662,7 +795,7 @@ __global__ __launch_bounds__(kBlock, AIPSTACK_FRAME_WAVES_PER_SIMD) void frame_k
     for (; c < c_end; ++c) {
         const uint64_t p0 = c * cpk;
         int cnt;
-        const FrameOut o = process_chunk<Desc, TX, U, P, NT, SU, GATHER>(
+        const FrameOut o = process_chunk<Desc, TX, U, P, NT, SU, GATHER, SECT>(
             desc, p0, n, (uint32_t)cpk, lane, voff, not_lane0, my, cnt);
         if (lane < cnt) {
             if constexpr (SPLIT)
@@ -671,13 +804,15 @@ __global__ __launch_bounds__(kBlock, AIPSTACK_FRAME_WAVES_PER_SIMD) void frame_k
 #else
                 records[p0 + lane] = (uint64_t)o.w0 | (uint64_t)o.w1 << 32;
 #endif
+            else if constexpr (SECT)
+                store_frame_sectors(o.S, o.w0, o.w1, o.fs, status, p0 + lane);
             else
                 store_frame<TX>(o.S, o.w0, o.w1, status, p0 + lane);
         }
     }
 }
 
-template <class Desc, bool TX, bool SPLIT, int GATHER>
+template <class Desc, bool TX, bool SPLIT, int GATHER, bool SECT = false>
 int launch_frames_g(const Desc &desc, uint64_t n, uint8_t *d_status, uint64_t *d_records,
                     hipStream_t stream, int cus) {
     // small batches: fewer frames per chunk, so that they spread over many waves (as the
@@ -699,7 +834,8 @@ int launch_frames_g(const Desc &desc, uint64_t n, uint8_t *d_status, uint64_t *d
     const uint64_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
     if (blocks > 0x7FFFFFFFull || cpw > 0xFFFFFFFFull) return AIPSTACK_CHKSUM_EINVAL;
 #define AIPSTACK_LAUNCH_FRAMES(P, SU)                                                          \
-    hipLaunchKernelGGL((frame_kernel<Desc, TX, 2, P, AIPSTACK_FRAME_NT != 0, SU, SPLIT, GATHER>), \
+    hipLaunchKernelGGL((frame_kernel<Desc, TX, 2, P, AIPSTACK_FRAME_NT != 0, SU, SPLIT, GATHER,  \
+                                     SECT>),                                                     \
                        dim3((unsigned)blocks), dim3(kBlock), 0, stream, desc, n, (uint32_t)cpw, \
                        cpk, d_status, d_records)
 #define AIPSTACK_LAUNCH_FRAMES_SU(P)                  \
@@ -736,6 +872,18 @@ int launch_frames(const void *d_base, const uint64_t *d_offsets, uint64_t n, uin
     if (cus <= 0) return AIPSTACK_CHKSUM_EHIP;
     CsrDesc desc{(uint64_t)(uintptr_t)d_base, d_offsets};
     int st;
+    if constexpr (TX && !SPLIT) {
+      if (tuning_tx_store(kTxStoreDefault) == kTxStoreSectors) {
+        // whole sectors need no line in the caches: captured headers, no touches by default
+        if (tuning_tx_header_mode(kHdrCapture) == kHdrCaptureTouch)
+            st = launch_frames_g<CsrDesc, true, false, kHdrCaptureTouch, true>(
+                desc, n, d_status, d_records, stream, cus);
+        else
+            st = launch_frames_g<CsrDesc, true, false, kHdrCapture, true>(
+                desc, n, d_status, d_records, stream, cus);
+        return st;
+      }
+    }
     if constexpr (TX) {
         const int mode = tuning_tx_header_mode(SPLIT && !scatter ? kHdrCapture : kHdrCaptureTouch);
         if (mode == kHdrCaptureTouch)
@@ -775,8 +923,20 @@ int launch_frames_slotted(const void *d_base, uint64_t slot_stride, const uint32
     desc.stride = slot_stride;
     desc.lens = d_len;
     desc.cap = (uint32_t)(slot_stride < AIPSTACK_CHKSUM_MAX_LEN ? slot_stride : AIPSTACK_CHKSUM_MAX_LEN);
-    return launch_frames_g<SlottedDesc, TX, SPLIT, kHdrLoads>(desc, n, d_status, d_records, stream,
-                                                             cus);
+    if constexpr (TX && !SPLIT) {
+        if (tuning_tx_store(kTxStoreDefault) == kTxStoreSectors)
+            return launch_frames_g<SlottedDesc, true, false, kHdrLoads, true>(desc, n, d_status,
+                                                                            d_records, stream, cus);
+    }
+    const int st = launch_frames_g<SlottedDesc, TX, SPLIT, kHdrLoads>(desc, n, d_status, d_records,
+                                                                     stream, cus);
+    if (st != AIPSTACK_CHKSUM_OK || !SPLIT || !d_status) return st;
+    // the split slotted fill's scatter pass (records pass above: d_status is null for the
+    // records-only call)
+    const uint64_t sblocks = min((n + kBlock - 1) / kBlock, (uint64_t)cus * 64);
+    hipLaunchKernelGGL(tx_scatter_slotted_kernel, dim3((unsigned)sblocks), dim3(kBlock), 0, stream,
+                       desc.base, slot_stride, d_records, d_status, n);
+    return check_hip(hipGetLastError());
 }
 
 int take_violations_frames(uint32_t *mask, bool clear) {
@@ -839,7 +999,8 @@ extern "C" int aipstack_chksum_rx_verify_slotted(const void *d_base, uint64_t sl
                                                  const uint32_t *d_len, uint64_t n,
                                                  uint8_t *d_verdict, void *stream) {
     if (n == 0) return AIPSTACK_CHKSUM_OK;
-    if (!d_base || !d_len || !d_verdict || slot_stride == 0 || n > (1ull << 40))
+    if (!d_base || !d_len || !d_verdict || slot_stride == 0 ||
+        slot_stride > kMaxSlotStride || n > (1ull << 40))
         return AIPSTACK_CHKSUM_EINVAL;
     return launch_frames_slotted<false, false>(d_base, slot_stride, d_len, n, d_verdict, nullptr,
                                                (hipStream_t)stream);
@@ -849,17 +1010,34 @@ extern "C" int aipstack_chksum_tx_fill_slotted(void *d_base, uint64_t slot_strid
                                                const uint32_t *d_len, uint64_t n,
                                                uint8_t *d_status, void *stream) {
     if (n == 0) return AIPSTACK_CHKSUM_OK;
-    if (!d_base || !d_len || !d_status || slot_stride == 0 || n > (1ull << 40))
+    if (!d_base || !d_len || !d_status || slot_stride == 0 ||
+        slot_stride > kMaxSlotStride || n > (1ull << 40))
         return AIPSTACK_CHKSUM_EINVAL;
     return launch_frames_slotted<true, false>(d_base, slot_stride, d_len, n, d_status, nullptr,
                                               (hipStream_t)stream);
+}
+
+extern "C" int aipstack_chksum_tx_fill_slotted_split(void *d_base, uint64_t slot_stride,
+                                                     const uint32_t *d_len, uint64_t n,
+                                                     uint8_t *d_status, void *d_workspace,
+                                                     uint64_t workspace_bytes, void *stream) {
+    if (n == 0) return AIPSTACK_CHKSUM_OK;
+    if (!d_base || !d_len || !d_status || !d_workspace || slot_stride == 0 ||
+        slot_stride > kMaxSlotStride || n > (1ull << 40) ||
+        workspace_bytes < aipstack_chksum_tx_fill_workspace_bytes(n) ||
+        ((uintptr_t)d_workspace & 7u) != 0)
+        return AIPSTACK_CHKSUM_EINVAL;
+    return launch_frames_slotted<true, true>(d_base, slot_stride, d_len, n, d_status,
+                                             static_cast<uint64_t *>(d_workspace),
+                                             (hipStream_t)stream);
 }
 
 extern "C" int aipstack_chksum_tx_fill_records_slotted(const void *d_base, uint64_t slot_stride,
                                                        const uint32_t *d_len, uint64_t n,
                                                        uint64_t *d_records, void *stream) {
     if (n == 0) return AIPSTACK_CHKSUM_OK;
-    if (!d_base || !d_len || !d_records || slot_stride == 0 || n > (1ull << 40) ||
+    if (!d_base || !d_len || !d_records || slot_stride == 0 ||
+        slot_stride > kMaxSlotStride || n > (1ull << 40) ||
         ((uintptr_t)d_records & 7u) != 0)
         return AIPSTACK_CHKSUM_EINVAL;
     return launch_frames_slotted<true, true>(d_base, slot_stride, d_len, n, nullptr, d_records,

@@ -46,6 +46,10 @@ extern "C" {
 /* Largest packet length the reference admits (Chksum.h:73-74). */
 #define AIPSTACK_CHKSUM_MAX_LEN 65535u
 
+/* Largest slot stride of the frame batches on ring slots (their 64-frame header window must
+ * span at most 4 MiB); a larger one is _EINVAL. */
+#define AIPSTACK_CHKSUM_MAX_SLOT_STRIDE 65536u
+
 /* ---- flags for the batch entry points ------------------------------------------ */
 /* Write IpChksum (= ~IpChksumInverted, Chksum.h:122-125) instead of the inverted sum. */
 #define AIPSTACK_CHKSUM_FINAL 1u
@@ -181,14 +185,20 @@ int aipstack_chksum_tx_fill_records(const void *d_base, const uint64_t *d_offset
                                     uint64_t *d_records, void *stream);
 
 /* The frame batches on a ring of slots (layout as aipstack_chksum_batch_slotted: frame i is
- * the d_len[i] bytes at d_base + i*slot_stride, slot_stride <= 65536, n whole slots): Rx
- * verify, the one-pass in-place Tx fill, and the Tx records. Same results per frame as the
- * CSR forms. */
+ * the d_len[i] bytes at d_base + i*slot_stride, 0 < slot_stride <=
+ * AIPSTACK_CHKSUM_MAX_SLOT_STRIDE, else _EINVAL; n whole slots): Rx verify, the one-pass
+ * in-place Tx fill, the split fill (records pass + scatter pass through a caller-owned
+ * workspace, as aipstack_chksum_tx_fill_split), and the Tx records. Same results per frame as
+ * the CSR forms. */
 int aipstack_chksum_rx_verify_slotted(const void *d_base, uint64_t slot_stride,
                                       const uint32_t *d_len, uint64_t n, uint8_t *d_verdict,
                                       void *stream);
 int aipstack_chksum_tx_fill_slotted(void *d_base, uint64_t slot_stride, const uint32_t *d_len,
                                     uint64_t n, uint8_t *d_status, void *stream);
+int aipstack_chksum_tx_fill_slotted_split(void *d_base, uint64_t slot_stride,
+                                          const uint32_t *d_len, uint64_t n, uint8_t *d_status,
+                                          void *d_workspace, uint64_t workspace_bytes,
+                                          void *stream);
 int aipstack_chksum_tx_fill_records_slotted(const void *d_base, uint64_t slot_stride,
                                             const uint32_t *d_len, uint64_t n,
                                             uint64_t *d_records, void *stream);
@@ -391,8 +401,12 @@ int aipstack_chksum_device_check(int device);
  * in memory, or chain chunks that lie close together: 2, 4, 8; -1 turns stream mode off,
  * so every packet, frame or chunk is summed on its own), "chunk_packets" (packets, frames
  * or chains per wave chunk: 1, 2, 4, ..., 64; automatic = 64, fewer for small batches so
- * that they spread over more waves). Process-wide; results never depend on them. Returns
- * _OK or _EINVAL for an unknown key. */
+ * that they spread over more waves), "tx_gather" (where the Tx fills take their header
+ * segments: 0 per-lane loads, 1 captured from the stream, 2 captured + the two field lines
+ * touched up front; -1 = by kind of launch), "tx_store" (how the in-place Tx fills write the
+ * two checksum fields: 0 = 2-byte stores, 1 = the fields' whole 32-byte sectors from the header
+ * bytes the kernel holds; -1 = the default). Process-wide; results never depend on them.
+ * Returns _OK or _EINVAL for an unknown key. */
 int aipstack_chksum_tune(const char *key, int value);
 
 /* The launch shape the batch entry points pick for n packets on a device with `cus` compute

@@ -1027,11 +1027,21 @@ def test_rx_verify_edge_frames(oracle, stream_mode, shift, su):
     assert np.all(np.bincount(want, minlength=9) > 0)
 
 
+@pytest.fixture
+def tx_store():
+    """Setter for the tx_store tunable (0 = 2-byte field stores, 1 = whole sectors, -1 =
+    the default); restores the default afterwards."""
+    yield lambda v: _tune("tx_store", v)
+    _tune("tx_store", -1)
+
+
+@pytest.mark.parametrize("store", [0, 1])
 @pytest.mark.parametrize("split", [False, True])
 @pytest.mark.parametrize("su", [0, 2, -1])
 @pytest.mark.parametrize("shift", [0, 3])
-def test_tx_fill_edge_frames(oracle, stream_mode, shift, su, split):
+def test_tx_fill_edge_frames(oracle, stream_mode, tx_store, shift, su, split, store):
     stream_mode(su)
+    tx_store(store)
     buf, off = _edge_frames(7 + shift, 3000)
     big = np.zeros(buf.size + shift, dtype=np.uint8)
     big[shift:] = buf
@@ -1087,6 +1097,85 @@ def test_slotted_full_size_1m(oracle):
     want = oracle.rx_verify_slotted(fring, 2048, flens)
     assert np.array_equal(v, want), np.nonzero(v != want)[0][:10]
     assert np.array_equal(want, oracle.rx_verify_batch(fr, foff))  # same verdicts as CSR
+
+
+@pytest.mark.parametrize("gather", [1, 2])
+@pytest.mark.parametrize("su", [0, -1])
+def test_tx_fill_sector_stores_every_alignment(oracle, stream_mode, tx_gather, tx_store, su,
+                                              gather):
+    """The in-place fill's sector stores (tx_store = 1): the batch starts at each of the 32
+    byte offsets of a sector, so both fields' sectors meet every position (inside the frame,
+    straddling its start, a field at byte 31); short frames keep 2-byte stores; the bytes
+    around the fields, and the frames' neighbours, are rewritten unchanged."""
+    stream_mode(su)
+    tx_gather(gather)
+    tx_store(1)
+    buf, off = _edge_frames(5150, 2000)
+    for shift in range(32):
+        big = synth.random_bytes(shift + 1, buf.size + shift + 64)
+        big[shift:shift + buf.size] = buf
+        dbig = _d(big)
+        st = _np(A.tx_fill(dbig, _d(off + np.uint64(shift)), split=False))
+        want = big.copy()
+        want_st = oracle.tx_fill_batch(want[shift:shift + buf.size], off)
+        assert np.array_equal(st, want_st), shift
+        got = _np(dbig)
+        assert np.array_equal(got, want), (shift, np.nonzero(got != want)[0][:10])
+
+
+@pytest.mark.parametrize("store,split", [(0, False), (1, False), (0, True)])
+@pytest.mark.parametrize("base", [0, 8, 21])
+@pytest.mark.parametrize("stride", [1601, 2048])
+def test_slotted_tx_fill_store_forms(oracle, tx_store, stride, base, store, split):
+    """The send ring's fill forms: one pass with 2-byte or sector field stores, and the split
+    slotted fill (aipstack_chksum_tx_fill_slotted_split), at slot starts of every alignment an
+    odd stride or a shifted base gives; filled, untouched and slack bytes all as the oracle's."""
+    tx_store(store)
+    buf, off = synth.frames_host(20000, seed=stride + base, max_payload=1460)
+    ring, lens = synth.to_slots(buf, off, stride, slack_seed=base + 1)
+    big = synth.random_bytes(base + 5, ring.size + base + 16)
+    big[base:base + ring.size] = ring
+    dbig = _d(big)
+    st = _np(A.tx_fill_slotted(dbig[base:base + ring.size], stride, _d(lens.view(np.int32)),
+                               split=split))
+    want = big.copy()
+    want_st = oracle.tx_fill_slotted(want[base:base + ring.size], stride, lens)
+    assert np.array_equal(st, want_st)
+    got = _np(dbig)
+    assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
+
+
+def test_slotted_frame_stride_limit(oracle):
+    """The frame batches on slots take slot_stride <= AIPSTACK_CHKSUM_MAX_SLOT_STRIDE (their
+    64-frame header window spans at most 4 MiB): 65536 works, 65537 is _EINVAL for every
+    slotted frame entry point."""
+    import torch
+    from aipstack_amd import _lib
+    lib = _lib.load()
+    buf, off = synth.frames_host(70, seed=3, max_payload=1460)
+    ring, lens = synth.to_slots(buf, off, 65536)
+    want = ring.copy()
+    want_st = oracle.tx_fill_slotted(want, 65536, lens)
+    dring = _d(ring)
+    st = _np(A.tx_fill_slotted(dring, 65536, _d(lens.view(np.int32))))
+    assert np.array_equal(st, want_st) and np.array_equal(_np(dring), want)
+    v = _np(A.rx_verify_slotted(dring, 65536, _d(lens.view(np.int32))))
+    assert np.array_equal(v, oracle.rx_verify_slotted(want, 65536, lens))
+    big = torch.zeros(70 * 65537, dtype=torch.uint8, device=DEV)
+    dl = _d(np.full(70, 60, dtype=np.int32))
+    out = torch.empty(70, dtype=torch.uint8, device=DEV)
+    rec = torch.empty(70, dtype=torch.int64, device=DEV)
+    ws = torch.empty(8 * 70, dtype=torch.uint8, device=DEV)
+    s = 0
+    for st in (lib.aipstack_chksum_rx_verify_slotted(big.data_ptr(), 65537, dl.data_ptr(), 70,
+                                                      out.data_ptr(), s),
+               lib.aipstack_chksum_tx_fill_slotted(big.data_ptr(), 65537, dl.data_ptr(), 70,
+                                                   out.data_ptr(), s),
+               lib.aipstack_chksum_tx_fill_records_slotted(big.data_ptr(), 65537, dl.data_ptr(),
+                                                           70, rec.data_ptr(), s),
+               lib.aipstack_chksum_tx_fill_slotted_split(big.data_ptr(), 65537, dl.data_ptr(), 70,
+                                                         out.data_ptr(), ws.data_ptr(), 8 * 70, s)):
+        assert st == A.AIPSTACK_CHKSUM_EINVAL
 
 
 @pytest.mark.parametrize("stride", [1600, 2048, 4096])

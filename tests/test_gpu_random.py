@@ -27,6 +27,11 @@ def _np(t):
     return t.cpu().numpy()
 
 
+def _tune(key, value):
+    from aipstack_amd import _lib
+    assert _lib.load().aipstack_chksum_tune(key.encode(), value) == A.AIPSTACK_CHKSUM_OK
+
+
 def _blob(rng, nbytes):
     """Random bytes with runs of 0x00 and 0xFF (the reference's zero rule and its all-ones
     known answer) and runs of one repeated word."""
@@ -138,10 +143,15 @@ def test_random_frames(oracle, seed):
     fr, off = synth.frames_host(n, seed=4000 + seed, max_payload=int(rng.choice([0, 46, 600, 1460, 8000])))
     want = fr.copy()
     want_st = oracle.tx_fill_batch(want, off)
-    for split in (False, True):
-        d = _d(fr)
-        st = _np(A.tx_fill(d, _d(off), split=split))
-        assert np.array_equal(st, want_st) and np.array_equal(_np(d), want), (seed, split)
+    store = int(rng.integers(0, 2))  # in-place field stores: 2-byte (0) or whole sectors (1)
+    _tune("tx_store", store)
+    try:
+        for split in (False, True):
+            d = _d(fr)
+            st = _np(A.tx_fill(d, _d(off), split=split))
+            assert np.array_equal(st, want_st) and np.array_equal(_np(d), want), (seed, split)
+    finally:
+        _tune("tx_store", -1)
     # corrupt a random fraction of the filled frames, then verify
     bad = want.copy()
     for i in np.nonzero(rng.random(n) < 0.2)[0]:
@@ -160,7 +170,12 @@ def test_random_frames(oracle, seed):
         got = _np(A.rx_verify_slotted(_d(ring), stride, _d(lens.view(np.int32))))
         assert np.array_equal(got, oracle.rx_verify_slotted(ring, stride, lens)), (seed, stride)
         dr = _d(ring)
-        st = _np(A.tx_fill_slotted(dr, stride, _d(lens.view(np.int32))))
+        split = bool(rng.integers(0, 2))
+        _tune("tx_store", store)
+        try:
+            st = _np(A.tx_fill_slotted(dr, stride, _d(lens.view(np.int32)), split=split))
+        finally:
+            _tune("tx_store", -1)
         wr = ring.copy()
-        assert np.array_equal(st, oracle.tx_fill_slotted(wr, stride, lens)), (seed, stride)
-        assert np.array_equal(_np(dr), wr), (seed, stride)
+        assert np.array_equal(st, oracle.tx_fill_slotted(wr, stride, lens)), (seed, stride, split)
+        assert np.array_equal(_np(dr), wr), (seed, stride, split)
