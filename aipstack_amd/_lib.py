@@ -79,6 +79,24 @@ SIGNATURES = {
     "aipstack_chksum_engine_group_size": (_c_int, [_c_vp]),
     "aipstack_chksum_engine_group_register": (_c_int, [_c_vp, _c_vp, _c_u64]),
     "aipstack_chksum_engine_group_unregister": (_c_int, [_c_vp, _c_vp]),
+    "aipstack_chksum_engine_group_engine": (_c_vp, [_c_vp, _c_int]),
+    "aipstack_chksum_engine_group_region_mapped": (_c_int, [_c_vp, _c_vp]),
+    "aipstack_chksum_engine_group_submit_strided": (_c_int, [_c_vp, _c_vp, _c_u64, _c_u32, _c_u64, _c_vp,
+                                                             _c_u32, _c_vp]),
+    "aipstack_chksum_engine_group_submit_csr": (_c_int, [_c_vp, _c_vp, _c_vp, _c_u64, _c_vp, _c_u32, _c_vp]),
+    "aipstack_chksum_engine_group_submit_rx_verify": (_c_int, [_c_vp, _c_vp, _c_vp, _c_u64, _c_vp, _c_vp]),
+    "aipstack_chksum_engine_group_submit_tx_fill": (_c_int, [_c_vp, _c_vp, _c_vp, _c_u64, _c_vp, _c_vp]),
+    "aipstack_chksum_engine_group_submit_slotted": (_c_int, [_c_vp, _c_vp, _c_u64, _c_vp, _c_u64, _c_vp,
+                                                             _c_u32, _c_vp]),
+    "aipstack_chksum_engine_group_submit_rx_verify_slotted": (_c_int, [_c_vp, _c_vp, _c_u64, _c_vp,
+                                                                       _c_u64, _c_vp, _c_vp]),
+    "aipstack_chksum_engine_group_submit_tx_fill_slotted": (_c_int, [_c_vp, _c_vp, _c_u64, _c_vp,
+                                                                     _c_u64, _c_vp, _c_vp]),
+    "aipstack_chksum_engine_group_poll": (_c_int, [_c_vp, _c_u64, _c_vp]),
+    "aipstack_chksum_engine_group_wait": (_c_int, [_c_vp, _c_u64, _c_vp]),
+    "aipstack_chksum_source_digest": (ctypes.c_char_p, []),
+    "aipstack_chksum_engine_locality": (_c_int, [_c_vp, _c_vp, _c_vp]),
+    "aipstack_chksum_engine_region_mapped": (_c_int, [_c_vp, _c_vp]),
     "aipstack_chksum_engine_group_host_strided": (_c_int, [_c_vp, _c_vp, _c_u64, _c_u32, _c_u64, _c_vp,
                                                            _c_u32, _c_vp]),
     "aipstack_chksum_engine_group_host_csr": (_c_int, [_c_vp, _c_vp, _c_vp, _c_u64, _c_vp, _c_u32, _c_vp]),
@@ -122,3 +140,24 @@ def load() -> ctypes.CDLL:
         raise ImportError("aipstack_amd: library ABI version mismatch")
     _lib = lib
     return lib
+
+
+def tree_source_digest(package_dir: str = _HERE) -> str:
+    """The digest aipstack_chksum_source_digest() reports, recomputed from the source tree
+    (the files and order of the Makefile's DIGEST_SRCS; `package_dir` = the aipstack_amd
+    directory whose csrc/ and ../include/ are read): equal iff the loaded library was built
+    from the sources beside it."""
+    import glob
+    import hashlib
+    csrc = os.path.join(package_dir, "csrc")
+    names = []
+    for pat in ("*.hip", "*.cpp", "*.cc", "*.h"):
+        names += [os.path.basename(p) for p in glob.glob(os.path.join(csrc, pat))]
+    names += [os.path.relpath(p, csrc) for p in
+              glob.glob(os.path.join(package_dir, "..", "include", "aipstack_amd", "*.h"))]
+    names.append("Makefile")
+    h = hashlib.sha256()
+    for n in sorted(set(names)):
+        with open(os.path.join(csrc, n), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()

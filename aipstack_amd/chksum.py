@@ -557,6 +557,14 @@ class ChksumEngine:
             raise ChksumError(st, where)
         self._keep(ticket, *arrays)
 
+    def locality(self):
+        """(NUMA node of the device or -1, CPUs the engine's host threads are pinned to)."""
+        node, cpus = ctypes.c_int(-1), ctypes.c_int(0)
+        _check(self._lib.aipstack_chksum_engine_locality(self._h, ctypes.byref(node),
+                                                         ctypes.byref(cpus)),
+               "aipstack_chksum_engine_locality")
+        return node.value, cpus.value
+
     def poll(self, ticket: int) -> bool:
         """True once batch `ticket` is complete (its `out` filled); False while running."""
         st = self._lib.aipstack_chksum_engine_poll(self._h, ticket)
@@ -626,6 +634,9 @@ class ChksumEngine:
         `status` written when the batch completes (wait / poll); `frames` must not be
         touched until then."""
         o, n, status = self._tx_args(frames, offsets, status)
+        # the completion reads the offsets again (it writes the fields into the frames, on
+        # the engine's applier thread): a private copy, so the caller may reuse its array
+        o = o.copy()
         t = ctypes.c_uint64(0)
         st = self._lib.aipstack_chksum_engine_submit_tx_fill(
             self._h, frames.ctypes.data, o.ctypes.data, max(n, 0), status.ctypes.data,
@@ -735,8 +746,10 @@ class ChksumEngine:
 class ChksumEngineGroup:
     """Several devices behind one host-memory batch in ONE process (C-ABI
     ``aipstack_chksum_engine_group_*``): one engine per entry of ``devices`` (repeats
-    allowed), each batch split into contiguous ranges of about equal bytes run concurrently,
-    one host thread per engine. ``last_status`` holds each engine's status of the last call."""
+    allowed), each batch split into contiguous ranges of about equal bytes run concurrently
+    (small batches go whole to one device, round robin). The synchronous calls return the
+    results; ``submit_*`` return ``(ticket, out)`` at once, ``poll`` / ``wait`` complete a
+    ticket. ``last_status`` holds each engine's status of the last completed call."""
 
     def __init__(self, devices, chunk_bytes: int = 0, nstreams: int = 4):
         self._lib = _lib.load()
@@ -748,13 +761,15 @@ class ChksumEngineGroup:
         self._h = h
         self.size = len(devices)
         self._registered = []
+        self._inflight = {}
         self.last_status = [0] * self.size
 
     def close(self) -> None:
         if self._h:
-            self._lib.aipstack_chksum_engine_group_destroy(self._h)
+            self._lib.aipstack_chksum_engine_group_destroy(self._h)  # completes every batch
             self._h = None
             self._registered = []
+            self._inflight = {}
 
     def __enter__(self):
         return self
@@ -784,6 +799,117 @@ class ChksumEngineGroup:
         st = getattr(self._lib, fn)(self._h, *args, ds)
         self.last_status = list(ds)
         _check(st, where)
+
+    def _submit(self, fn, arrays, *args):
+        """A submit_* C call; the arrays of the batch stay referenced until it completes."""
+        t = ctypes.c_uint64(0)
+        st = getattr(self._lib, fn)(self._h, *args, ctypes.byref(t))
+        if st != AIPSTACK_CHKSUM_OK:
+            if t.value:  # ranges already enqueued still read (and, Tx, write) the arrays
+                self._lib.aipstack_chksum_engine_group_wait(self._h, t.value, None)
+            raise ChksumError(st, fn)
+        self._inflight[t.value] = arrays
+        return t.value
+
+    def poll(self, ticket: int) -> bool:
+        """True once group batch `ticket` is complete; False while a device still works."""
+        ds = (ctypes.c_int * self.size)()
+        st = self._lib.aipstack_chksum_engine_group_poll(self._h, ticket, ds)
+        if st == 1:
+            return False
+        self._inflight.pop(ticket, None)
+        self.last_status = list(ds)
+        _check(st, "aipstack_chksum_engine_group_poll")
+        return True
+
+    def wait(self, ticket: int) -> None:
+        """Block until group batch `ticket` is complete."""
+        ds = (ctypes.c_int * self.size)()
+        st = self._lib.aipstack_chksum_engine_group_wait(self._h, ticket, ds)
+        self._inflight.pop(ticket, None)
+        self.last_status = list(ds)
+        _check(st, "aipstack_chksum_engine_group_wait")
+
+    def locality(self):
+        """Per engine: (NUMA node of its device or -1, CPUs its host threads are pinned to)."""
+        out = []
+        for k in range(self.size):
+            e = self._lib.aipstack_chksum_engine_group_engine(self._h, k)
+            node, cpus = ctypes.c_int(-1), ctypes.c_int(0)
+            _check(self._lib.aipstack_chksum_engine_locality(e, ctypes.byref(node),
+                                                             ctypes.byref(cpus)),
+                   "aipstack_chksum_engine_locality")
+            out.append((node.value, cpus.value))
+        return out
+
+    def region_mapped(self, arr: np.ndarray) -> bool:
+        """Whether every device's kernels read the registered `arr` in place (zero copy)."""
+        st = self._lib.aipstack_chksum_engine_group_region_mapped(self._h, arr.ctypes.data)
+        _check(min(st, 0), "aipstack_chksum_engine_group_region_mapped")
+        return st == 1
+
+    def submit_strided(self, buf, stride: int, length: int, n: int, *, out=None, final=False):
+        if n and (n - 1) * stride + length > buf.nbytes:
+            raise ValueError("batch exceeds buf")
+        out = ChksumEngine._host_args(buf, out, n)
+        t = self._submit("aipstack_chksum_engine_group_submit_strided", (buf, out),
+                         buf.ctypes.data, stride, length, n, out.ctypes.data,
+                         AIPSTACK_CHKSUM_FINAL if final else 0)
+        return t, out
+
+    def submit_csr(self, buf, offsets, *, out=None, final=False):
+        o = _host_u64(offsets)
+        n = o.size - 1
+        if n > 0 and int(o[-1]) > buf.nbytes:
+            raise ValueError("offsets exceed buf")
+        out = ChksumEngine._host_args(buf, out, n)
+        t = self._submit("aipstack_chksum_engine_group_submit_csr", (buf, o, out),
+                         buf.ctypes.data, o.ctypes.data, max(n, 0), out.ctypes.data,
+                         AIPSTACK_CHKSUM_FINAL if final else 0)
+        return t, out
+
+    def submit_rx_verify(self, frames, offsets, *, out=None):
+        o = _host_u64(offsets)
+        n = o.size - 1
+        if n > 0 and int(o[-1]) > frames.nbytes:
+            raise ValueError("offsets exceed frames")
+        out = ChksumEngine._host_args(frames, out, n, np.uint8)
+        t = self._submit("aipstack_chksum_engine_group_submit_rx_verify", (frames, o, out),
+                         frames.ctypes.data, o.ctypes.data, max(n, 0), out.ctypes.data)
+        return t, out
+
+    def submit_tx_fill(self, frames, offsets, *, status=None):
+        o, n, status = ChksumEngine._tx_args(frames, offsets, status)
+        o = o.copy()  # read again when the fields are applied (see ChksumEngine.submit_tx_fill)
+        t = self._submit("aipstack_chksum_engine_group_submit_tx_fill", (frames, o, status),
+                         frames.ctypes.data, o.ctypes.data, max(n, 0), status.ctypes.data)
+        return t, status
+
+    def submit_slotted(self, buf, slot_stride: int, lens, *, out=None, final=False):
+        ln, n = ChksumEngine._slot_args(buf, slot_stride, lens)
+        out = ChksumEngine._host_args(buf, out, n)
+        t = self._submit("aipstack_chksum_engine_group_submit_slotted", (buf, ln, out),
+                         buf.ctypes.data, slot_stride, ln.ctypes.data, n, out.ctypes.data,
+                         AIPSTACK_CHKSUM_FINAL if final else 0)
+        return t, out
+
+    def submit_rx_verify_slotted(self, frames, slot_stride: int, lens, *, out=None):
+        ln, n = ChksumEngine._slot_args(frames, slot_stride, lens)
+        out = ChksumEngine._host_args(frames, out, n, np.uint8)
+        t = self._submit("aipstack_chksum_engine_group_submit_rx_verify_slotted",
+                         (frames, ln, out), frames.ctypes.data, slot_stride, ln.ctypes.data, n,
+                         out.ctypes.data)
+        return t, out
+
+    def submit_tx_fill_slotted(self, frames, slot_stride: int, lens, *, status=None):
+        if not frames.flags.writeable:
+            raise ValueError("frames must be writable (filled in place)")
+        ln, n = ChksumEngine._slot_args(frames, slot_stride, lens)
+        status = ChksumEngine._host_args(frames, status, n, np.uint8)
+        t = self._submit("aipstack_chksum_engine_group_submit_tx_fill_slotted",
+                         (frames, ln, status), frames.ctypes.data, slot_stride, ln.ctypes.data,
+                         n, status.ctypes.data)
+        return t, status
 
     def strided(self, buf, stride: int, length: int, n: int, *, out=None, final=False):
         if n and (n - 1) * stride + length > buf.nbytes:

@@ -29,6 +29,17 @@
 // is completed by _poll / _wait, so a failure is never reported for, nor hidden from,
 // another batch. Destroy completes every piece still in flight as _wait would (results
 // delivered, Tx fields applied) before it frees anything.
+//
+// Locking (round 4): `submit_mu` serialises the submits (and register / unregister, which
+// change what a submit reads); `mu` guards the slots' bookkeeping, the failure records and
+// the ticket counter, and is only ever held for short bookkeeping -- never while the host
+// waits for a GPU piece (a back-pressured submit, _wait), copies pageable input into staging
+// or waits for the Tx applier. So _poll from the receive loop's other thread always answers
+// at once.
+//
+// Host threads (round 4): a persistent pool per engine (host_threads.h), pinned with the
+// applier thread to the CPUs next to the device; the pinned staging is allocated from those
+// CPUs too, so that its pages sit on the device's NUMA node.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -49,6 +60,7 @@
 
 #include "aipstack_amd/chksum.h"
 #include "chksum_internal.h"
+#include "host_threads.h"
 
 using namespace aipstack_amd;
 
@@ -167,15 +179,19 @@ struct aipstack_chksum_engine {
     uint64_t zero_copy_max = 65536;  // metadata in pinned staging for pieces up to this
     bool pageable_rows = true;  // pageable ring slots: frame bytes staged, read in place
     std::vector<Slot> slots;
-    std::vector<Region> registered;
-    size_t next_slot = 0;      // round robin over the slots, across batches
-    uint64_t next_ticket = 1;  // tickets are never 0
-    uint64_t pieces = 0;       // pieces enqueued so far (Slot::seq)
+    std::vector<Region> registered;  // changed under submit_mu (and mu)
+    size_t next_slot = 0;      // round robin over the slots, across batches (submit_mu)
+    uint64_t next_ticket = 1;  // tickets are never 0 (mu)
+    uint64_t submitting = 0;   // the ticket whose submit is running (mu): not complete yet
+    uint64_t pieces = 0;       // pieces enqueued so far (Slot::seq; submit_mu)
     // tickets with a failed piece -> the first failure's status, until the ticket is
     // completed (poll / wait) or the engine is destroyed
     std::map<uint64_t, int> failed;
-    std::mutex mu;  // serialises the calls on one engine
+    std::mutex submit_mu;  // serialises the submits, register and unregister
+    std::mutex mu;         // the slots' bookkeeping, failures, tickets: short sections only
     std::unique_ptr<Applier> applier;  // Tx record apply, off the submitting thread
+    DeviceLocality loc;    // the device's NUMA node and local CPUs
+    HostPool pool;         // pinned host workers: staging copies, Tx record applies
     Stats stats;
 };
 
@@ -202,9 +218,12 @@ const char *mapped_address(const void *host_ptr) {
 // Test builds only (tests/cpp): make chosen pieces fail, at their launch or at their
 // completion, as a HIP error would. Bit k-1 of a mask = piece k (Slot::seq), k <= 64.
 std::atomic<uint64_t> g_fail_at_launch{0}, g_fail_at_completion{0};
-std::atomic<uint64_t> g_wait_delay_us{0};  // _wait sleeps this long outside the engine lock
-bool injected(const std::atomic<uint64_t> &mask, uint64_t seq) {
-    return seq >= 1 && seq <= 64 && ((mask.load() >> (seq - 1)) & 1u);
+std::atomic<uint64_t> g_wait_delay_us{0};  // _wait and a back-pressured submit sleep this
+                                           // long outside the engine lock
+std::atomic<const aipstack_chksum_engine *> g_fail_engine{nullptr};  // null: every engine
+bool injected(const aipstack_chksum_engine *e, const std::atomic<uint64_t> &mask, uint64_t seq) {
+    const aipstack_chksum_engine *only = g_fail_engine.load();
+    return (!only || only == e) && seq >= 1 && seq <= 64 && ((mask.load() >> (seq - 1)) & 1u);
 }
 #endif
 
@@ -231,8 +250,8 @@ void release(aipstack_chksum_engine *e) {
         if (r.owned) (void)hipHostUnregister(const_cast<char *>(r.p));
 }
 
-// Host threads the engine may use for one piece's Tx records / pageable staging copy
-// (AIPSTACK_ENGINE_HOST_THREADS, default 8; read once).
+// Host threads the engine uses for one piece's Tx records / pageable staging copy, the caller
+// included (AIPSTACK_ENGINE_HOST_THREADS, default 8; read once): the pool holds one fewer.
 unsigned host_threads_cap() {
     static const unsigned cap = [] {
         const char *v = std::getenv("AIPSTACK_ENGINE_HOST_THREADS");
@@ -242,31 +261,24 @@ unsigned host_threads_cap() {
     return cap;
 }
 
+// Parts a piece's host work is split into: one per `per_part_min` units, at most the pool's
+// threads plus the caller.
+unsigned host_parts(const HostPool &pool, uint64_t units, uint64_t per_part_min) {
+    return (unsigned)std::max<uint64_t>(
+        1, std::min<uint64_t>(units / per_part_min, pool.workers() + 1u));
+}
+
 // Pageable input into pinned staging: one core copies ~20 GB/s, below the PCIe link the
-// DMA then feeds, so large pieces are copied by several threads over disjoint 4 KiB-aligned
+// DMA then feeds, so large pieces are copied by the pool over disjoint 4 KiB-aligned
 // ranges (the previous piece's DMA runs meanwhile).
-void stage_copy(void *dst, const void *src, uint64_t bytes) {
-    constexpr uint64_t kPerThreadMin = 4ull << 20;
-    const unsigned hw = std::thread::hardware_concurrency();
-    const uint64_t want = bytes / kPerThreadMin;
-    const unsigned nt = (unsigned)std::min<uint64_t>(std::min<uint64_t>(want, host_threads_cap()),
-                                                     hw ? hw : 1);
-    if (nt <= 1) {
-        std::memcpy(dst, src, bytes);
-        return;
-    }
+void stage_copy(HostPool &pool, void *dst, const void *src, uint64_t bytes) {
+    const unsigned nt = host_parts(pool, bytes, 4ull << 20);
     const uint64_t per = ((bytes + nt - 1) / nt + 4095) & ~4095ull;
-    std::vector<std::thread> pool;
-    pool.reserve(nt);
-    for (unsigned t = 0; t < nt; ++t) {
-        const uint64_t lo = (uint64_t)t * per;
-        if (lo >= bytes) break;
+    pool.run(nt, [=](unsigned t) {
+        const uint64_t lo = std::min((uint64_t)t * per, bytes);
         const uint64_t len = std::min(per, bytes - lo);
-        pool.emplace_back([=] {
-            std::memcpy(static_cast<char *>(dst) + lo, static_cast<const char *>(src) + lo, len);
-        });
-    }
-    for (std::thread &t : pool) t.join();
+        std::memcpy(static_cast<char *>(dst) + lo, static_cast<const char *>(src) + lo, len);
+    });
 }
 
 // Tx fill from host memory: write the checksum fields (big-endian) of frames [lo, hi) of a
@@ -299,30 +311,19 @@ void apply_tx_range(const uint64_t *rec, char *frames, const uint64_t *offs, uin
 }
 
 // A piece's frames are spread over up to 64 MiB of host memory: every frame is a cache miss,
-// so a large piece is applied by several threads (16 Ki frames and more each).
-void apply_tx_records(const uint64_t *rec, char *frames, const uint64_t *offs, uint64_t stride,
-                      uint8_t *status, uint64_t count) {
-    constexpr uint64_t kPerThreadMin = 16384;
-    const unsigned hw = std::thread::hardware_concurrency();
-    const unsigned nt = (unsigned)std::min<uint64_t>(
-        std::min<uint64_t>(count / kPerThreadMin, host_threads_cap()), hw ? hw : 1);
-    if (nt <= 1) {
-        apply_tx_range(rec, frames, offs, stride, status, 0, count);
-        return;
-    }
+// so a large piece is applied by the pool (16 Ki frames and more per part).
+void apply_tx_records(HostPool &pool, const uint64_t *rec, char *frames, const uint64_t *offs,
+                      uint64_t stride, uint8_t *status, uint64_t count) {
+    const unsigned nt = host_parts(pool, count, 16384);
     const uint64_t per = (count + nt - 1) / nt;
-    std::vector<std::thread> pool;
-    pool.reserve(nt);
-    for (unsigned t = 0; t < nt; ++t) {
-        const uint64_t lo = (uint64_t)t * per;
-        if (lo >= count) break;
-        const uint64_t hi = std::min(count, lo + per);
-        pool.emplace_back([=] { apply_tx_range(rec, frames, offs, stride, status, lo, hi); });
-    }
-    for (std::thread &t : pool) t.join();
+    pool.run(nt, [=](unsigned t) {
+        const uint64_t lo = std::min((uint64_t)t * per, count);
+        apply_tx_range(rec, frames, offs, stride, status, lo, std::min(count, lo + per));
+    });
 }
 
-void applier_loop(Applier *a) {
+void applier_loop(Applier *a, HostPool *pool, const std::vector<int> *cpus) {
+    pin_current_thread(*cpus);
     std::unique_lock<std::mutex> lock(a->mu);
     for (;;) {
         a->work.wait(lock, [a] { return a->stop || !a->queue.empty(); });
@@ -331,7 +332,7 @@ void applier_loop(Applier *a) {
         a->queue.pop_front();
         lock.unlock();
         const uint64_t t0 = a->busy_ns ? now_ns() : 0;
-        apply_tx_records(job.rec.data(), job.frames, job.offs, job.stride, job.status,
+        apply_tx_records(*pool, job.rec.data(), job.frames, job.offs, job.stride, job.status,
                          job.rec.size());
         if (a->busy_ns) a->busy_ns->fetch_add(now_ns() - t0, std::memory_order_relaxed);
         lock.lock();
@@ -340,12 +341,14 @@ void applier_loop(Applier *a) {
     }
 }
 
+// The applier starts with the engine (its thread pinned beside the pool's).
+void start_applier(aipstack_chksum_engine *e) {
+    e->applier.reset(new Applier);
+    if (e->stats.on) e->applier->busy_ns = &e->stats.apply;
+    e->applier->thread = std::thread(applier_loop, e->applier.get(), &e->pool, &e->loc.cpus);
+}
+
 void queue_apply(aipstack_chksum_engine *e, ApplyJob &&job) {
-    if (!e->applier) {
-        e->applier.reset(new Applier);
-        if (e->stats.on) e->applier->busy_ns = &e->stats.apply;
-        e->applier->thread = std::thread(applier_loop, e->applier.get());
-    }
     Applier *a = e->applier.get();
     std::lock_guard<std::mutex> lock(a->mu);
     ++a->pending[job.ticket];
@@ -354,7 +357,8 @@ void queue_apply(aipstack_chksum_engine *e, ApplyJob &&job) {
 }
 
 // Whether ticket's records (every ticket's for 0) are still being applied; with `blocking`,
-// waits until they are not.
+// waits until they are not (callers hold no engine lock then: the applier may take ~0.3 ms
+// per queued 64 MiB piece).
 bool applies_pending(aipstack_chksum_engine *e, uint64_t ticket, bool blocking) {
     Applier *a = e->applier.get();
     if (!a) return false;
@@ -393,7 +397,7 @@ int drain(aipstack_chksum_engine *e, Slot &s, bool blocking = true) {
         if (r == hipErrorNotReady) return 1;
     }
 #ifdef AIPSTACK_ENGINE_FAULT_INJECTION
-    if (r == hipSuccess && injected(g_fail_at_completion, s.seq)) r = hipErrorLaunchFailure;
+    if (r == hipSuccess && injected(e, g_fail_at_completion, s.seq)) r = hipErrorLaunchFailure;
 #endif
     const int st = check_hip(r);
     if (st == AIPSTACK_CHKSUM_OK && s.tx_frames) {
@@ -426,38 +430,39 @@ struct Span {
 // Pageable ring slots into pinned staging: each slot's frame bytes only (row r's first
 // row_len[r] bytes, at the same pitch), by up to host_threads_cap() threads; the kernel then
 // reads the staging in place, so neither the CPU nor the link moves any slack.
-void stage_copy_frames(void *dst, const void *src, uint64_t pitch, const uint32_t *row_len,
-                       uint64_t rows) {
-    auto run = [=](uint64_t lo, uint64_t hi) {
-        for (uint64_t r = lo; r < hi; ++r)
+void stage_copy_frames(HostPool &pool, void *dst, const void *src, uint64_t pitch,
+                       const uint32_t *row_len, uint64_t rows) {
+    const unsigned nt = host_parts(pool, rows, 2048);
+    const uint64_t per = (rows + nt - 1) / nt;
+    pool.run(nt, [=](unsigned t) {
+        const uint64_t hi = std::min(rows, (uint64_t)(t + 1) * per);
+        for (uint64_t r = (uint64_t)t * per; r < hi; ++r)
             std::memcpy(static_cast<char *>(dst) + r * pitch,
                         static_cast<const char *>(src) + r * pitch, row_len[r]);
-    };
-    const unsigned hw = std::thread::hardware_concurrency();
-    const unsigned nt = (unsigned)std::min<uint64_t>(
-        std::min<uint64_t>(rows / 2048, host_threads_cap()), hw ? hw : 1);
-    if (nt <= 1) {
-        run(0, rows);
-        return;
-    }
-    const uint64_t per = (rows + nt - 1) / nt;
-    std::vector<std::thread> pool;
-    for (unsigned t = 0; t < nt && (uint64_t)t * per < rows; ++t)
-        pool.emplace_back(run, (uint64_t)t * per, std::min(rows, (uint64_t)(t + 1) * per));
-    for (std::thread &t : pool) t.join();
+    });
 }
 
 // Enqueue one batch as chunks over the slots. chunker(i0, &i1, &span) describes chunk
 // [i0, i1) of packets and its bytes in host memory; launch(slot, i0, i1) enqueues its
 // kernel, whose results (elem bytes per packet) land in the slot's d_out. Returns the
 // status of the enqueue; *ticket identifies the batch.
+//
+// Called with submit_mu held and mu NOT held. A slot whose previous piece is still running
+// is waited for without mu (so _poll / _wait from other threads go on), then drained under it;
+// a slot taken by this submit is not busy, so nothing else touches it while its piece is
+// staged and launched without mu, and only its hand-over (busy, ticket, results) is under mu.
 template <class Chunker, class Launch>
 int enqueue(aipstack_chksum_engine *e, uint64_t n, void *h_out, uint32_t elem, Chunker chunker,
             Launch launch, uint64_t *ticket) {
     Span_ns timed(e->stats, e->stats.enqueue);
     DeviceGuard dg(e->device);
     if (!dg.ok) return AIPSTACK_CHKSUM_ENODEV;
-    const uint64_t t = e->next_ticket++;
+    uint64_t t;
+    {
+        std::lock_guard<std::mutex> lock(e->mu);
+        t = e->next_ticket++;
+        e->submitting = t;
+    }
     *ticket = t;
     int status = AIPSTACK_CHKSUM_OK;
     uint64_t i0 = 0;
@@ -467,8 +472,39 @@ int enqueue(aipstack_chksum_engine *e, uint64_t n, void *h_out, uint32_t elem, C
         // An earlier piece (this batch's or an older one's) completes; its failure is
         // recorded against its own ticket. One of this batch's own pieces failing ends
         // the enqueue (the rest would be wasted work).
-        const uint64_t prev = s.ticket;
-        const int ds = drain(e, s);
+        hipEvent_t ev = nullptr;
+        uint64_t prev = 0, prev_seq = 0;
+        {
+            std::lock_guard<std::mutex> lock(e->mu);
+            if (s.busy) {
+                ev = s.done;
+                prev = s.ticket;
+                prev_seq = s.seq;
+            }
+        }
+#ifdef AIPSTACK_ENGINE_FAULT_INJECTION
+        if (ev) {  // a long back-pressure wait, made deterministic (test builds)
+            if (const uint64_t us = g_wait_delay_us.load())
+                std::this_thread::sleep_for(std::chrono::microseconds(us));
+        }
+#endif
+        if (ev && hipEventQuery(ev) == hipErrorNotReady) {  // back-pressure, without mu
+            Span_ns waited(e->stats, e->stats.slot_wait);
+            (void)hipEventSynchronize(ev);
+        } else if (ev) {
+            (void)hipGetLastError();
+        }
+        int ds = AIPSTACK_CHKSUM_OK;
+        if (ev) {
+            std::lock_guard<std::mutex> lock(e->mu);
+            // a _poll / _wait may have completed it meanwhile (its failure, if any, is then
+            // recorded against its ticket already)
+            if (s.busy && s.seq == prev_seq) ds = drain(e, s);
+            else if (prev == t) {
+                const auto it = e->failed.find(t);
+                if (it != e->failed.end()) ds = it->second;
+            }
+        }
         if (ds < 0 && prev == t) {
             status = ds;
             break;
@@ -494,11 +530,11 @@ int enqueue(aipstack_chksum_engine *e, uint64_t n, void *h_out, uint32_t elem, C
         } else if (staged_rows) {
             // the frames' bytes into pinned staging, read there by the kernel
             Span_ns staged(e->stats, e->stats.stage);
-            stage_copy_frames(s.h_stage, sp.src, sp.pitch, sp.row_len, sp.bytes / sp.pitch);
+            stage_copy_frames(e->pool, s.h_stage, sp.src, sp.pitch, sp.row_len, sp.bytes / sp.pitch);
             s.k_bytes = s.dh_stage;
         } else if (sp.bytes && !registered) {  // pageable: CPU copy into pinned staging
             Span_ns staged(e->stats, e->stats.stage);
-            stage_copy(s.h_stage, sp.src, sp.bytes);
+            stage_copy(e->pool, s.h_stage, sp.src, sp.bytes);
             h_src = s.h_stage;
         }
         const bool copy = sp.bytes && s.k_bytes == s.d_bytes;
@@ -512,7 +548,7 @@ int enqueue(aipstack_chksum_engine *e, uint64_t n, void *h_out, uint32_t elem, C
         s.seq = ++e->pieces;
         e->stats.pieces.fetch_add(1, std::memory_order_relaxed);
 #ifdef AIPSTACK_ENGINE_FAULT_INJECTION
-        if (status == AIPSTACK_CHKSUM_OK && injected(g_fail_at_launch, s.seq))
+        if (status == AIPSTACK_CHKSUM_OK && injected(e, g_fail_at_launch, s.seq))
             status = AIPSTACK_CHKSUM_EHIP;
 #endif
         if (status == AIPSTACK_CHKSUM_OK) status = launch(s, i0, i1);
@@ -520,21 +556,29 @@ int enqueue(aipstack_chksum_engine *e, uint64_t n, void *h_out, uint32_t elem, C
             status = check_hip(hipMemcpyAsync(s.h_out, s.d_out, cnt * elem,
                                               hipMemcpyDeviceToHost, s.stream));
         if (status == AIPSTACK_CHKSUM_OK) status = check_hip(hipEventRecord(s.done, s.stream));
-        s.busy = status == AIPSTACK_CHKSUM_OK;
-        s.user_out = static_cast<char *>(h_out) + i0 * elem;
-        s.count = cnt;
-        s.out_elem = elem;
-        s.ticket = t;
+        {
+            std::lock_guard<std::mutex> lock(e->mu);
+            s.user_out = static_cast<char *>(h_out) + i0 * elem;
+            s.count = cnt;
+            s.out_elem = elem;
+            s.ticket = t;
+            s.busy = status == AIPSTACK_CHKSUM_OK;
+        }
         i0 = i1;
     }
+    std::lock_guard<std::mutex> lock(e->mu);
     if (status != AIPSTACK_CHKSUM_OK) record_failure(e, t, status);
+    e->submitting = 0;
     return status;
 }
 
-// Complete batch `ticket`: 0 = done (results in place), 1 = still running (non-blocking
-// only), < 0 = it failed (its first failure; the record is consumed).
+// Complete batch `ticket` (with mu held): 0 = done (results in place), 1 = still running
+// (a piece, or its Tx records in the applier), < 0 = it failed (its first failure; the
+// record is consumed). `blocking` waits for its pieces (whose events the caller has already
+// waited for without mu), never for the applier: _wait does that outside mu.
 int complete(aipstack_chksum_engine *e, uint64_t ticket, bool blocking) {
     if (ticket == 0 || ticket >= e->next_ticket) return AIPSTACK_CHKSUM_EINVAL;
+    if (ticket == e->submitting) return 1;
     Span_ns timed(e->stats, e->stats.complete);
     DeviceGuard dg(e->device);
     if (!dg.ok) return AIPSTACK_CHKSUM_ENODEV;
@@ -545,7 +589,7 @@ int complete(aipstack_chksum_engine *e, uint64_t ticket, bool blocking) {
         if (st == 1) pending = 1;
     }
     if (pending) return 1;
-    if (applies_pending(e, ticket, blocking)) return 1;  // (false when blocking)
+    if (applies_pending(e, ticket, false)) return 1;
     const auto it = e->failed.find(ticket);
     if (it == e->failed.end()) return AIPSTACK_CHKSUM_OK;
     const int st = it->second;
@@ -554,7 +598,8 @@ int complete(aipstack_chksum_engine *e, uint64_t ticket, bool blocking) {
 }
 
 // Every piece in flight, completed as _wait completes it (results delivered, Tx records
-// applied); failures stay recorded.
+// applied); failures stay recorded. Called with mu held, only where no submit can run
+// (destroy; unregister holds submit_mu): the applier then only holds pieces queued before.
 void drain_all(aipstack_chksum_engine *e) {
     for (Slot &s : e->slots) (void)drain(e, s, true);
     (void)applies_pending(e, 0, true);
@@ -585,6 +630,12 @@ extern "C" int aipstack_chksum_engine_create(int device, uint64_t chunk_bytes, i
     e->pageable_rows = tuning_engine_pageable_rows() != 0;
     if (const char *v = std::getenv("AIPSTACK_ENGINE_STATS")) e->stats.on = std::atoi(v) != 0;
     e->stats.created = now_ns();
+    // host threads next to the device: the pool and the applier pinned to its local CPUs,
+    // and the pinned staging allocated from them (its pages on the device's NUMA node)
+    e->loc = device_locality(device);
+    e->pool.start(host_threads_cap() - 1u, e->loc.cpus);
+    start_applier(e);
+    ScopedAffinity near_device(e->loc.cpus);
     e->slots.resize((size_t)nstreams);
     int st = AIPSTACK_CHKSUM_OK;
     for (Slot &s : e->slots) {
@@ -615,11 +666,13 @@ extern "C" int aipstack_chksum_engine_create(int device, uint64_t chunk_bytes, i
 extern "C" void aipstack_chksum_engine_destroy(aipstack_chksum_engine *e) {
     if (!e) return;
     {
+        std::lock_guard<std::mutex> sub(e->submit_mu);
         std::lock_guard<std::mutex> lock(e->mu);
         DeviceGuard dg(e->device);
         drain_all(e);  // pieces in flight complete: results written, Tx fields applied
     }
     release(e);
+    e->pool.stop();
     if (e->stats.on) {
         const Stats &t = e->stats;
         auto ms = [](const std::atomic<uint64_t> &v) { return (double)v.load() / 1e6; };
@@ -639,12 +692,16 @@ namespace aipstack_amd {
 // For the engine group (chksum_engine_group.cpp): a region page-locked once for every
 // device (hipHostRegisterPortable) becomes DMA-direct input of this engine too; removing it
 // first completes the pieces in flight (they may still read it).
-void engine_adopt_region(aipstack_chksum_engine *e, const void *p, uint64_t bytes) {
+bool engine_adopt_region(aipstack_chksum_engine *e, const void *p, uint64_t bytes) {
+    std::lock_guard<std::mutex> sub(e->submit_mu);
     std::lock_guard<std::mutex> lock(e->mu);
     DeviceGuard dg(e->device);
-    e->registered.push_back(Region{static_cast<const char *>(p), bytes, false, mapped_address(p)});
+    const char *dev = mapped_address(p);
+    e->registered.push_back(Region{static_cast<const char *>(p), bytes, false, dev});
+    return dev != nullptr;
 }
 void engine_drop_region(aipstack_chksum_engine *e, const void *p) {
+    std::lock_guard<std::mutex> sub(e->submit_mu);
     std::lock_guard<std::mutex> lock(e->mu);
     for (size_t i = 0; i < e->registered.size(); ++i) {
         if (e->registered[i].p == p) {
@@ -660,10 +717,11 @@ void engine_drop_region(aipstack_chksum_engine *e, const void *p) {
 extern "C" int aipstack_chksum_engine_register(aipstack_chksum_engine *e, void *host_ptr,
                                                uint64_t bytes) {
     if (!e || !host_ptr || bytes == 0) return AIPSTACK_CHKSUM_EINVAL;
+    std::lock_guard<std::mutex> sub(e->submit_mu);
     std::lock_guard<std::mutex> lock(e->mu);
     DeviceGuard dg(e->device);
     if (!dg.ok) return AIPSTACK_CHKSUM_ENODEV;
-    const int st = check_hip(hipHostRegister(host_ptr, bytes, hipHostRegisterDefault));
+    const int st = check_hip(hipHostRegister(host_ptr, bytes, hipHostRegisterMapped));
     if (st == AIPSTACK_CHKSUM_OK)
         e->registered.push_back(Region{static_cast<char *>(host_ptr), bytes, true,
                                        mapped_address(host_ptr)});
@@ -672,6 +730,7 @@ extern "C" int aipstack_chksum_engine_register(aipstack_chksum_engine *e, void *
 
 extern "C" int aipstack_chksum_engine_unregister(aipstack_chksum_engine *e, void *host_ptr) {
     if (!e || !host_ptr) return AIPSTACK_CHKSUM_EINVAL;
+    std::lock_guard<std::mutex> sub(e->submit_mu);
     std::lock_guard<std::mutex> lock(e->mu);
     for (size_t i = 0; i < e->registered.size(); ++i) {
         if (e->registered[i].p == host_ptr) {
@@ -707,7 +766,7 @@ extern "C" int aipstack_chksum_engine_submit_strided(aipstack_chksum_engine *e,
         return aipstack_chksum_batch_strided(s.k_bytes, stride, len, i1 - i0, s.k_out, flags,
                                              s.stream);
     };
-    std::lock_guard<std::mutex> lock(e->mu);
+    std::lock_guard<std::mutex> lock(e->submit_mu);
     return enqueue(e, n, h_out, 2, chunker, launch, ticket);
 }
 
@@ -744,7 +803,7 @@ int submit_csr_like(aipstack_chksum_engine *e, const void *h_base, const uint64_
         }
         return kernel(s, i0, cnt);
     };
-    std::lock_guard<std::mutex> lock(e->mu);
+    std::lock_guard<std::mutex> lock(e->submit_mu);
     return enqueue(e, n, h_out, elem, chunker, launch, ticket);
 }
 }  // namespace
@@ -860,7 +919,7 @@ int submit_slotted_like(aipstack_chksum_engine *e, const void *h_base, uint64_t 
         }
         return kernel(s, i0, cnt, reinterpret_cast<const uint32_t *>(s.k_off));
     };
-    std::lock_guard<std::mutex> lock(e->mu);
+    std::lock_guard<std::mutex> lock(e->submit_mu);
     return enqueue(e, n, h_out, elem, chunker, launch, ticket);
 }
 }  // namespace
@@ -882,7 +941,9 @@ extern "C" int aipstack_chksum_engine_submit_slotted(aipstack_chksum_engine *e, 
 extern "C" int aipstack_chksum_engine_submit_rx_verify_slotted(
     aipstack_chksum_engine *e, const void *h_base, uint64_t slot_stride, const uint32_t *h_len,
     uint64_t n, uint8_t *h_verdicts, uint64_t *ticket) {
-    if (!e || !h_base || !h_len || !h_verdicts || !ticket) return AIPSTACK_CHKSUM_EINVAL;
+    if (!e || !h_base || !h_len || !h_verdicts || !ticket ||
+        slot_stride > AIPSTACK_CHKSUM_MAX_SLOT_STRIDE)
+        return AIPSTACK_CHKSUM_EINVAL;
     return submit_slotted_like(e, h_base, slot_stride, h_len, n, h_verdicts, 1,
                                [&](Slot &s, uint64_t, uint64_t cnt, const uint32_t *d_len) {
                                    return aipstack_chksum_rx_verify_slotted(
@@ -895,7 +956,9 @@ extern "C" int aipstack_chksum_engine_submit_rx_verify_slotted(
 extern "C" int aipstack_chksum_engine_submit_tx_fill_slotted(
     aipstack_chksum_engine *e, void *h_base, uint64_t slot_stride, const uint32_t *h_len,
     uint64_t n, uint8_t *h_status, uint64_t *ticket) {
-    if (!e || !h_base || !h_len || !h_status || !ticket) return AIPSTACK_CHKSUM_EINVAL;
+    if (!e || !h_base || !h_len || !h_status || !ticket ||
+        slot_stride > AIPSTACK_CHKSUM_MAX_SLOT_STRIDE)
+        return AIPSTACK_CHKSUM_EINVAL;
     char *frames = static_cast<char *>(h_base);
     return submit_slotted_like(e, h_base, slot_stride, h_len, n, h_status, 8,
                                [&](Slot &s, uint64_t i0, uint64_t cnt, const uint32_t *d_len) {
@@ -978,8 +1041,16 @@ extern "C" int aipstack_chksum_engine_wait(aipstack_chksum_engine *e, uint64_t t
         std::this_thread::sleep_for(std::chrono::microseconds(us));
 #endif
     for (hipEvent_t ev : events) (void)hipEventSynchronize(ev);
-    std::lock_guard<std::mutex> lock(e->mu);
-    return complete(e, ticket, true);
+    for (;;) {
+        {
+            std::lock_guard<std::mutex> lock(e->mu);
+            const int st = complete(e, ticket, true);
+            if (st != 1) return st;
+        }
+        // its Tx records are still queued in the applier: wait for them without mu
+        // (ADVICE round 3), then collect the ticket's status
+        (void)applies_pending(e, ticket, true);
+    }
 }
 
 #ifdef AIPSTACK_ENGINE_FAULT_INJECTION
@@ -990,7 +1061,28 @@ extern "C" void aipstack_chksum_engine_test_inject(uint64_t fail_at_launch,
     g_fail_at_completion = fail_at_completion;
 }
 extern "C" void aipstack_chksum_engine_test_wait_delay(uint64_t us) { g_wait_delay_us = us; }
+// Restricts the injected failures to one engine (null: every engine), e.g. one engine of a
+// group (aipstack_chksum_engine_group_engine).
+extern "C" void aipstack_chksum_engine_test_inject_only(const aipstack_chksum_engine *e) {
+    g_fail_engine = e;
+}
 #endif
+
+extern "C" int aipstack_chksum_engine_locality(const aipstack_chksum_engine *e, int *numa_node,
+                                               int *pinned_cpus) {
+    if (!e) return AIPSTACK_CHKSUM_EINVAL;
+    if (numa_node) *numa_node = e->loc.numa_node;
+    if (pinned_cpus) *pinned_cpus = (int)e->loc.cpus.size();
+    return AIPSTACK_CHKSUM_OK;
+}
+
+extern "C" int aipstack_chksum_engine_region_mapped(aipstack_chksum_engine *e, const void *host_ptr) {
+    if (!e || !host_ptr) return AIPSTACK_CHKSUM_EINVAL;
+    std::lock_guard<std::mutex> lock(e->mu);
+    const Region *r = find_registered(e, host_ptr, 1);
+    if (!r) return AIPSTACK_CHKSUM_EINVAL;
+    return r->dev && e->zero_copy_bytes ? 1 : 0;
+}
 
 extern "C" int aipstack_chksum_engine_host_strided(aipstack_chksum_engine *e, const void *h_base,
                                                    uint64_t stride, uint32_t len, uint64_t n,

@@ -69,6 +69,10 @@ extern "C" int aipstack_chksum_last_hip_error(void) { return g_last_hip_error; }
 
 extern "C" int aipstack_chksum_abi_version(void) { return AIPSTACK_CHKSUM_ABI_VERSION; }
 
+// Generated at build time from the library's sources (Makefile: build/source_digest.h).
+#include "build/source_digest.h"
+extern "C" const char *aipstack_chksum_source_digest(void) { return AIPSTACK_SOURCE_DIGEST; }
+
 extern "C" int aipstack_chksum_device_check(int device) {
     int count = 0;
     hipError_t e = hipGetDeviceCount(&count);

@@ -70,7 +70,9 @@ int tuning_engine_pageable_rows();  // pageable ring slots: frame bytes staged, 
 struct aipstack_chksum_engine;
 namespace aipstack_amd {
 // Host engine internals shared with the engine group (chksum_engine.cpp).
-void engine_adopt_region(aipstack_chksum_engine *e, const void *p, uint64_t bytes);
+// The region (page-locked by the group, portable) as input of this engine too; returns
+// whether the engine's kernels read it in place (mapped into this device's address space).
+bool engine_adopt_region(aipstack_chksum_engine *e, const void *p, uint64_t bytes);
 void engine_drop_region(aipstack_chksum_engine *e, const void *p);
 }  // namespace aipstack_amd
 

@@ -940,6 +940,8 @@ def e2e(args, rank, world, local_rank, layout, n, plen):
                              nstreams=args.e2e_streams)
     if not args.e2e_pageable:
         eng.register(host)
+    # where each engine's host threads run (its device's NUMA node, CPUs pinned)
+    locality = eng.locality() if args.engines > 0 else [eng.locality()]
 
     def step():
         if layout == "strided":
@@ -1056,9 +1058,12 @@ def e2e(args, rank, world, local_rank, layout, n, plen):
                            "value_counts": "frame/packet bytes (the lengths), not slot bytes"}
                           if layout in ("rxslot", "csrslot", "txslot") else {}),
                        **({"engines": args.engines, "engine_devices": engine_devices,
-                           "engine_group": "one process, disjoint ranges of equal bytes, one "
-                                           "host thread per engine"}
-                          if args.engines > 0 else {})},
+                           "engine_group": "one process, disjoint ranges of equal bytes per "
+                                           "device; group tickets; pageable ranges staged by "
+                                           "a worker thread per device"}
+                          if args.engines > 0 else {}),
+                       "engine_locality": [{"device": d, "numa_node": nn, "pinned_cpus": pc}
+                                           for d, (nn, pc) in zip(engine_devices, locality)]},
             "per_gpu": {"devices": pcis, "arch": [i["arch"] for i in infos],
                         "distinct_devices": len(set(pcis)) == world,
                         "parity": [i["parity"] for i in infos]},

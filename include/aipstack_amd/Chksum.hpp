@@ -22,6 +22,27 @@
 
 #include "aipstack_amd/chksum.h"
 
+// Assertions follow the reference's configuration (misc/Assert.h): checked only where the
+// application defines AIPSTACK_CONFIG_ENABLE_ASSERTIONS; a failure calls the application's
+// AIPSTACK_CONFIG_ASSERT_HANDLER(msg) if it has one, else prints the message and aborts.
+#ifdef AIPSTACK_CONFIG_ENABLE_ASSERTIONS
+#ifdef AIPSTACK_CONFIG_ASSERT_INCLUDE
+#include AIPSTACK_CONFIG_ASSERT_INCLUDE
+#endif
+#include <cstdio>
+#include <cstdlib>
+#ifdef AIPSTACK_CONFIG_ASSERT_HANDLER
+#define AIPSTACK_AMD_ASSERT_FAIL(msg) AIPSTACK_CONFIG_ASSERT_HANDLER(msg)
+#else
+#define AIPSTACK_AMD_ASSERT_FAIL(msg) \
+    (std::fprintf(stderr, "%s:%d: %s\n", __FILE__, __LINE__, msg), std::abort())
+#endif
+#define AIPSTACK_AMD_ASSERT(e) \
+    ((e) ? (void)0 : (void)(AIPSTACK_AMD_ASSERT_FAIL("Assertion failed: " #e), 0))
+#else
+#define AIPSTACK_AMD_ASSERT(e) ((void)0)
+#endif
+
 namespace AIpStackAmd {
 
 // meta/BasicMetaUtils.h:39-42: the tag type the reference's addWord overloads take
@@ -123,8 +144,12 @@ public:
     void addWordOctets(std::uint8_t hi, std::uint8_t lo) {
         addWord(WrapType<std::uint16_t>(), std::uint16_t((std::uint16_t(hi) << 8) | lo));
     }
-    // Chksum.h:225-235 (num_bytes must be even, as the reference asserts at :227)
+    // Chksum.h:225-235. num_bytes must be even: asserted as the reference asserts it (:227),
+    // when the application enables the stack's assertions (AIPSTACK_CONFIG_ENABLE_ASSERTIONS,
+    // misc/Assert.h); without them an odd trailing byte is ignored (the reference would read
+    // one byte past the range).
     void addEvenBytes(char const *ptr, std::size_t num_bytes) {
+        AIPSTACK_AMD_ASSERT(num_bytes % 2 == 0);
         unsigned char const *p = reinterpret_cast<unsigned char const *>(ptr);
         for (std::size_t i = 0; i + 1 < num_bytes; i += 2)
             addWord(WrapType<std::uint16_t>(), std::uint16_t((std::uint16_t(p[i]) << 8) | p[i + 1]));
@@ -398,8 +423,107 @@ public:
     int poll(std::uint64_t ticket) { return aipstack_chksum_engine_poll(m_engine, ticket); }
     int wait(std::uint64_t ticket) { return aipstack_chksum_engine_wait(m_engine, ticket); }
 
+    // NUMA node of the device (-1 unknown) and the CPUs the engine's host threads are pinned to.
+    int locality(int *numa_node, int *pinned_cpus) const {
+        return aipstack_chksum_engine_locality(m_engine, numa_node, pinned_cpus);
+    }
+
 private:
     aipstack_chksum_engine *m_engine = nullptr;
+    int m_status = AIPSTACK_CHKSUM_EINVAL;
+};
+
+// Several devices behind one host-memory batch, in one process (aipstack_chksum_engine_group):
+// owns the group, move-only. submit* return one group ticket over the devices' ranges;
+// poll / wait complete it (0 done, 1 running, < 0 the first failure) and fill devStatus (NULL
+// or size() ints) with each device's status.
+class HostChksumEngineGroup {
+public:
+    HostChksumEngineGroup(int const *devices, int n_devices, std::uint64_t chunk_bytes = 0,
+                          int nstreams = 4) {
+        m_status = aipstack_chksum_engine_group_create(devices, n_devices, chunk_bytes, nstreams,
+                                                       &m_group);
+    }
+    ~HostChksumEngineGroup() { aipstack_chksum_engine_group_destroy(m_group); }
+    HostChksumEngineGroup(HostChksumEngineGroup &&o) noexcept
+        : m_group(o.m_group), m_status(o.m_status) {
+        o.m_group = nullptr;
+    }
+    HostChksumEngineGroup &operator=(HostChksumEngineGroup &&o) noexcept {
+        if (this != &o) {
+            aipstack_chksum_engine_group_destroy(m_group);
+            m_group = o.m_group;
+            m_status = o.m_status;
+            o.m_group = nullptr;
+        }
+        return *this;
+    }
+    HostChksumEngineGroup(HostChksumEngineGroup const &) = delete;
+    HostChksumEngineGroup &operator=(HostChksumEngineGroup const &) = delete;
+
+    bool valid() const { return m_group != nullptr; }
+    int createStatus() const { return m_status; }
+    int size() const { return aipstack_chksum_engine_group_size(m_group); }
+    aipstack_chksum_engine_group *handle() const { return m_group; }
+    aipstack_chksum_engine *engine(int k) const {
+        return aipstack_chksum_engine_group_engine(m_group, k);
+    }
+
+    int registerMemory(void *ptr, std::uint64_t bytes) {
+        return aipstack_chksum_engine_group_register(m_group, ptr, bytes);
+    }
+    int unregisterMemory(void *ptr) { return aipstack_chksum_engine_group_unregister(m_group, ptr); }
+
+    int submitStrided(void const *h_base, std::uint64_t stride, std::uint32_t len,
+                      std::uint64_t n, std::uint16_t *h_out, bool final_chksum,
+                      std::uint64_t *ticket) {
+        return aipstack_chksum_engine_group_submit_strided(
+            m_group, h_base, stride, len, n, h_out, final_chksum ? AIPSTACK_CHKSUM_FINAL : 0u,
+            ticket);
+    }
+    int submitCsr(void const *h_base, std::uint64_t const *h_offsets, std::uint64_t n,
+                  std::uint16_t *h_out, bool final_chksum, std::uint64_t *ticket) {
+        return aipstack_chksum_engine_group_submit_csr(
+            m_group, h_base, h_offsets, n, h_out, final_chksum ? AIPSTACK_CHKSUM_FINAL : 0u,
+            ticket);
+    }
+    int submitRxVerify(void const *h_frames, std::uint64_t const *h_offsets, std::uint64_t n,
+                       std::uint8_t *h_verdict, std::uint64_t *ticket) {
+        return aipstack_chksum_engine_group_submit_rx_verify(m_group, h_frames, h_offsets, n,
+                                                             h_verdict, ticket);
+    }
+    int submitTxFill(void *h_frames, std::uint64_t const *h_offsets, std::uint64_t n,
+                     std::uint8_t *h_status, std::uint64_t *ticket) {
+        return aipstack_chksum_engine_group_submit_tx_fill(m_group, h_frames, h_offsets, n,
+                                                           h_status, ticket);
+    }
+    int submitSlotted(void const *h_base, std::uint64_t slot_stride, std::uint32_t const *h_len,
+                      std::uint64_t n, std::uint16_t *h_out, bool final_chksum,
+                      std::uint64_t *ticket) {
+        return aipstack_chksum_engine_group_submit_slotted(
+            m_group, h_base, slot_stride, h_len, n, h_out,
+            final_chksum ? AIPSTACK_CHKSUM_FINAL : 0u, ticket);
+    }
+    int submitRxVerifySlotted(void const *h_base, std::uint64_t slot_stride,
+                              std::uint32_t const *h_len, std::uint64_t n,
+                              std::uint8_t *h_verdict, std::uint64_t *ticket) {
+        return aipstack_chksum_engine_group_submit_rx_verify_slotted(m_group, h_base, slot_stride,
+                                                                     h_len, n, h_verdict, ticket);
+    }
+    int submitTxFillSlotted(void *h_base, std::uint64_t slot_stride, std::uint32_t const *h_len,
+                            std::uint64_t n, std::uint8_t *h_status, std::uint64_t *ticket) {
+        return aipstack_chksum_engine_group_submit_tx_fill_slotted(m_group, h_base, slot_stride,
+                                                                   h_len, n, h_status, ticket);
+    }
+    int poll(std::uint64_t ticket, int *devStatus = nullptr) {
+        return aipstack_chksum_engine_group_poll(m_group, ticket, devStatus);
+    }
+    int wait(std::uint64_t ticket, int *devStatus = nullptr) {
+        return aipstack_chksum_engine_group_wait(m_group, ticket, devStatus);
+    }
+
+private:
+    aipstack_chksum_engine_group *m_group = nullptr;
     int m_status = AIPSTACK_CHKSUM_EINVAL;
 };
 

@@ -318,22 +318,48 @@ int aipstack_chksum_engine_submit_tx_fill_slotted(aipstack_chksum_engine *engine
 int aipstack_chksum_engine_poll(aipstack_chksum_engine *engine, uint64_t ticket);
 int aipstack_chksum_engine_wait(aipstack_chksum_engine *engine, uint64_t ticket);
 
+/* Where the engine's host threads run: the NUMA node of its device (-1 unknown) and how many
+ * of the CPUs next to the device (sysfs local_cpulist, within this process's affinity) its
+ * host threads are pinned to (0 = not pinned). Its pinned staging is allocated from them. */
+int aipstack_chksum_engine_locality(const aipstack_chksum_engine *engine, int *numa_node,
+                                    int *pinned_cpus);
+/* 1 if the engine's kernels read the registered region holding host_ptr in place (zero copy),
+ * 0 if it is DMA'd to the device first, _EINVAL if host_ptr is in no registered region. */
+int aipstack_chksum_engine_region_mapped(aipstack_chksum_engine *engine, const void *host_ptr);
+
 /* ---- 4. several devices in one process -------------------------------------------- */
 
 /* The reference stack is one process on one event-loop thread (event_loop/event_loop.dox:
- * 48-50); a host batch is PCIe-bound per device (~52 GiB/s). An engine group owns one engine
- * per entry of `devices` (repeats allowed), splits every batch into contiguous ranges of about
- * equal bytes, runs each range on its engine from its own host thread and joins: disjoint
- * packet ranges, no data exchanged between the devices. The host_* calls mirror the single
- * engine's; dev_status (NULL or n_devices ints) receives each engine's status, the return
- * value is the first failure (or _OK). _register page-locks a region once for all devices
- * (hipHostRegisterPortable). Calls on one group are serialised. */
+ * 48-50); a host batch is PCIe-bound per device (~50 GiB/s). An engine group owns one engine
+ * per entry of `devices` (repeats allowed) and splits a batch into contiguous ranges of about
+ * equal bytes, one per device (a batch of less than 4 MiB per device goes to fewer devices,
+ * round robin, whole): disjoint packet ranges, no data exchanged between the devices.
+ *
+ * The submit_* calls enqueue a batch and return ONE group ticket at once; _poll / _wait
+ * complete it: 0 = done, 1 = still running (poll), else the first failure by device order;
+ * dev_status (NULL or n_devices ints) then receives each device's status (0 for a device
+ * without a range). A ticket is reported once; completing it again returns 0. Each range is
+ * submitted to its engine on the calling thread when the batch lies in a region registered
+ * with the group (the kernels read it in place) or is small, else by a persistent worker
+ * thread of its device (pinned, like the engine's own host threads, to the CPUs next to the
+ * device), so the pageable staging copies of all devices run in parallel while the caller
+ * goes on. Every input, output and frame buffer of a submitted batch must stay valid, and its
+ * input unchanged, until the ticket completes. The host_* calls are submit + wait.
+ * _register page-locks a region once for all devices (portable, mapped into each device). */
 typedef struct aipstack_chksum_engine_group aipstack_chksum_engine_group;
 
 int aipstack_chksum_engine_group_create(const int *devices, int n_devices, uint64_t chunk_bytes,
                                         int nstreams, aipstack_chksum_engine_group **out);
 void aipstack_chksum_engine_group_destroy(aipstack_chksum_engine_group *group);
 int aipstack_chksum_engine_group_size(const aipstack_chksum_engine_group *group);
+/* The engine of entry k (owned by the group, valid until it is destroyed), e.g. for
+ * aipstack_chksum_engine_locality; NULL for k out of range. */
+aipstack_chksum_engine *aipstack_chksum_engine_group_engine(aipstack_chksum_engine_group *group,
+                                                            int k);
+/* 1 if every engine of the group reads the group-registered region holding host_ptr in place,
+ * 0 if some DMA it, _EINVAL if it is not registered with the group. */
+int aipstack_chksum_engine_group_region_mapped(aipstack_chksum_engine_group *group,
+                                               const void *host_ptr);
 int aipstack_chksum_engine_group_register(aipstack_chksum_engine_group *group, void *host_ptr,
                                           uint64_t bytes);
 int aipstack_chksum_engine_group_unregister(aipstack_chksum_engine_group *group, void *host_ptr);
@@ -365,6 +391,36 @@ int aipstack_chksum_engine_group_host_tx_fill_slotted(aipstack_chksum_engine_gro
                                                       void *h_base, uint64_t slot_stride,
                                                       const uint32_t *h_len, uint64_t n,
                                                       uint8_t *h_status, int *dev_status);
+int aipstack_chksum_engine_group_submit_strided(aipstack_chksum_engine_group *group,
+                                                const void *h_base, uint64_t stride, uint32_t len,
+                                                uint64_t n, uint16_t *h_out, uint32_t flags,
+                                                uint64_t *ticket);
+int aipstack_chksum_engine_group_submit_csr(aipstack_chksum_engine_group *group,
+                                            const void *h_base, const uint64_t *h_offsets,
+                                            uint64_t n, uint16_t *h_out, uint32_t flags,
+                                            uint64_t *ticket);
+int aipstack_chksum_engine_group_submit_rx_verify(aipstack_chksum_engine_group *group,
+                                                  const void *h_base, const uint64_t *h_offsets,
+                                                  uint64_t n, uint8_t *h_verdicts, uint64_t *ticket);
+int aipstack_chksum_engine_group_submit_tx_fill(aipstack_chksum_engine_group *group, void *h_base,
+                                                const uint64_t *h_offsets, uint64_t n,
+                                                uint8_t *h_status, uint64_t *ticket);
+int aipstack_chksum_engine_group_submit_slotted(aipstack_chksum_engine_group *group,
+                                                const void *h_base, uint64_t slot_stride,
+                                                const uint32_t *h_len, uint64_t n, uint16_t *h_out,
+                                                uint32_t flags, uint64_t *ticket);
+int aipstack_chksum_engine_group_submit_rx_verify_slotted(aipstack_chksum_engine_group *group,
+                                                          const void *h_base, uint64_t slot_stride,
+                                                          const uint32_t *h_len, uint64_t n,
+                                                          uint8_t *h_verdicts, uint64_t *ticket);
+int aipstack_chksum_engine_group_submit_tx_fill_slotted(aipstack_chksum_engine_group *group,
+                                                        void *h_base, uint64_t slot_stride,
+                                                        const uint32_t *h_len, uint64_t n,
+                                                        uint8_t *h_status, uint64_t *ticket);
+int aipstack_chksum_engine_group_poll(aipstack_chksum_engine_group *group, uint64_t ticket,
+                                      int *dev_status);
+int aipstack_chksum_engine_group_wait(aipstack_chksum_engine_group *group, uint64_t ticket,
+                                      int *dev_status);
 
 /* ---- diagnostics ------------------------------------------------------------------ */
 
@@ -420,6 +476,11 @@ int aipstack_chksum_launch_shape(uint64_t n, int cus, int csr, uint32_t *chunk_p
 /* ABI version of this header: bumped on any incompatible change. */
 #define AIPSTACK_CHKSUM_ABI_VERSION 1
 int aipstack_chksum_abi_version(void);
+
+/* sha256 (hex) of the sources this library was built from (aipstack_amd/csrc/ *.hip, *.cpp,
+ * *.cc, *.h, its Makefile, include/aipstack_amd/ *.h, concatenated in sorted path order):
+ * lets a test or a deployment tell a library from a stale build. */
+const char *aipstack_chksum_source_digest(void);
 
 #ifdef __cplusplus
 }

@@ -11,6 +11,11 @@
 //   4. destroy with a Tx fill batch pending: the frames end up filled (as the oracle fills)
 //   5. unregister while a batch on the region is in flight: the batch completes first
 //   6. _wait does not hold the engine while it waits: _poll from another thread returns
+//   7. a submit waiting for a busy slot (back-pressure) does not hold the engine either: _poll
+//      of an earlier batch from another thread answers at once (round 4)
+//   8. an engine group (two engines on device 0): a group ticket with one failing device
+//      reports that device's failure (dev_status) and the other's results are exact; group
+//      tickets in flight completed out of order; the group's own destroy with a batch pending
 // Needs a GPU (exit 3 without one). Exit 0 = pass.
 #include <atomic>
 #include <chrono>
@@ -28,6 +33,7 @@
 extern "C" void aipstack_chksum_engine_test_inject(uint64_t fail_at_launch,
                                                     uint64_t fail_at_completion);
 extern "C" void aipstack_chksum_engine_test_wait_delay(uint64_t us);
+extern "C" void aipstack_chksum_engine_test_inject_only(const aipstack_chksum_engine *e);
 
 static int failures = 0;
 #define EXPECT(cond, ...)                        \
@@ -200,6 +206,90 @@ void wait_does_not_hold_the_engine() {
     aipstack_chksum_engine_destroy(e);
 }
 
+void poll_answers_while_submit_is_back_pressured() {
+    // One stream: batch B's submit must first complete batch A's piece on it. The test hook
+    // makes that back-pressure wait 300 ms long (outside the engine lock); a _poll of A from
+    // another thread meanwhile must answer at once.
+    aipstack_chksum_engine *e = make_engine(kChunk, 1);
+    const uint64_t n = kPerPiece;
+    std::vector<unsigned char> a(n * kLen), b(n * kLen);
+    aipstack_synth_fill_host(a.data(), a.size(), 11, 0);
+    aipstack_synth_fill_host(b.data(), b.size(), 12, 0);
+    std::vector<uint16_t> oa(n), ob(n);
+    uint64_t ta = 0, tb = 0;
+    EXPECT(aipstack_chksum_engine_submit_strided(e, a.data(), kLen, kLen, n, oa.data(), 0, &ta) == 0,
+           "submit A");
+    aipstack_chksum_engine_test_wait_delay(300000);
+    std::atomic<bool> submitted{false};
+    int sst = -100;
+    std::thread submitter([&] {
+        sst = aipstack_chksum_engine_submit_strided(e, b.data(), kLen, kLen, n, ob.data(), 0, &tb);
+        submitted = true;
+    });
+    std::this_thread::sleep_for(std::chrono::milliseconds(50));
+    const auto p0 = std::chrono::steady_clock::now();
+    const int p = aipstack_chksum_engine_poll(e, ta);
+    const double poll_ms =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - p0).count();
+    const bool done_before = submitted.load();
+    submitter.join();
+    aipstack_chksum_engine_test_wait_delay(0);
+    EXPECT(!done_before && poll_ms < 100.0 && (p == 0 || p == 1),
+           "poll must answer while a submit is back-pressured (poll %d after %.1f ms, submit "
+           "done %d)", p, poll_ms, (int)done_before);
+    EXPECT(sst == 0 && aipstack_chksum_engine_wait(e, tb) == 0, "submit / wait B");
+    EXPECT(aipstack_chksum_engine_wait(e, ta) == 0, "wait A");
+    EXPECT(oa == host_sums(a, n) && ob == host_sums(b, n), "results of A and B");
+    aipstack_chksum_engine_destroy(e);
+}
+
+void group_ticket_with_one_failing_device() {
+    const int devs[2] = {0, 0};
+    aipstack_chksum_engine_group *g = nullptr;
+    EXPECT(aipstack_chksum_engine_group_create(devs, 2, kChunk, kStreams, &g) == 0, "group create");
+    if (!g) return;
+    // 12 MB: split over both engines (>= 4 MiB each)
+    const uint64_t n = 8000;
+    std::vector<unsigned char> a(n * kLen), b(n * kLen), c(n * kLen);
+    aipstack_synth_fill_host(a.data(), a.size(), 21, 0);
+    aipstack_synth_fill_host(b.data(), b.size(), 22, 0);
+    aipstack_synth_fill_host(c.data(), c.size(), 23, 0);
+    std::vector<uint16_t> oa(n), ob(n), oc(n);
+    aipstack_chksum_engine *e1 = aipstack_chksum_engine_group_engine(g, 1);
+    EXPECT(e1 != nullptr && aipstack_chksum_engine_group_engine(g, 2) == nullptr, "group engines");
+    aipstack_chksum_engine_test_inject_only(e1);
+    aipstack_chksum_engine_test_inject(0, bit(1));  // engine 1's first piece fails
+    uint64_t ta = 0, tb = 0, tc = 0;
+    EXPECT(aipstack_chksum_engine_group_submit_strided(g, a.data(), kLen, kLen, n, oa.data(), 0,
+                                                       &ta) == 0, "group submit A");
+    int ds[2] = {-100, -100};
+    const int wa = aipstack_chksum_engine_group_wait(g, ta, ds);
+    EXPECT(wa < 0 && ds[0] == 0 && ds[1] < 0,
+           "group wait A: device 1's failure (got %d, dev %d / %d)", wa, ds[0], ds[1]);
+    const std::vector<uint16_t> want_a = host_sums(a, n);
+    EXPECT(std::equal(oa.begin(), oa.begin() + 100, want_a.begin()),
+           "device 0's range holds its results");
+    EXPECT(aipstack_chksum_engine_group_wait(g, ta, nullptr) == 0, "a group failure is reported once");
+    aipstack_chksum_engine_test_inject(0, 0);
+    aipstack_chksum_engine_test_inject_only(nullptr);
+    // two clean tickets in flight, completed out of order
+    EXPECT(aipstack_chksum_engine_group_submit_strided(g, b.data(), kLen, kLen, n, ob.data(), 0,
+                                                       &tb) == 0, "group submit B");
+    EXPECT(aipstack_chksum_engine_group_submit_strided(g, c.data(), kLen, kLen, n, oc.data(), 0,
+                                                       &tc) == 0, "group submit C");
+    EXPECT(aipstack_chksum_engine_group_wait(g, tc, ds) == 0 && ds[0] == 0 && ds[1] == 0, "wait C");
+    int pb = 1;
+    for (int i = 0; i < 100000 && pb == 1; ++i) pb = aipstack_chksum_engine_group_poll(g, tb, ds);
+    EXPECT(pb == 0, "poll B completes (%d)", pb);
+    EXPECT(ob == host_sums(b, n) && oc == host_sums(c, n), "results of B and C");
+    // destroy with a batch pending completes it
+    std::vector<uint16_t> oa2(n);
+    EXPECT(aipstack_chksum_engine_group_submit_strided(g, a.data(), kLen, kLen, n, oa2.data(), 0,
+                                                       &ta) == 0, "group submit A again");
+    aipstack_chksum_engine_group_destroy(g);
+    EXPECT(oa2 == want_a, "group destroy completes the pending batch");
+}
+
 }  // namespace
 
 int main() {
@@ -213,6 +303,8 @@ int main() {
     destroy_completes_tx();
     unregister_in_flight();
     wait_does_not_hold_the_engine();
+    poll_answers_while_submit_is_back_pressured();
+    group_ticket_with_one_failing_device();
     if (failures) std::fprintf(stderr, "%d failures\n", failures);
     else std::printf("engine_fault_test: OK\n");
     std::fflush(nullptr);

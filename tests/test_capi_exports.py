@@ -124,3 +124,31 @@ def test_launch_shape_small_and_large_batches():
         assert shape(1 << 20)[0] == 16
     finally:
         assert lib.aipstack_chksum_tune(b"chunk_packets", 0) == 0
+
+
+def test_library_matches_its_sources():
+    """The library carries the digest of the sources it was built from
+    (aipstack_chksum_source_digest); it must equal the digest of the sources in the tree, so
+    a stale prebuilt .so fails here (and in the GPU suite's loaded-library test)."""
+    lib = _lib.load()
+    built = lib.aipstack_chksum_source_digest().decode()
+    assert len(built) == 64
+    assert built == _lib.tree_source_digest(), (
+        "libaipstack_chksum.so was not built from the sources in the tree: "
+        "make -C aipstack_amd/csrc")
+
+
+def test_source_digest_detects_a_changed_source(tmp_path):
+    """A one-byte change in any digested source changes the tree digest (what a stale
+    library is caught by): a copy of the sources with one byte flipped."""
+    import shutil
+    pkg = tmp_path / "aipstack_amd"
+    shutil.copytree(os.path.join(ROOT, "aipstack_amd", "csrc"), pkg / "csrc",
+                    ignore=shutil.ignore_patterns("build"))
+    shutil.copytree(os.path.join(ROOT, "include"), tmp_path / "include")
+    assert _lib.tree_source_digest(str(pkg)) == _lib.tree_source_digest()
+    f = pkg / "csrc" / "frame_kernels.hip"
+    data = bytearray(f.read_bytes())
+    data[100] ^= 1
+    f.write_bytes(bytes(data))
+    assert _lib.tree_source_digest(str(pkg)) != _lib.load().aipstack_chksum_source_digest().decode()

@@ -52,8 +52,13 @@ class _engine_copy_mode:
 
 
 def test_native_library_loaded_in_process():
+    """The in-tree product library is what this process runs, and it was built from the
+    sources beside it (its embedded source digest equals the tree's): a stale prebuilt .so
+    pushed to the box fails here."""
+    from aipstack_amd import _lib
     maps = open("/proc/self/maps").read()
     assert os.path.join("aipstack_amd", "lib", "libaipstack_chksum.so") in maps
+    assert _lib.load().aipstack_chksum_source_digest().decode() == _lib.tree_source_digest()
 
 
 def test_golden_flat_cases_strided_n1(golden):
@@ -1430,6 +1435,69 @@ def test_engine_group_ring_slots(oracle, devices, register):
             grp.unregister(ring)
 
 
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0]])
+def test_engine_group_async_tickets(oracle, devices):
+    """Group tickets (aipstack_chksum_engine_group_submit_* / _poll / _wait): large batches
+    split over every engine (pageable ones submitted by the devices' worker threads, registered
+    ones on the calling thread), small ones whole on one engine in turn; several tickets in
+    flight, completed out of order, every result against the oracle; a registered region is
+    read in place by every engine; each engine reports its locality."""
+    with A.ChksumEngineGroup(devices, chunk_bytes=4 << 20, nstreams=2) as grp:
+        loc = grp.locality()
+        assert len(loc) == len(devices) and all(c >= 0 for _, c in loc)
+        assert len({l for l in loc}) == 1  # one device, one locality
+        big, boff = synth.mixed_batch(200000)                      # ~160 MB: split
+        fr, foff = synth.frames_host(100000, seed=91, max_payload=1460)
+        reg, roff = synth.mixed_batch(60000)                       # registered
+        grp.register(reg)
+        assert grp.region_mapped(reg)
+        small = [synth.frames_host(64, seed=300 + i, max_payload=1460) for i in range(2 * len(devices))]
+        t_big, o_big = grp.submit_csr(big, boff, final=True)
+        want_fr = fr.copy()
+        want_st = oracle.tx_fill_batch(want_fr, foff)
+        t_tx, st_tx = grp.submit_tx_fill(fr, foff)
+        t_reg, o_reg = grp.submit_csr(reg, roff)
+        t_small = [grp.submit_rx_verify(b, o) for b, o in small]
+        for (t, out), (b, o) in zip(reversed(t_small), reversed(small)):
+            grp.wait(t)
+            assert np.array_equal(out, oracle.rx_verify_batch(b, o))
+        while not grp.poll(t_reg):
+            pass
+        assert np.array_equal(o_reg, oracle.batch_csr(reg, roff))
+        grp.wait(t_tx)
+        assert np.array_equal(st_tx, want_st) and np.array_equal(fr, want_fr)
+        assert grp.last_status == [0] * len(devices)
+        grp.wait(t_big)
+        assert np.array_equal(o_big, oracle.batch_csr(big, boff, final=True))
+        grp.wait(t_big)  # completing a ticket again is a no-op
+        ring, lens = synth.to_slots(*synth.frames_host(20000, seed=92, max_payload=1460), 2048)
+        want = ring.copy()
+        want_st = oracle.tx_fill_slotted(want, 2048, lens)
+        t, st = grp.submit_tx_fill_slotted(ring, 2048, lens)
+        t2, v = grp.submit_rx_verify_slotted(want, 2048, lens)
+        grp.wait(t2)
+        grp.wait(t)
+        assert np.array_equal(st, want_st) and np.array_equal(ring, want)
+        assert np.array_equal(v, oracle.rx_verify_slotted(want, 2048, lens))
+        grp.unregister(reg)
+
+
+def test_engine_slotted_frame_stride_limit():
+    """The engine's and the group's frame submits on slots reject slot_stride > 65536 before
+    any work; the checksum form has no such limit."""
+    ring = np.zeros(4 * 65537, dtype=np.uint8)
+    lens = np.full(4, 60, dtype=np.uint32)
+    with A.ChksumEngine(0, chunk_bytes=1 << 20) as eng:
+        with pytest.raises(A.ChksumError):
+            eng.rx_verify_slotted(ring, 65537, lens)
+        with pytest.raises(A.ChksumError):
+            eng.tx_fill_slotted(ring, 65537, lens)
+        assert eng.slotted(ring, 65537, lens).shape == (4,)
+    with A.ChksumEngineGroup([0, 0], chunk_bytes=1 << 20) as grp:
+        with pytest.raises(A.ChksumError):
+            grp.rx_verify_slotted(ring, 65537, lens)
+
+
 def test_bench_e2e_engine_group_line():
     """bench.py --e2e --engines 3 (all on device 0 here): one JSON line, bit-exact, the
     engines and their devices named."""
@@ -1732,3 +1800,21 @@ def test_chain_fill_udp_zero_as_ffff_and_skipped_fields():
     for i in range(n):
         f = 33 + 40 * i + 6
         assert (h[f], h[f + 1]) == ((0xFF, 0xFF) if i % 5 else (0, 0)), i
+
+
+@pytest.mark.parametrize("args", [["-r", "4", "256"], ["-g", "2", "-r", "4", "256"],
+                                  ["-s", "-r", "4", "64", "256"],
+                                  ["-s", "-g", "2", "-r", "4", "64"]])
+def test_ring_loop_program(args):
+    """tools/ring_loop from C++ over the C-ABI: the registered receive ring (ring mode), and
+    the descriptor-driven loop (-s): frames read() one per slot from a SOCK_SEQPACKET
+    socketpair into a registered ring and Rx-verified, frames Tx-filled in a send ring and
+    write()n to a second socketpair whose consumer compares each with the oracle's fill; with
+    one engine and with an engine group (-g 2). Every verdict and every sent frame exact."""
+    import json
+    exe = os.path.join(ROOT, "tools", "build", "ring_loop")
+    assert os.path.exists(exe), f"{exe} not built (make -C tools)"
+    r = subprocess.run([exe, *args], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert lines and all(d["parity"].startswith("bit-exact") for d in lines), lines

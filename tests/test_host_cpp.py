@@ -221,3 +221,12 @@ def test_asan_ubsan(prog, tmp_path, cases, golden):
         args.append("300000")
     out = _run(args, env=ASAN_ENV, timeout=600)
     assert "OK" in out or "0 mismatches" in out
+
+
+def test_add_even_bytes_asserts_an_even_count():
+    """Chksum.hpp's addEvenBytes asserts an even count as the reference does (Chksum.h:227),
+    under the reference's assertion configuration (AIPSTACK_CONFIG_ENABLE_ASSERTIONS)."""
+    (exe,) = _built("assert_test")
+    assert "sum" in _run([exe, "even"])
+    r = subprocess.run([exe, "odd"], capture_output=True, text=True, timeout=60)
+    assert r.returncode < 0 and "num_bytes % 2 == 0" in r.stderr, (r.returncode, r.stderr)

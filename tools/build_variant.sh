@@ -10,7 +10,7 @@ mkdir -p "$obj"
 cd "$root/aipstack_amd/csrc"
 flags="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-parameter -I../../include -I. $*"
 for f in chksum_kernels.hip frame_kernels.hip synth.hip chksum_host.cpp chksum_engine.cpp \
-         chksum_engine_group.cpp; do
+         chksum_engine_group.cpp host_threads.cpp; do
   /opt/rocm/bin/hipcc $flags -c $f -o "$obj/$f.o" &
 done
 g++ -std=c++17 -O3 -fPIC -c host_hook.cc -o "$obj/host_hook.cc.o" &

@@ -2,6 +2,9 @@
 # Round-4 GPU experiments, one mode per gpurun call; output under gpurun_out/r04/<mode>.
 #   txsect  the Tx fill forms (2-byte vs whole-sector field stores, split slotted fill):
 #           their GPU tests, then tools/tx_sweep.py on TX2K and TX, interleaved
+#   engine  the engine's host path (pool, locking) and the async engine group: their GPU
+#           tests, the fault program, e2e RX / TX with host-time stats, ring_loop latency
+#           (engine vs group of 2) and the descriptor-driven loop (-s)
 set -e
 mode=${1:?mode}
 out=gpurun_out/r04/$mode
@@ -18,6 +21,37 @@ sweep() {  # sweep NAME ARGS... -> $out/NAME.jsonl (appended)
   timeout -k 10 300 python tools/tx_sweep.py "$@" >> "$out/$name.jsonl" 2>> "$out/$name.err"
 }
 
+engine_e2e() {
+  export AIPSTACK_ENGINE_STATS=1
+  for c in RX TX; do
+    for i in 1 2; do
+      timeout -k 10 300 python bench.py --e2e --config $c --steps 5 --warmup 1 \
+          >> "$out/e2e_$c.jsonl" 2>> "$out/e2e_$c.err"
+    done
+  done
+  unset AIPSTACK_ENGINE_STATS
+  timeout -k 10 300 python bench.py --e2e --config TX --e2e-pageable --steps 3 --warmup 1 \
+      >> "$out/e2e_TX_pageable.jsonl" 2>> "$out/e2e_TX_pageable.err"
+  # the group's engines all on the box's one device
+  AIPSTACK_BENCH_FORCE_DEVICE=0 timeout -k 10 300 python bench.py --e2e --engines 2 --config C \
+      --steps 3 --warmup 1 >> "$out/e2e_group2_C.jsonl" 2>> "$out/e2e_group2_C.err"
+  AIPSTACK_BENCH_FORCE_DEVICE=0 timeout -k 10 300 python bench.py --e2e --engines 2 --config C \
+      --e2e-pageable --steps 3 --warmup 1 >> "$out/e2e_group2_C_pageable.jsonl" \
+      2>> "$out/e2e_group2_C_pageable.err"
+}
+
+engine_loops() {
+  for i in 1 2; do
+    timeout -k 10 120 tools/build/ring_loop -r 1 64 256 >> "$out/lat_engine.jsonl"
+    timeout -k 10 120 tools/build/ring_loop -g 2 -r 1 64 256 >> "$out/lat_group2.jsonl"
+    timeout -k 10 120 tools/build/ring_loop -r 8 64 1024 4096 >> "$out/loop_engine.jsonl"
+    timeout -k 10 120 tools/build/ring_loop -g 2 -r 8 64 1024 4096 >> "$out/loop_group2.jsonl"
+  done
+  timeout -k 10 200 tools/build/ring_loop -s -r 8 64 256 1024 4096 >> "$out/socket_engine.jsonl"
+  timeout -k 10 200 tools/build/ring_loop -s -r 1 64 >> "$out/socket_engine_r1.jsonl"
+  timeout -k 10 200 tools/build/ring_loop -s -g 2 -r 8 64 1024 >> "$out/socket_group2.jsonl"
+}
+
 case $mode in
 txsect)
   pyt pytest_tx -m gpu -k "tx_fill or slotted or random_frames"
@@ -25,6 +59,15 @@ txsect)
     sweep tx2k --config TX2K --variants "split=0,store=0;split=0,store=1;split=1,store=0"
     sweep tx --config TX --variants "split=1;split=0,store=0;split=0,store=1;split=0,store=1,gather=2;split=1,gather=1"
   done
+  ;;
+engine)
+  pyt pytest_engine -m gpu -k "engine or ring_loop or group"
+  engine_e2e
+  engine_loops
+  ;;
+engine2)  # the engine mode's measurements after its tests
+  engine_e2e
+  engine_loops
   ;;
 *)
   echo "unknown mode $mode" >&2; exit 2 ;;
