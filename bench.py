@@ -360,7 +360,54 @@ def cpu_baseline(spec):
     res["cpu_model"] = _cpu_model()
     res["nproc"] = os.cpu_count()
     res["affinity_cores"] = _affinity_cores()
+    hook = hook_baseline(spec, host, total, _affinity_cores(), out)
+    if hook is not None:
+        res["hook"] = hook
     return res, out
+
+
+def hook_baseline(spec, host, total, cores_all, want):
+    """The repo's own drop-in per-packet hook (libaipstack_chksum_hook: IpChksumInverted, the
+    symbol the stack links under -DAIPSTACK_EXTERNAL_CHKSUM, reference Chksum.h:46-51) timed
+    over the same host batch as the reference loop beside it, 1 thread and every affinity core
+    (tools/hook_time.cpp, the reference leg's harness). Not the reference: labelled as the
+    repo's drop-in. Its outputs are compared with the reference leg's (`want`). None when the
+    harness is not built."""
+    path = os.path.join(ROOT, "tools", "build", "libhook_time.so")
+    if not os.path.exists(path):
+        return None
+    layout, n, plen, off_host = spec["layout"], spec["n"], spec["plen"], spec["offsets"]
+    stride = spec.get("stride", plen)
+    lib = ctypes.CDLL(path)
+    lib.hook_time_batch_strided.restype = ctypes.c_double
+    lib.hook_time_batch_strided.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                            ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
+                                            ctypes.c_void_p]
+    lib.hook_time_batch_csr.restype = ctypes.c_double
+    lib.hook_time_batch_csr.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+    out = np.empty(n, dtype=np.uint16)
+    o = off_host.astype(np.uint64) if layout == "csr" else None
+
+    def timed(threads, reps):
+        if layout == "csr":
+            return lib.hook_time_batch_csr(threads, reps, host.ctypes.data, o.ctypes.data, n,
+                                           out.ctypes.data)
+        return lib.hook_time_batch_strided(threads, reps, host.ctypes.data, stride, plen, n,
+                                           out.ctypes.data)
+
+    t1 = timed(1, CPU_REPS)
+    res = {"value": round(total / t1 / 2**30, 3), "unit": "GiB/s", "cores": 1,
+           "kind": "repo drop-in hook (libaipstack_chksum_hook IpChksumInverted; AVX-512 / "
+                   "AVX2 / SSE2 body picked at load), not the reference",
+           "sample": f"the same batch as the reference leg, median of {CPU_REPS} passes, "
+                     "1 thread",
+           "matches_reference": bool(np.array_equal(out, want))}
+    if cores_all > 1:
+        tn = timed(cores_all, 5)
+        res["all_cores"] = {"value": round(total / tn / 2**30, 3), "threads": cores_all,
+                            "sample": "disjoint packet ranges per std::thread, median of 5"}
+    return res
 
 
 def cpu_baseline_chain(chain):

@@ -207,3 +207,21 @@ def test_device_code_digest_reads_the_fatbin():
         f.write(b"not an elf")
         f.flush()
         assert bench.device_code_digest(f.name) is None
+
+
+@pytest.mark.parametrize("config", ["A", "C"])
+def test_cpu_baseline_carries_the_hook(config):
+    """The N=1 line's cpu_baseline gains a `hook` entry: the repo's drop-in
+    libaipstack_chksum_hook IpChksumInverted over the same batch, 1 thread and every affinity
+    core, labelled as the repo's (not the reference), its outputs equal to the reference
+    leg's."""
+    import subprocess
+    subprocess.run(["make", "-C", os.path.join(ROOT, "tools"), "build/libhook_time.so"],
+                   check=True, stdout=subprocess.DEVNULL)
+    spec = bench.shard_spec(config, 0, 1, n=4000)
+    res, out = bench.cpu_baseline(spec)
+    hook = res["hook"]
+    assert hook["value"] > 0 and hook["cores"] == 1 and "not the reference" in hook["kind"]
+    assert hook["matches_reference"] is True
+    if res["affinity_cores"] > 1:
+        assert hook["all_cores"]["threads"] == res["affinity_cores"]
