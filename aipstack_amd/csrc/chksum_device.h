@@ -10,6 +10,7 @@
 #include <cstdint>
 
 #include "aipstack_amd/chksum.h"
+#include "chksum_internal.h"
 
 namespace aipstack_amd {
 namespace {
@@ -29,6 +30,35 @@ __device__ uint32_t g_violations;
 __device__ __forceinline__ void note_violation(bool bad, uint32_t bit) {
     if (__builtin_amdgcn_ballot_w64(bad) != 0 && bad)
         __hip_atomic_fetch_or(&g_violations, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Reads this translation unit's violation word into *out -- and clears it in the same atomic
+// exchange when `clear`, so a bit a kernel sets meanwhile is either returned or kept, never
+// lost (a read and a separate clear could drop it). One thread, on its own stream.
+__global__ void take_violations_kernel(uint32_t *out, uint32_t clear) {
+    out[0] = clear ? __hip_atomic_exchange(&g_violations, 0u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT)
+                   : __hip_atomic_load(&g_violations, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Host side of the above for the current device: ORs the word into *mask.
+inline int take_violations_here(uint32_t *mask, bool clear) {
+    uint32_t *h = nullptr;
+    int st = check_hip(hipHostMalloc(reinterpret_cast<void **>(&h), sizeof(uint32_t),
+                                     hipHostMallocMapped));
+    if (st != AIPSTACK_CHKSUM_OK) return st;
+    *h = 0;
+    hipStream_t s = nullptr;
+    st = check_hip(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    if (st == AIPSTACK_CHKSUM_OK) {
+        hipLaunchKernelGGL(take_violations_kernel, dim3(1), dim3(1), 0, s, h, clear ? 1u : 0u);
+        st = check_hip(hipGetLastError());
+    }
+    if (st == AIPSTACK_CHKSUM_OK) st = check_hip(hipStreamSynchronize(s));
+    if (st == AIPSTACK_CHKSUM_OK) *mask |= *h;
+    if (s) (void)hipStreamDestroy(s);
+    (void)hipHostFree(h);
+    return st;
 }
 
 // ---------------------------------------------------------------------------------

@@ -39,6 +39,10 @@ int tuning_tx_header_mode(int family_default);
 constexpr int kTxStoreFields = 0, kTxStoreSectors = 1;
 int tuning_tx_store(int family_default);
 
+// Chains: chunks of at most this many bytes are read first in a group's gathered stream
+// (tunable "chain_short"; 0 = the table's order).
+int tuning_chain_short();
+
 // The contract-violation word of each kernel translation unit on the current device:
 // OR it into *mask, clear it if `clear`.
 int take_violations_batch(uint32_t *mask, bool clear);

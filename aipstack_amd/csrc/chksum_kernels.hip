@@ -182,12 +182,14 @@ __device__ __forceinline__ uint32_t parity_below(uint64_t mask, uint32_t s) {  /
     return (uint32_t)__builtin_popcountll(mask & below) & 1u;
 }
 
+// 5 waves per SIMD for the default SU = 2 (80 VGPRs); the SU = 4 tunable holds four more
+// segment quads per lane and gets 4 (at 5 it spilled 68 bytes per lane at 96 VGPRs).
 template <bool NT, int SU>
-__global__ __launch_bounds__(kBlock, 5) void chksum_chain_kernel(
+__global__ __launch_bounds__(kBlock, SU > 2 ? 4 : 5) void chksum_chain_kernel(
     const uint64_t *__restrict__ chunk_addr, const uint32_t *__restrict__ chunk_len,
     const uint64_t *__restrict__ index, const uint32_t *__restrict__ states, uint64_t n,
     uint32_t chunks_per_wave, uint32_t chains_per_group, uint16_t *__restrict__ out,
-    uint32_t flags) {
+    uint32_t flags, uint32_t short_first) {
     __shared__ uint64_t lds_acc[kWavesPerBlock][kWave];  // per-chain sum of chunk sums
     __shared__ int lds_mark[kWavesPerBlock][kWave];      // chain starting at chunk lane
     __shared__ GatherLds lds_gather[kWavesPerBlock];                  // gathered stream owners
@@ -256,10 +258,32 @@ __global__ __launch_bounds__(kBlock, 5) void chksum_chain_kernel(
             const uint32_t s = before ? 0u : scs - kr;
             uint32_t q = parity_below(odd, (uint32_t)lane) ^ parity_below(odd, s);
             if (before) q ^= carry_par;
-            // the 64 chunk sums: one gathered stream over just the chunks' bytes
-            const uint32_t sums =
-                sum_gathered_chunks<SU, NT>(a, valid ? l : 0u, lane, &lds_gather[wave_in_block],
-                                            lds_keep);
+            // the 64 chunk sums: one gathered stream over just the chunks' bytes. Short chunks
+            // (<= short_first bytes) go first in the stream (round 4): a TCP Tx chain's header
+            // nodes usually lie side by side in their own array, and read together they are whole
+            // lines instead of one 32-byte piece between two payloads' windows each (CHAIN:
+            // 20-byte nodes at a 32-byte stride). Any order gives the same sums; each chunk's
+            // sum returns to its lane through the inverse permutation.
+            uint32_t sums;
+            const uint32_t lv = valid ? l : 0u;
+            if (short_first) {
+                const bool sc = lv != 0 && lv <= short_first;
+                const uint64_t sm = __builtin_amdgcn_ballot_w64(sc);
+                const uint32_t below_s = __builtin_amdgcn_mbcnt_hi(
+                    (uint32_t)(sm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
+                const uint32_t rank = sc ? below_s
+                                         : (uint32_t)__builtin_popcountll(sm) + (uint32_t)lane - below_s;
+                const int to = (int)(rank << 2);
+                const uint32_t a_lo = (uint32_t)__builtin_amdgcn_ds_permute(to, (int)(uint32_t)a);
+                const uint32_t a_hi = (uint32_t)__builtin_amdgcn_ds_permute(to, (int)(uint32_t)(a >> 32));
+                const uint32_t l_p = (uint32_t)__builtin_amdgcn_ds_permute(to, (int)lv);
+                const uint32_t s_p = sum_gathered_chunks<SU, NT>(
+                    ((uint64_t)a_hi << 32) | a_lo, l_p, lane, &lds_gather[wave_in_block], lds_keep);
+                sums = (uint32_t)__builtin_amdgcn_ds_bpermute(to, (int)s_p);
+            } else {
+                sums = sum_gathered_chunks<SU, NT>(a, lv, lane, &lds_gather[wave_in_block],
+                                                   lds_keep);
+            }
             uint32_t r = fold16(sums);
             if ((uint32_t)(a & 1) == q)
                 r = bswap16(r);
@@ -311,6 +335,8 @@ struct Tuning {
                                           // touched up front; else by kind of Tx launch
     std::atomic<int> tx_store{-1};        // in-place Tx fills: 0 = 2-byte field stores, 1 =
                                           // whole sectors; else the default
+    std::atomic<int> chain_short{128};    // chains: chunks of at most this many bytes first in
+                                          // the gathered stream (0 = table order)
     // host engine (read when an engine is created, chksum_engine.cpp):
     std::atomic<int> engine_zero_copy{1};         // kernels read registered input in place
     std::atomic<int> engine_zero_copy_small{65536};  // pieces of at most this many packets
@@ -332,6 +358,7 @@ struct Tuning {
         env("AIPSTACK_CHKSUM_CHUNK_PACKETS", chunk_packets);
         env("AIPSTACK_CHKSUM_TX_GATHER", tx_gather);
         env("AIPSTACK_CHKSUM_TX_STORE", tx_store);
+        env("AIPSTACK_CHKSUM_CHAIN_SHORT", chain_short);
         env("AIPSTACK_ENGINE_ZERO_COPY", engine_zero_copy);
         env("AIPSTACK_ENGINE_ZERO_COPY_SMALL", engine_zero_copy_small);
         env("AIPSTACK_ENGINE_PAGEABLE_ROWS", engine_pageable_rows);
@@ -512,7 +539,7 @@ int launch_chain(const uint64_t *d_addr, const uint32_t *d_len, const uint64_t *
     if (blocks > 0x7FFFFFFFull || cpw > 0xFFFFFFFFull) return AIPSTACK_CHKSUM_EINVAL;
     hipLaunchKernelGGL((chksum_chain_kernel<NT, SU>), dim3((unsigned)blocks), dim3(kBlock), 0,
                        stream, d_addr, d_len, d_index, d_states, n, (uint32_t)cpw, cpg, d_out,
-                       flags);
+                       flags, (uint32_t)tuning_chain_short());
     if (d_fields) {  // chain fill: the field stores as a pass of their own
         const int st = check_hip(hipGetLastError());
         if (st != AIPSTACK_CHKSUM_OK) return st;
@@ -526,15 +553,7 @@ int launch_chain(const uint64_t *d_addr, const uint32_t *d_len, const uint64_t *
 }  // namespace
 
 int take_violations_batch(uint32_t *mask, bool clear) {
-    uint32_t v = 0;
-    int st = check_hip(hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_violations), sizeof(v)));
-    if (st != AIPSTACK_CHKSUM_OK) return st;
-    *mask |= v;
-    if (clear && v) {
-        const uint32_t z = 0;
-        st = check_hip(hipMemcpyToSymbol(HIP_SYMBOL(g_violations), &z, sizeof(z)));
-    }
-    return st;
+    return take_violations_here(mask, clear);
 }
 
 int tuning_waves_per_cu() {
@@ -563,6 +582,11 @@ int tuning_chunk_packets() { return tuning().chunk_packets.load(std::memory_orde
 int tuning_tx_header_mode(int family_default) {
     const int t = tuning().tx_gather.load(std::memory_order_relaxed);
     return (t >= 0 && t <= 2) ? t : family_default;
+}
+
+int tuning_chain_short() {
+    const int t = tuning().chain_short.load(std::memory_order_relaxed);
+    return t < 0 ? 0 : (t > 65535 ? 65535 : t);
 }
 
 int tuning_tx_store(int family_default) {
@@ -645,6 +669,7 @@ extern "C" int aipstack_chksum_tune(const char *key, int value) {
     else if (!std::strcmp(key, "chunk_packets")) t.chunk_packets = value;
     else if (!std::strcmp(key, "tx_gather")) t.tx_gather = value;
     else if (!std::strcmp(key, "tx_store")) t.tx_store = value;
+    else if (!std::strcmp(key, "chain_short")) t.chain_short = value;
     else if (!std::strcmp(key, "engine_zero_copy")) t.engine_zero_copy = value;
     else if (!std::strcmp(key, "engine_zero_copy_small")) t.engine_zero_copy_small = value;
     else if (!std::strcmp(key, "engine_pageable_rows")) t.engine_pageable_rows = value;

@@ -940,15 +940,7 @@ int launch_frames_slotted(const void *d_base, uint64_t slot_stride, const uint32
 }
 
 int take_violations_frames(uint32_t *mask, bool clear) {
-    uint32_t v = 0;
-    int st = check_hip(hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_violations), sizeof(v)));
-    if (st != AIPSTACK_CHKSUM_OK) return st;
-    *mask |= v;
-    if (clear && v) {
-        const uint32_t z = 0;
-        st = check_hip(hipMemcpyToSymbol(HIP_SYMBOL(g_violations), &z, sizeof(z)));
-    }
-    return st;
+    return take_violations_here(mask, clear);
 }
 
 }  // namespace aipstack_amd

@@ -431,8 +431,9 @@ int aipstack_chksum_engine_group_wait(aipstack_chksum_engine_group *group, uint6
  *                result: the exact sum up to 2^26 bytes, else 0; frames: NOT_IP4)
  *   _CHUNK_LEN   a chain chunk longer than 65535 bytes (summed as an empty chunk)
  *   _SPAN        64 consecutive frames spanning more than 4 MiB (their headers read as 0)
- * aipstack_chksum_contract_violations waits for the device to go idle (hipDeviceSynchronize),
- * then stores the bits in *mask and clears them if `clear` is non-zero. */
+ * aipstack_chksum_contract_violations synchronises the whole device (hipDeviceSynchronize:
+ * every stream of every engine on it waits), then stores the bits in *mask and, if `clear` is
+ * non-zero, clears them in the same atomic exchange (a bit set meanwhile is never lost). */
 #define AIPSTACK_CHKSUM_VIOLATION_PACKET_LEN 1u
 #define AIPSTACK_CHKSUM_VIOLATION_CHUNK_LEN  2u
 #define AIPSTACK_CHKSUM_VIOLATION_SPAN       4u
@@ -461,7 +462,8 @@ int aipstack_chksum_device_check(int device);
  * segments: 0 per-lane loads, 1 captured from the stream, 2 captured + the two field lines
  * touched up front; -1 = by kind of launch), "tx_store" (how the in-place Tx fills write the
  * two checksum fields: 0 = 2-byte stores, 1 = the fields' whole 32-byte sectors from the header
- * bytes the kernel holds; -1 = the default). Process-wide; results never depend on them.
+ * bytes the kernel holds; -1 = the default), "chain_short" (chained batches: chunks of at most
+ * this many bytes are read first in each 64-chunk group, 0 = the table's order). Process-wide; results never depend on them.
  * Returns _OK or _EINVAL for an unknown key. */
 int aipstack_chksum_tune(const char *key, int value);
 

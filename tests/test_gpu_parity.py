@@ -628,12 +628,23 @@ def _chain_tables(golden, db):
             np.array(want, dtype=np.uint16))
 
 
+@pytest.fixture
+def chain_short():
+    """Setter for the chain_short tunable (chunks of at most this many bytes first in each
+    group's gathered stream; 0 = table order); restores the default (128) afterwards."""
+    yield lambda v: _tune("chain_short", v)
+    _tune("chain_short", 128)
+
+
+@pytest.mark.parametrize("short", [0, 128, 65535])
 @pytest.mark.parametrize("su", [0, -1])
-def test_chain_golden_reference_cases(golden, stream_mode, su):
+def test_chain_golden_reference_cases(golden, stream_mode, chain_short, su, short):
     """All 3,609 reference chain cases (the 512-node 0x00FF KAT, the chain==flat splits,
     scatter chains with states/offsets/tot_len) in ONE GPU batch; with and without the
-    stream runs over chunks that lie close together."""
+    stream runs over chunks that lie close together; chunks in table order, short ones
+    first (the default) and every chunk counted short (the partition then keeps table order)."""
     stream_mode(su)
+    chain_short(short)
     db = _d(golden["blob"])
     addr, ln, idx, st, want = _chain_tables(golden, db)
     got = _np(A.chksum_batch_chain(_d(addr.view(np.int64)), _d(ln.view(np.int32)),
@@ -726,11 +737,13 @@ def test_chain_flatten_and_null_states(oracle):
     assert np.array_equal(got, np.array(want, dtype=np.uint16))
 
 
+@pytest.mark.parametrize("short", [0, 128])
 @pytest.mark.parametrize("su", [0, -1])
-def test_chain_tcp_tx_shape(oracle, stream_mode, su):
+def test_chain_tcp_tx_shape(oracle, stream_mode, chain_short, su, short):
     """TCP Tx shape (tcp/IpTcpProto_output.h:1251-1277): pseudo-header state + header node
     + up to 2 send-ring chunks (utils/TcpRingBufferUtils.h:51), 100k segments."""
     stream_mode(su)
+    chain_short(short)
     rng = np.random.default_rng(9)
     ring = rng.integers(0, 256, size=1 << 22, dtype=np.uint8)
     hdrs = rng.integers(0, 256, size=100000 * 60, dtype=np.uint8)
@@ -764,11 +777,13 @@ def test_chain_tcp_tx_shape(oracle, stream_mode, su):
     assert np.array_equal(got, np.array(want, dtype=np.uint16))
 
 
+@pytest.mark.parametrize("short", [0, 128])
 @pytest.mark.parametrize("su", [2, 4, 8, -1])
-def test_chain_bench_shape(su, stream_mode):
+def test_chain_bench_shape(su, stream_mode, chain_short, short):
     """bench.py's CHAIN layout (20-B header nodes at a 32-B stride + a contiguous payload ring
     split in two chunks per chain): header and payload chunks each stream as one run."""
     stream_mode(su)
+    chain_short(short)
     sys.path.insert(0, ROOT)
     import bench
     spec = {"n": 50000, "seed": 77}

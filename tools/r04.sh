@@ -2,6 +2,8 @@
 # Round-4 GPU experiments, one mode per gpurun call; output under gpurun_out/r04/<mode>.
 #   txsect  the Tx fill forms (2-byte vs whole-sector field stores, split slotted fill):
 #           their GPU tests, then tools/tx_sweep.py on TX2K and TX, interleaved
+#   kern    chained batches with short chunks first (chain_short 0 vs 128): GPU tests,
+#           alternating CHAIN bench lines, FETCH_SIZE / VALU per variant; C2K launch shapes
 #   engine  the engine's host path (pool, locking) and the async engine group: their GPU
 #           tests, the fault program, e2e RX / TX with host-time stats, ring_loop latency
 #           (engine vs group of 2) and the descriptor-driven loop (-s)
@@ -52,7 +54,34 @@ engine_loops() {
   timeout -k 10 200 tools/build/ring_loop -s -g 2 -r 8 64 1024 >> "$out/socket_group2.jsonl"
 }
 
+bench() {  # bench NAME ARGS... -> $out/NAME.jsonl (appended)
+  name=$1; shift
+  timeout -k 10 300 python bench.py "$@" >> "$out/$name.jsonl" 2>> "$out/$name.err"
+}
+pmc1() {  # pmc1 NAME CONFIG COUNTERS...: one PMC pass of a bench config (env passes through)
+  name=$1; cfg=$2; shift 2
+  timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d "$out/pmc_$name" -o run \
+      --pmc "$@" -- python3 bench.py --config "$cfg" --no-cpu-baseline --no-parity \
+      --steps 5 --warmup 2 > "$out/pmc_$name.log" 2>&1
+}
+
 case $mode in
+kern)
+  pyt pytest_kern -m gpu -k "chain or contract_violations or native_library"
+  for i in 1 2 3; do
+    AIPSTACK_CHKSUM_CHAIN_SHORT=0 bench chain_table --config CHAIN --per-launch --no-cpu-baseline
+    bench chain_short --config CHAIN --per-launch --no-cpu-baseline
+  done
+  AIPSTACK_CHKSUM_CHAIN_SHORT=0 pmc1 chain_table_fetch CHAIN FETCH_SIZE
+  pmc1 chain_short_fetch CHAIN FETCH_SIZE
+  AIPSTACK_CHKSUM_CHAIN_SHORT=0 pmc1 chain_table_sq CHAIN SQ_INSTS_VALU SQ_INSTS_SALU
+  pmc1 chain_short_sq CHAIN SQ_INSTS_VALU SQ_INSTS_SALU
+  timeout -k 10 300 python tools/slot_sweep.py --config C2K --rounds 6 --variants \
+      "chunk_packets=16;stream=2,chunk_packets=16;stream=8,chunk_packets=16;chunk_packets=32;stream=2,chunk_packets=32;stream=8,chunk_packets=32;chunk_packets=8" \
+      > "$out/c2k_sweep.jsonl" 2> "$out/c2k_sweep.err"
+  pmc1 c2k_sq C2K SQ_INSTS_VALU SQ_INSTS_SALU
+  AIPSTACK_CHKSUM_CHUNK_PACKETS=32 pmc1 c2k_32_sq C2K SQ_INSTS_VALU SQ_INSTS_SALU
+  ;;
 txsect)
   pyt pytest_tx -m gpu -k "tx_fill or slotted or random_frames"
   for i in 1 2; do
