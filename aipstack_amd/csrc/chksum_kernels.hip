@@ -258,12 +258,13 @@ __global__ __launch_bounds__(kBlock, SU > 2 ? 4 : 5) void chksum_chain_kernel(
             const uint32_t s = before ? 0u : scs - kr;
             uint32_t q = parity_below(odd, (uint32_t)lane) ^ parity_below(odd, s);
             if (before) q ^= carry_par;
-            // the 64 chunk sums: one gathered stream over just the chunks' bytes. Short chunks
-            // (<= short_first bytes) go first in the stream (round 4): a TCP Tx chain's header
-            // nodes usually lie side by side in their own array, and read together they are whole
-            // lines instead of one 32-byte piece between two payloads' windows each (CHAIN:
-            // 20-byte nodes at a 32-byte stride). Any order gives the same sums; each chunk's
-            // sum returns to its lane through the inverse permutation.
+            // the 64 chunk sums: one gathered stream over just the chunks' bytes. With
+            // short_first (tunable "chain_short", round 4; off by default), chunks of at most
+            // that many bytes go first in the stream, so that header nodes lying side by side
+            // are read together as whole lines rather than one 32-byte piece between two
+            // payloads' windows each; any order gives the same sums, each chunk's sum returns
+            // to its lane through the inverse permutation. Measured on CHAIN: FETCH_SIZE -0.5 %
+            // and 2 us slower (profiles/r04/kern), so the table's order stays.
             uint32_t sums;
             const uint32_t lv = valid ? l : 0u;
             if (short_first) {
@@ -335,8 +336,10 @@ struct Tuning {
                                           // touched up front; else by kind of Tx launch
     std::atomic<int> tx_store{-1};        // in-place Tx fills: 0 = 2-byte field stores, 1 =
                                           // whole sectors; else the default
-    std::atomic<int> chain_short{128};    // chains: chunks of at most this many bytes first in
-                                          // the gathered stream (0 = table order)
+    std::atomic<int> chain_short{0};      // chains: chunks of at most this many bytes first in
+                                          // the gathered stream (0 = table order; measured:
+                                          // CHAIN 250.0-250.6 us at 128 against 248.0-248.9,
+                                          // FETCH_SIZE -0.5 %, profiles/r04/kern)
     // host engine (read when an engine is created, chksum_engine.cpp):
     std::atomic<int> engine_zero_copy{1};         // kernels read registered input in place
     std::atomic<int> engine_zero_copy_small{65536};  // pieces of at most this many packets
