@@ -1048,8 +1048,9 @@ extern "C" int aipstack_chksum_engine_wait(aipstack_chksum_engine *e, uint64_t t
             if (st != 1) return st;
         }
         // its Tx records are still queued in the applier: wait for them without mu
-        // (ADVICE round 3), then collect the ticket's status
-        (void)applies_pending(e, ticket, true);
+        // (ADVICE round 3), then collect the ticket's status (a ticket whose submit is still
+        // running on another thread -- it cannot have been returned yet -- yields meanwhile)
+        if (!applies_pending(e, ticket, true)) std::this_thread::yield();
     }
 }
 

@@ -211,7 +211,15 @@ def test_capi_validation():
     assert "OK" in _run([exe])
 
 
-@pytest.mark.parametrize("prog", ["ip_chksum_test", "call_sites_test", "capi_validation_test"])
+def test_host_threads():
+    """The engines' host-thread layer: sysfs CPU-list parsing and the persistent HostPool
+    (every part once, concurrent callers, pools with 0-7 workers)."""
+    (exe,) = _built("host_threads_test")
+    assert "OK" in _run([exe])
+
+
+@pytest.mark.parametrize("prog", ["ip_chksum_test", "call_sites_test", "capi_validation_test",
+                                  "host_threads_test"])
 def test_asan_ubsan(prog, tmp_path, cases, golden):
     (exe,) = _built(f"asan/{prog}")
     args = [exe]

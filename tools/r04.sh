@@ -66,6 +66,10 @@ pmc1() {  # pmc1 NAME CONFIG COUNTERS...: one PMC pass of a bench config (env pa
 }
 
 case $mode in
+calib)  # FETCH_SIZE by access width (tools/width_calib.hip), 3 dispatches per kernel
+  timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv -d "$out/width" -o run \
+      --pmc FETCH_SIZE -- tools/build/width_calib > "$out/width.log" 2>&1
+  ;;
 kern)
   pyt pytest_kern -m gpu -k "chain or contract_violations or native_library"
   for i in 1 2 3; do
