@@ -116,6 +116,33 @@ int main() {
     CHECK(aipstack_chksum_engine_group_host_strided(nullptr, dummy, 1, 1, 1, out, 0, nullptr) == EINVAL_);
     CHECK(aipstack_chksum_engine_group_host_rx_verify(nullptr, dummy, off, 1, verdicts, nullptr) == EINVAL_);
     CHECK(aipstack_chksum_engine_group_host_tx_fill(nullptr, dummy, off, 1, verdicts, nullptr) == EINVAL_);
+    std::uint32_t lens1[1] = {60};
+    CHECK(aipstack_chksum_engine_group_submit_csr(nullptr, dummy, off, 1, out, 0, &ticket) == EINVAL_);
+    CHECK(aipstack_chksum_engine_group_submit_strided(nullptr, dummy, 1, 1, 1, out, 0, &ticket) == EINVAL_);
+    CHECK(aipstack_chksum_engine_group_submit_rx_verify(nullptr, dummy, off, 1, verdicts, &ticket) == EINVAL_);
+    CHECK(aipstack_chksum_engine_group_submit_tx_fill(nullptr, dummy, off, 1, verdicts, &ticket) == EINVAL_);
+    CHECK(aipstack_chksum_engine_group_submit_slotted(nullptr, dummy, 64, lens1, 1, out, 0, &ticket) == EINVAL_);
+    CHECK(aipstack_chksum_engine_group_submit_rx_verify_slotted(nullptr, dummy, 64, lens1, 1, verdicts,
+                                                                &ticket) == EINVAL_);
+    CHECK(aipstack_chksum_engine_group_submit_tx_fill_slotted(nullptr, dummy, 64, lens1, 1, verdicts,
+                                                              &ticket) == EINVAL_);
+    CHECK(aipstack_chksum_engine_group_poll(nullptr, 1, nullptr) == EINVAL_);
+    CHECK(aipstack_chksum_engine_group_wait(nullptr, 1, nullptr) == EINVAL_);
+    CHECK(aipstack_chksum_engine_group_engine(nullptr, 0) == nullptr);
+    CHECK(aipstack_chksum_engine_group_region_mapped(nullptr, dummy) == EINVAL_);
+    CHECK(aipstack_chksum_engine_locality(nullptr, nullptr, nullptr) == EINVAL_);
+    CHECK(aipstack_chksum_engine_region_mapped(nullptr, dummy) == EINVAL_);
+    // the frame forms on slots reject strides over AIPSTACK_CHKSUM_MAX_SLOT_STRIDE before any
+    // device work (here: no device needed)
+    CHECK(aipstack_chksum_rx_verify_slotted(dummy, AIPSTACK_CHKSUM_MAX_SLOT_STRIDE + 1, lens1, 1,
+                                            verdicts, nullptr) == EINVAL_);
+    CHECK(aipstack_chksum_tx_fill_slotted(dummy, AIPSTACK_CHKSUM_MAX_SLOT_STRIDE + 1, lens1, 1,
+                                          verdicts, nullptr) == EINVAL_);
+    CHECK(aipstack_chksum_tx_fill_slotted_split(dummy, 2048, lens1, 1, verdicts, nullptr, 8,
+                                                nullptr) == EINVAL_);  // no workspace
+    CHECK(aipstack_chksum_tx_fill_slotted_split(dummy, 2048, lens1, 1, verdicts, dummy, 4,
+                                                nullptr) == EINVAL_);  // workspace too small
+    CHECK(std::strlen(aipstack_chksum_source_digest()) == 64);
     aipstack_chksum_engine_group_destroy(nullptr);  // no-op
     std::uint32_t vmask = 0;
     CHECK(aipstack_chksum_contract_violations(0, nullptr, 1) == EINVAL_);
