@@ -66,9 +66,15 @@ pmc1() {  # pmc1 NAME CONFIG COUNTERS...: one PMC pass of a bench config (env pa
 }
 
 case $mode in
-calib)  # FETCH_SIZE by access width (tools/width_calib.hip), 3 dispatches per kernel
+calib)  # FETCH_SIZE by access width (tools/width_calib.hip), 3 dispatches per kernel;
+        # CHAIN at 4 stream windows (no spill since round 4) against the default 2
   timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv -d "$out/width" -o run \
       --pmc FETCH_SIZE -- tools/build/width_calib > "$out/width.log" 2>&1
+  for i in 1 2 3; do
+    bench chain_su2 --config CHAIN --per-launch --no-cpu-baseline
+    AIPSTACK_CHKSUM_STREAM=4 bench chain_su4 --config CHAIN --per-launch --no-cpu-baseline
+  done
+  sweep tx2k_frames --config TX2K --variants "frames=4;frames=2;frames=8;frames=4,split=1;frames=8,split=1"
   ;;
 kern)
   pyt pytest_kern -m gpu -k "chain or contract_violations or native_library"
