@@ -40,7 +40,7 @@ constexpr int kTxStoreFields = 0, kTxStoreSectors = 1;
 int tuning_tx_store(int family_default);
 
 // Chains: chunks of at most this many bytes are read first in a group's gathered stream
-// (tunable "chain_short"; 0 = the table's order).
+// (tunable "chain_short"; 0 = the table's order, -1 = the default, 128).
 int tuning_chain_short();
 
 // The contract-violation word of each kernel translation unit on the current device:

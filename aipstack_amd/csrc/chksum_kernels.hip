@@ -182,8 +182,8 @@ __device__ __forceinline__ uint32_t parity_below(uint64_t mask, uint32_t s) {  /
     return (uint32_t)__builtin_popcountll(mask & below) & 1u;
 }
 
-// 5 waves per SIMD for the default SU = 2 (80 VGPRs); the SU = 4 tunable holds four more
-// segment quads per lane and gets 4 (at 5 it spilled 68 bytes per lane at 96 VGPRs).
+// SU = 4 (the default since round 4) holds four more segment quads per lane than SU = 2 and
+// gets 4 waves per SIMD (at 5 it spilled 68 bytes per lane at 96 VGPRs); SU = 2 keeps 5.
 template <bool NT, int SU>
 __global__ __launch_bounds__(kBlock, SU > 2 ? 4 : 5) void chksum_chain_kernel(
     const uint64_t *__restrict__ chunk_addr, const uint32_t *__restrict__ chunk_len,
@@ -210,9 +210,11 @@ __global__ __launch_bounds__(kBlock, SU > 2 ? 4 : 5) void chksum_chain_kernel(
 
     for (; c < c_end; ++c) {
         const uint64_t p0 = c * cpg;
-        const auto grp = idx_desc.begin_chunk(p0, n, lane);
         const int cnt = (int)min(cpg, n - p0);
-        const uint32_t state = (states != nullptr && p0 + lane < n) ? states[p0 + lane] : 0u;
+        // only the group's cnt + 1 index entries and cnt states: lanes past them re-read
+        // entry p0 + cnt (one line), so no wave fetches the next groups' table lines
+        const auto grp = idx_desc.begin_chunk(p0, p0 + (uint64_t)cnt, lane);
+        const uint32_t state = (states != nullptr && lane < cnt) ? states[p0 + lane] : 0u;
         // chain `lane` = chunks [cs, ce) (relative to the group's first chunk K0)
         uint64_t cs64, ce64;
         idx_desc.lane_bounds(grp, lane, cs64, ce64);
@@ -259,16 +261,28 @@ __global__ __launch_bounds__(kBlock, SU > 2 ? 4 : 5) void chksum_chain_kernel(
             uint32_t q = parity_below(odd, (uint32_t)lane) ^ parity_below(odd, s);
             if (before) q ^= carry_par;
             // the 64 chunk sums: one gathered stream over just the chunks' bytes. With
-            // short_first (tunable "chain_short", round 4; off by default), chunks of at most
-            // that many bytes go first in the stream, so that header nodes lying side by side
-            // are read together as whole lines rather than one 32-byte piece between two
-            // payloads' windows each; any order gives the same sums, each chunk's sum returns
-            // to its lane through the inverse permutation. Measured on CHAIN: FETCH_SIZE -0.5 %
-            // and 2 us slower (profiles/r04/kern), so the table's order stays.
+            // short_first (tunable "chain_short", default 128 since round 4; 0 = the table's
+            // order), chunks of at most that many bytes that share no line with their
+            // neighbours in the table go first in the stream, so that header nodes lying side
+            // by side are read together as whole lines rather than one 32-byte piece between
+            // two payloads' windows each (the nontemporal stream keeps no line cached until
+            // the next header's turn). Any order gives the same sums: each chunk's sum
+            // returns to its lane through the inverse permutation. CHAIN: FETCH_SIZE -1.3 %,
+            // 241.0-241.7 vs 241.9-242.9 us (profiles/r04/short, probe).
             uint32_t sums;
             const uint32_t lv = valid ? l : 0u;
             if (short_first) {
-                const bool sc = lv != 0 && lv <= short_first;
+                // a short chunk goes first only if it shares no line with its neighbours in
+                // the table (a header node apart from the payload; a short payload piece
+                // stays beside the pieces it shares lines with)
+                const uint32_t line_s = (uint32_t)(a >> 7);
+                const uint32_t line_e = (uint32_t)((a + lv - 1u) >> 7);
+                const uint32_t prev_e =
+                    (uint32_t)__builtin_amdgcn_ds_bpermute((lane - 1) << 2, (int)line_e);
+                const uint32_t next_s =
+                    (uint32_t)__builtin_amdgcn_ds_bpermute((lane + 1) << 2, (int)line_s);
+                const bool sc = lv != 0 && lv <= short_first && prev_e != line_s &&
+                                next_s != line_e;
                 const uint64_t sm = __builtin_amdgcn_ballot_w64(sc);
                 const uint32_t below_s = __builtin_amdgcn_mbcnt_hi(
                     (uint32_t)(sm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
@@ -336,7 +350,7 @@ struct Tuning {
                                           // touched up front; else by kind of Tx launch
     std::atomic<int> tx_store{-1};        // in-place Tx fills: 0 = 2-byte field stores, 1 =
                                           // whole sectors; else the default
-    std::atomic<int> chain_short{0};      // chains: chunks of at most this many bytes first in
+    std::atomic<int> chain_short{-1};      // chains: chunks of at most this many bytes first in
                                           // the gathered stream (0 = table order; measured:
                                           // CHAIN 250.0-250.6 us at 128 against 248.0-248.9,
                                           // FETCH_SIZE -0.5 %, profiles/r04/kern)
@@ -589,7 +603,7 @@ int tuning_tx_header_mode(int family_default) {
 
 int tuning_chain_short() {
     const int t = tuning().chain_short.load(std::memory_order_relaxed);
-    return t < 0 ? 0 : (t > 65535 ? 65535 : t);
+    return t < 0 ? 128 : (t > 65535 ? 65535 : t);
 }
 
 int tuning_tx_store(int family_default) {
@@ -702,8 +716,10 @@ int chain_batch(const uint64_t *d_chunk_addr, const uint32_t *d_chunk_len,
     return launch_chain<NT, SU>(d_chunk_addr, d_chunk_len, d_chunk_index, d_states, d_fields, \
                                 n, d_out, flags, (hipStream_t)stream)
     if (!tuning().nontemporal.load(std::memory_order_relaxed)) AIPSTACK_LAUNCH_CHAIN(false, 2);
-    if (tuning_stream_windows(2) == 4) AIPSTACK_LAUNCH_CHAIN(true, 4);
-    AIPSTACK_LAUNCH_CHAIN(true, 2);
+    // 4 windows in flight (round 4, once the SU = 4 kernel no longer spilled): CHAIN 242.0-242.4
+    // against 248.3-248.4 us with 2, alternating processes (profiles/r04/calib)
+    if (tuning_stream_windows(4) == 2) AIPSTACK_LAUNCH_CHAIN(true, 2);
+    AIPSTACK_LAUNCH_CHAIN(true, 4);
 #undef AIPSTACK_LAUNCH_CHAIN
 }
 }  // namespace

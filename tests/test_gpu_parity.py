@@ -630,10 +630,11 @@ def _chain_tables(golden, db):
 
 @pytest.fixture
 def chain_short():
-    """Setter for the chain_short tunable (chunks of at most this many bytes first in each
-    group's gathered stream; 0 = table order); restores the default (0) afterwards."""
+    """Setter for the chain_short tunable (chunks of at most this many bytes that share no
+    line with their table neighbours first in each group's gathered stream; 0 = table
+    order); restores the default (-1: 128) afterwards."""
     yield lambda v: _tune("chain_short", v)
-    _tune("chain_short", 0)
+    _tune("chain_short", -1)
 
 
 @pytest.mark.parametrize("short", [0, 128, 65535])
@@ -641,8 +642,8 @@ def chain_short():
 def test_chain_golden_reference_cases(golden, stream_mode, chain_short, su, short):
     """All 3,609 reference chain cases (the 512-node 0x00FF KAT, the chain==flat splits,
     scatter chains with states/offsets/tot_len) in ONE GPU batch; with and without the
-    stream runs over chunks that lie close together; chunks in table order (the default),
-    short ones first and every chunk counted short (the partition then keeps table order)."""
+    stream runs over chunks that lie close together; chunks in table order, short ones
+    apart from their neighbours' lines first (the default) and every chunk counted short."""
     stream_mode(su)
     chain_short(short)
     db = _d(golden["blob"])

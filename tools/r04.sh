@@ -76,6 +76,41 @@ calib)  # FETCH_SIZE by access width (tools/width_calib.hip), 3 dispatches per k
   done
   sweep tx2k_frames --config TX2K --variants "frames=4;frames=2;frames=8;frames=4,split=1;frames=8,split=1"
   ;;
+chain)  # CHAIN at its round-4 defaults (4 stream windows, group-bounded table reads): tests,
+        # bench lines, rocprof stats, PMC; tools/chain_probe.py's layouts under FETCH_SIZE
+  pyt pytest_chain -m gpu -k "chain or native_library"
+  for i in 1 2; do bench chain --config CHAIN --per-launch; done
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/prof_CHAIN" -o run \
+      -- python3 bench.py --config CHAIN --no-cpu-baseline --no-parity > "$out/prof_CHAIN.log" 2>&1
+  tools/pmc_run.sh CHAIN "$out/pmc_CHAIN"
+  ;&
+probe)  # tools/chain_probe.py's layouts under FETCH_SIZE, then timed, per launch variant
+        # (VARIANTS: space-separated, each a comma-separated list of AIPSTACK_CHKSUM_ settings)
+  for v in ${VARIANTS:-base CHAIN_SHORT=128}; do
+    name=${v//=/}; name=${name//,/_}
+    (
+      if [ "$v" != base ]; then
+        for kv in ${v//,/ }; do export "AIPSTACK_CHKSUM_$kv"; done
+      fi
+      timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d "$out/probe_$name" -o run \
+          --pmc FETCH_SIZE -- python3 tools/chain_probe.py > "$out/probe_$name.jsonl" \
+          2> "$out/probe_$name.err"
+      python3 tools/chain_probe.py --summarize "$out/probe_$name/run_counter_collection.csv" \
+          "$out/probe_$name.jsonl" > "$out/probe_${name}_fetch.jsonl"
+      timeout -k 10 240 python3 tools/chain_probe.py --reps 30 > "$out/probe_${name}_timing.jsonl" \
+          2>> "$out/probe_$name.err"
+    )
+  done
+  ;;
+short)  # neighbour-aware short chunks first in chained batches: GPU tests, CHAIN A/B, the probe
+  pyt pytest_short -m gpu -k "chain or native_library"
+  for i in 1 2 3; do
+    bench chain_table --config CHAIN --per-launch --no-cpu-baseline
+    AIPSTACK_CHKSUM_CHAIN_SHORT=128 bench chain_short128 --config CHAIN --per-launch --no-cpu-baseline
+    AIPSTACK_CHKSUM_CHAIN_SHORT=32 bench chain_short32 --config CHAIN --per-launch --no-cpu-baseline
+  done
+  VARIANTS="base CHAIN_SHORT=128 CHAIN_SHORT=32" "$0" probe
+  ;;
 kern)
   pyt pytest_kern -m gpu -k "chain or contract_violations or native_library"
   for i in 1 2 3; do
