@@ -409,8 +409,9 @@ extern "C" int aipstack_chksum_engine_group_submit_strided(aipstack_chksum_engin
                                                            uint32_t len, uint64_t n,
                                                            uint16_t *h_out, uint32_t flags,
                                                            uint64_t *ticket) {
-    if (!g || !h_base || !h_out || !ticket || len > AIPSTACK_CHKSUM_MAX_LEN)
-        return AIPSTACK_CHKSUM_EINVAL;
+    if (!g || !h_base || !h_out || !ticket) return AIPSTACK_CHKSUM_EINVAL;
+    *ticket = 0;
+    if (len > AIPSTACK_CHKSUM_MAX_LEN) return AIPSTACK_CHKSUM_EINVAL;
     const char *b = static_cast<const char *>(h_base);
     const uint64_t span = n ? (n - 1) * stride + len : 0;
     return group_submit(g, n, b, span, [=](uint64_t i) { return i * stride; },
@@ -427,6 +428,7 @@ namespace {
 template <class Submit>
 int submit_csr_like(aipstack_chksum_engine_group *g, const void *h_base, const uint64_t *h_offsets,
                     uint64_t n, Submit submit, uint64_t *ticket) {
+    *ticket = 0;
     if (!csr_ok(h_offsets, n)) return AIPSTACK_CHKSUM_EINVAL;
     const char *b = static_cast<const char *>(h_base);
     return group_submit(g, n, b + h_offsets[0], h_offsets[n] - h_offsets[0],
@@ -483,6 +485,7 @@ namespace {
 template <class Submit>
 int submit_slotted_like(aipstack_chksum_engine_group *g, const void *h_base, uint64_t slot_stride,
                         const uint32_t *h_len, uint64_t n, Submit submit, uint64_t *ticket) {
+    *ticket = 0;
     if (!slots_ok(slot_stride, h_len, n)) return AIPSTACK_CHKSUM_EINVAL;
     return group_submit(g, n, h_base, n * slot_stride, [=](uint64_t i) { return i * slot_stride; },
                         [=](size_t k, uint64_t i0, uint64_t i1, uint64_t *et) {
@@ -512,8 +515,9 @@ extern "C" int aipstack_chksum_engine_group_submit_slotted(aipstack_chksum_engin
 extern "C" int aipstack_chksum_engine_group_submit_rx_verify_slotted(
     aipstack_chksum_engine_group *g, const void *h_base, uint64_t slot_stride,
     const uint32_t *h_len, uint64_t n, uint8_t *h_verdicts, uint64_t *ticket) {
-    if (!g || !h_base || !h_len || !h_verdicts || !ticket ||
-        slot_stride > AIPSTACK_CHKSUM_MAX_SLOT_STRIDE)
+    if (!g || !h_base || !h_len || !h_verdicts || !ticket) return AIPSTACK_CHKSUM_EINVAL;
+    *ticket = 0;
+    if (slot_stride > AIPSTACK_CHKSUM_MAX_SLOT_STRIDE)
         return AIPSTACK_CHKSUM_EINVAL;
     const char *b = static_cast<const char *>(h_base);
     return submit_slotted_like(
@@ -528,8 +532,9 @@ extern "C" int aipstack_chksum_engine_group_submit_rx_verify_slotted(
 extern "C" int aipstack_chksum_engine_group_submit_tx_fill_slotted(
     aipstack_chksum_engine_group *g, void *h_base, uint64_t slot_stride, const uint32_t *h_len,
     uint64_t n, uint8_t *h_status, uint64_t *ticket) {
-    if (!g || !h_base || !h_len || !h_status || !ticket ||
-        slot_stride > AIPSTACK_CHKSUM_MAX_SLOT_STRIDE)
+    if (!g || !h_base || !h_len || !h_status || !ticket) return AIPSTACK_CHKSUM_EINVAL;
+    *ticket = 0;
+    if (slot_stride > AIPSTACK_CHKSUM_MAX_SLOT_STRIDE)
         return AIPSTACK_CHKSUM_EINVAL;
     char *b = static_cast<char *>(h_base);
     return submit_slotted_like(

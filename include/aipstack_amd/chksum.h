@@ -344,7 +344,11 @@ int aipstack_chksum_engine_region_mapped(aipstack_chksum_engine *engine, const v
  * thread of its device (pinned, like the engine's own host threads, to the CPUs next to the
  * device), so the pageable staging copies of all devices run in parallel while the caller
  * goes on. Every input, output and frame buffer of a submitted batch must stay valid, and its
- * input unchanged, until the ticket completes. The host_* calls are submit + wait.
+ * input unchanged, until the ticket completes. A submit returns _OK or a negative status: the
+ * argument checks fail before anything starts (*ticket = 0); a range whose engine submit fails
+ * on the calling thread leaves *ticket set, the batch's other ranges running, and the failure
+ * reported again by _poll / _wait, which must still complete the ticket (as for one engine).
+ * The host_* calls are submit + wait.
  * _register page-locks a region once for all devices (portable, mapped into each device). */
 typedef struct aipstack_chksum_engine_group aipstack_chksum_engine_group;
 

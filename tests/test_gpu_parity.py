@@ -6,6 +6,7 @@ Covers the BASELINE configs at full size (A: 1M x 1500 B, B: 256K x 9000 B, C: 2
 a 1M shard of the 8-GPU batch) plus the edge cases the reference contract admits: empty
 batches and packets, ragged counts, odd base pointers, len 65535, FINAL flag, seeds.
 """
+import ctypes
 import os
 import subprocess
 import sys
@@ -1512,6 +1513,46 @@ def test_engine_slotted_frame_stride_limit():
     with A.ChksumEngineGroup([0, 0], chunk_bytes=1 << 20) as grp:
         with pytest.raises(A.ChksumError):
             grp.rx_verify_slotted(ring, 65537, lens)
+
+
+def test_engine_group_submit_check_failures_leave_no_ticket():
+    """A group submit whose argument checks fail returns _EINVAL before anything starts and
+    sets *ticket = 0 (chksum.h, section 4): decreasing CSR offsets, a packet over 65535 bytes,
+    a slot length over the stride, a frame slot stride over 65536."""
+    from aipstack_amd import _lib
+    lib = _lib.load()
+    buf = np.zeros(1 << 20, dtype=np.uint8)
+    out16 = np.zeros(4, dtype=np.uint16)
+    out8 = np.zeros(4, dtype=np.uint8)
+    p = lambda a: a.ctypes.data  # noqa: E731
+    with A.ChksumEngineGroup([0, 0], chunk_bytes=1 << 20) as grp:
+        t = ctypes.c_uint64(123)
+        bad = np.array([0, 100, 50], dtype=np.uint64)
+        assert lib.aipstack_chksum_engine_group_submit_csr(
+            grp._h, p(buf), p(bad), 2, p(out16), 0, ctypes.byref(t)) == A.AIPSTACK_CHKSUM_EINVAL
+        assert t.value == 0
+        t.value = 123
+        long = np.array([0, 70000], dtype=np.uint64)
+        assert lib.aipstack_chksum_engine_group_submit_rx_verify(
+            grp._h, p(buf), p(long), 1, p(out8), ctypes.byref(t)) == A.AIPSTACK_CHKSUM_EINVAL
+        assert t.value == 0
+        t.value = 123
+        lens = np.array([60, 2049], dtype=np.uint32)
+        assert lib.aipstack_chksum_engine_group_submit_slotted(
+            grp._h, p(buf), 2048, p(lens), 2, p(out16), 0, ctypes.byref(t)) == A.AIPSTACK_CHKSUM_EINVAL
+        assert t.value == 0
+        t.value = 123
+        lens = np.array([60, 60], dtype=np.uint32)
+        assert lib.aipstack_chksum_engine_group_submit_tx_fill_slotted(
+            grp._h, p(buf), 65537, p(lens), 2, p(out8), ctypes.byref(t)) == A.AIPSTACK_CHKSUM_EINVAL
+        assert t.value == 0
+        t.value = 123
+        assert lib.aipstack_chksum_engine_group_submit_strided(
+            grp._h, p(buf), 1500, 70000, 2, p(out16), 0, ctypes.byref(t)) == A.AIPSTACK_CHKSUM_EINVAL
+        assert t.value == 0
+        # a good batch still goes through afterwards
+        good = np.array([0, 1500, 3000], dtype=np.uint64)
+        assert np.array_equal(grp.csr(buf, good), np.zeros(2, dtype=np.uint16))
 
 
 def test_bench_e2e_engine_group_line():
