@@ -814,23 +814,38 @@ __device__ __forceinline__ int wave_max_scan(int v) {
 // Owners: the non-empty chunks' load parameters sit in LDS by rank; per group of U windows
 // each chunk starting there ORs its start lane into its window's 64-bit mask, and lane k of
 // window w takes rank base_w - 1 + popcount(mask bits <= k) (two mbcnt; round 2 -- a mark
-// table and a DPP max-scan per window before). The owner also tells the loading lane whether its segment is the chunk's first (bytes
-// below a_j & 15 are not the chunk's) or last (bytes from the chunk's end on are not), and
-// the lane masks those bytes off before it sums the segment ("cleaned" segments, mask table
-// in LDS). The cleaned segments of chunk j then hold exactly its bytes, so with
-// G_j = the prefix of cleaned halves-sums up to segment cs_j (a segment-aligned position: no
-// partial segment to fetch), chunk j's exact halves-sum is G_{j+1} - G_j: one boundary per
-// lane, evaluated with one ds_bpermute of the window's exclusive scan. A segment shared by
-// two chunks is loaded once for each (the second time from L2); bytes outside every chunk's
-// segments are never read, so chunks may sit in separate allocations (a 16-byte segment
-// around a mapped byte is mapped). Lanes past the stream re-read its last segment and count
-// 0, so every address stays inside a chunk.
+// table and a DPP max-scan per window before). With G_j = the prefix of whole-segment
+// halves-sums up to segment cs_j (a segment-aligned position: no partial segment to fetch),
+// G_{j+1} - G_j is the sum of chunk j's segments: one boundary per lane, evaluated with one
+// ds_bpermute of the window's exclusive scan. Those segments also hold bytes that are not the
+// chunk's -- below a_j & 15 in its first segment, from its end on in its last -- and lane j
+// subtracts them: it reads its chunk's two edge segments itself before the stream starts
+// (round 4, AIPSTACK_GATHER_MODE 1; rounds 2-3 masked them off in the stream, every lane of
+// every window looking up a keep mask, mode 0). A segment shared by two chunks is loaded once
+// for each (the second time from L2); bytes outside every chunk's segments are never read,
+// so chunks may sit in separate allocations (a 16-byte segment around a mapped byte is
+// mapped). Lanes past the stream re-read its last segment and count 0, so every address
+// stays inside a chunk.
 //
 // Software-pipelined: group g + 1's owners and loads are issued before group g is
-// consumed. The loop always runs whole pairs of groups and the next group is issued
-// unconditionally (a window past the stream sums zeros and holds no boundary), so the loads
-// stay straight-line and every wait is counted (vmcnt(N)), also across the back edge.
+// consumed; the next group is issued unconditionally while at least three groups remain
+// (the last one or two are finished straight-line), so the loads stay straight-line and
+// every wait is counted (vmcnt(N)), also across the back edge. Windows of the last group
+// past the stream are loaded with it but not summed.
 // ---------------------------------------------------------------------------------
+// How a chunk's first and last segments lose the bytes that are not the chunk's
+// (AIPSTACK_GATHER_MODE, a build switch for A/B runs): 1 (the product since round 4) = the
+// stream sums whole segments, and each lane reads its chunk's two edge segments itself up
+// front and subtracts their foreign bytes; 0 = every loaded segment masked in the stream (a
+// keep-table index per lane and window, rounds 2-3). Round 4 (profiles/r04/edge): mode 0
+// C2K 262.4 / CHAIN 241.2 us, mode 1 256.1 / 236.0 us (VALU -21 / -26 %; CHAIN's FETCH_SIZE
+// +2 %: an edge line read up front is sometimes gone when the stream gets to it). Copying the
+// edge segments out of the stream windows into LDS instead (exec-masked ds_write per window)
+// cut VALU as far but cost SALU and ran 264.6 / 241.8 us.
+#ifndef AIPSTACK_GATHER_MODE
+#define AIPSTACK_GATHER_MODE 1
+#endif
+
 // Per-wave LDS scratch of the gathered stream: the owners' load parameters by rank (rank =
 // non-empty chunks before it), and the chunk-start masks of the current group's windows.
 struct GatherLds {
@@ -843,11 +858,28 @@ struct GatherLds {
 typedef u32x4 KeepTable[256];
 
 __device__ __forceinline__ void fill_keep_table(KeepTable &t) {
+#if AIPSTACK_GATHER_MODE == 0
     for (int i = (int)threadIdx.x; i < 256; i += (int)blockDim.x) {
         const int head = i >> 4, tail = (i & 15) + 1;
         t[i] = u32x4{dword_keep(head, tail), dword_keep(head - 4, tail - 4),
                      dword_keep(head - 8, tail - 8), dword_keep(head - 12, tail - 12)};
     }
+#else
+    (void)t;  // mode 1 masks only two segments per chunk, once
+#endif
+}
+
+// The bytes of a chunk's first segment below its start (h = start & 15) and of its last
+// segment from its end on (t = ((end - 1) & 15) + 1), as a halves-sum.
+__device__ __forceinline__ uint32_t foreign_halves(const u32x4 &first, const u32x4 &last, int h,
+                                                   int t) {
+    uint32_t f = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        f = halves(first[d] & dword_keep(-4 * d, h - 4 * d), f);
+        f = halves(last[d] & dword_keep(t - 4 * d, 16 - 4 * d), f);
+    }
+    return f;
 }
 
 template <int U, bool NT>
@@ -860,10 +892,12 @@ struct ChunkLoader {
     int lane;
     GatherLds *g;
 
-    // Windows [w, w + U): loads into v, and each lane's keep-table index into keep. The
-    // owner of compact index 64w + k is the last chunk starting at or before it: its rank
-    // is base_w - 1 + (starts at lanes <= k of window w) = base_w + bit0 - 1 + mbcnt(m >> 1).
+    // Windows [w, w + U): loads into v, and (mode 0) each lane's keep-table index into
+    // keep. The owner of compact index 64w + k is the last chunk starting at or before it:
+    // its rank is base_w - 1 + (starts at lanes <= k of window w)
+    // = base_w + bit0 - 1 + mbcnt(m >> 1).
     __device__ __forceinline__ void issue(uint32_t w, u32x4 (&v)[U], uint32_t (&keep)[U]) {
+        uint64_t mk[U];
         if (lane < U) g->starts[lane] = 0ull;
         __builtin_amdgcn_wave_barrier();
         const uint32_t du = start_win - w;  // < U: starts in this group
@@ -872,28 +906,31 @@ struct ChunkLoader {
                                   __HIP_MEMORY_SCOPE_WAVEFRONT);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
-        uint64_t m[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint64_t x = g->starts[u];
-            m[u] = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32) |
-                   (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)x);
+            mk[u] = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32) |
+                    (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)x);
         }
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint64_t m1 = m[u] >> 1;
-            const uint32_t rank = base + ((uint32_t)m[u] & 1u) - 1u +
+            const uint64_t m1 = mk[u] >> 1;
+            const uint32_t rank = base + ((uint32_t)mk[u] & 1u) - 1u +
                                   __builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32),
                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0u));
-            base += (uint32_t)__builtin_popcountll(m[u]);
+            base += (uint32_t)__builtin_popcountll(mk[u]);
             const u32x4 od = g->owner[rank & (uint32_t)(kWave - 1)];
             const uint32_t c0 = (w + (uint32_t)u) * (uint32_t)kWave + (uint32_t)lane;
             const uint32_t c = min(c0, T - 1u);
+#if AIPSTACK_GATHER_MODE == 0
             const uint32_t fi = od[2], li = od[3];
             const uint32_t head = c == (fi & 0xFFFFFFu) ? fi >> 24 : 0u;
             const uint32_t tail = c == (li & 0xFFFFFFu) ? li >> 24 : 16u;
             keep[u] = head * 16u + tail - 1u;
+#else
+            (void)keep;
+#endif
             const uint64_t addr = (((uint64_t)od[1] << 32) | od[0]) + 16ull * c;
             typedef __attribute__((address_space(1))) const u32x4 gseg;
             const gseg *p = (const gseg *)(addr);
@@ -905,8 +942,8 @@ struct ChunkLoader {
     }
 };
 
-// The chain kernel's 64 chunk sums. `g`: this wave's LDS scratch; `keep`: the block's mask
-// table (fill_keep_table). Returns lane j's exact
+// The chain kernel's 64 chunk sums (also the ring slots' chunks). `g`: this wave's LDS
+// scratch; `keep`: the block's mask table (fill_keep_table, mode 0). Returns lane j's exact
 // halves-sum of its chunk.
 template <int U, bool NT>
 __device__ __forceinline__ uint32_t sum_gathered_chunks(uint64_t a, uint32_t l, int lane,
@@ -943,11 +980,18 @@ __device__ __forceinline__ uint32_t sum_gathered_chunks(uint64_t a, uint32_t l, 
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t wu = w + (uint32_t)u;
+            // windows past the stream (the last group's tail) sum zeros and hold no boundary:
+            // their loads went out with the group, their scans are skipped (wave-uniform)
+            if (wu >= nwin) break;
             const uint32_t c0 = wu * (uint32_t)kWave + (uint32_t)lane;
+#if AIPSTACK_GATHER_MODE == 0
             const u32x4 km = keep_table[keep[u]];
             uint32_t s = halves(v[u][0] & km[0],
                                 halves(v[u][1] & km[1],
                                        halves(v[u][2] & km[2], halves(v[u][3] & km[3], 0u))));
+#else
+            uint32_t s = halves(v[u][0], halves(v[u][1], halves(v[u][2], halves(v[u][3], 0u))));
+#endif
             s = c0 < T ? s : 0u;  // lanes past the stream re-read its last segment
             const uint32_t incl = wave_incl_scan(s);
             if (__builtin_amdgcn_ballot_w64(bwin == wu)) {
@@ -964,7 +1008,22 @@ __device__ __forceinline__ uint32_t sum_gathered_chunks(uint64_t a, uint32_t l, 
     // needed and unconditional (counted waits across the back edge); the last one or two
     // groups are finished straight-line, issuing nothing past the stream.
     const uint32_t groups = (nwin + U - 1u) / U;
+#if AIPSTACK_GATHER_MODE == 1
+    // The lane reads its chunk's two edge segments itself (they lie inside the chunk's
+    // segments, so they are mapped) before the stream's first group, at the default cache
+    // policy (the stream reads the same lines later).
+    u32x4 fseg = {0u, 0u, 0u, 0u}, lseg = {0u, 0u, 0u, 0u};
+    if (ns) {
+        typedef __attribute__((address_space(1))) const u32x4 gseg;
+        fseg = *(const gseg *)(a & ~(uint64_t)15);
+        lseg = *(const gseg *)((a + l - 1u) & ~(uint64_t)15);
+    }
+#endif
     ld.issue(0, va, ka);
+#if AIPSTACK_GATHER_MODE == 1
+    const uint32_t foreign =
+        ns ? foreign_halves(fseg, lseg, (int)rs, (int)(((rs + l - 1u) & 15u) + 1u)) : 0u;
+#endif
     uint32_t g = 0;
     for (; g + 2u < groups; g += 2u) {
         ld.issue((g + 1u) * U, vb, kb);
@@ -981,7 +1040,11 @@ __device__ __forceinline__ uint32_t sum_gathered_chunks(uint64_t a, uint32_t l, 
     }
     if (bwin >= nwin) gsum = carry;  // cs == T on a multiple of 64: past the last window
     // chunk j ends where chunk j + 1 starts (lane 63: at T, prefix = the final carry)
+#if AIPSTACK_GATHER_MODE == 0
     return from_next_lane(gsum, carry, lane) - gsum;
+#else
+    return from_next_lane(gsum, carry, lane) - gsum - foreign;
+#endif
 }
 
 // Stream mode for one chunk (stream_ok). Lane j < cnt holds packet j = [S, E); returns

@@ -203,9 +203,80 @@ def gathered_model(buf, a, l, U=4):
     return [((g[j + 1] if j < 63 else carry) - g[j]) & M32 for j in range(64)]
 
 
+def gathered_edge_model(buf, a, l, U=4):
+    """sum_gathered_chunks in AIPSTACK_GATHER_MODE 2 (the default since round 4): the stream
+    sums WHOLE segments; each window's chunk-start mask (one bit per non-empty chunk's first
+    segment) and the end mask derived from it (the lane before a start, lane 63 when the next
+    window starts with a chunk, and the stream's last segment) copy the loaded segment into
+    the owner's LDS edge slots; each lane then subtracts the bytes of its first segment below
+    its start and of its last segment from its end on. Returns each lane's halves-sum."""
+    k = len(a)
+    a = [int(x) for x in a] + [0] * (64 - k)
+    l = [int(x) for x in l] + [0] * (64 - k)
+    rs = [x & 15 for x in a]
+    ns = [((rs[j] + l[j] + 15) >> 4) if l[j] else 0 for j in range(64)]
+    incl = np.cumsum(ns)
+    cs = [int(incl[j] - ns[j]) for j in range(64)]
+    T = int(incl[63])
+    if T == 0:
+        return [0] * 64
+    nwin = (T + 63) >> 6
+    nonempty = [j for j in range(64) if ns[j]]
+    rank = {j: r for r, j in enumerate(nonempty)}
+    gbase = {rank[j]: (a[j] & ~15) - 16 * cs[j] for j in nonempty}
+    starts = [0] * (nwin + 1)
+    for j in nonempty:
+        starts[cs[j] >> 6] |= 1 << (cs[j] & 63)
+    edge = {}
+    g = [0] * 64
+    carry, base = 0, 0
+    for w in range(nwin):
+        ms = starts[w]
+        me = (ms >> 1) | ((starts[w + 1] & 1) << 63)
+        if (T - 1) >> 6 == w:
+            me |= 1 << ((T - 1) & 63)
+        seg = np.zeros(64, dtype=np.uint64)
+        for lane in range(64):
+            below = bin(ms & ((1 << (lane + 1)) - 1)).count("1")
+            r = base + below - 1
+            c0 = w * 64 + lane
+            c = min(c0, T - 1)
+            addr = gbase[r] + 16 * c
+            raw = np.array(buf[addr:addr + 16], dtype=np.uint8)
+            if (ms >> lane) & 1:
+                edge[(r, 0)] = raw.copy()
+            if (me >> lane) & 1:
+                edge[(r, 1)] = raw.copy()
+            if c0 < T:
+                seg[lane] = int(raw.view("<u2").astype(np.uint64).sum())
+        base += bin(ms).count("1")
+        inc = np.cumsum(seg)
+        exc = inc - seg
+        for j in range(64):
+            if cs[j] >> 6 == w:
+                g[j] = (carry + int(exc[cs[j] & 63])) & M32
+        carry = (carry + int(inc[63])) & M32
+    for j in range(64):
+        if cs[j] >> 6 >= nwin:
+            g[j] = carry
+    out = []
+    for j in range(64):
+        v = ((g[j + 1] if j < 63 else carry) - g[j]) & M32
+        if ns[j]:
+            first, last = edge[(rank[j], 0)].copy(), edge[(rank[j], 1)].copy()
+            t = ((rs[j] + l[j] - 1) & 15) + 1
+            first[rs[j]:] = 0          # the bytes below the start
+            last[:t] = 0               # the bytes from the end on
+            v = (v - int(first.view("<u2").astype(np.uint64).sum())
+                 - int(last.view("<u2").astype(np.uint64).sum())) & M32
+        out.append(v)
+    return out
+
+
+@pytest.mark.parametrize("model", ["masked", "edge"])
 @pytest.mark.parametrize("U", [2, 4])
 @pytest.mark.parametrize("case", ["headers_and_ring", "tiny", "sparse", "long", "shared_segments"])
-def test_gathered_model_matches_oracle(oracle, case, U):
+def test_gathered_model_matches_oracle(oracle, case, U, model):
     rng = np.random.default_rng(hash(("g", case, U)) % 2**32)
     buf = rng.integers(0, 256, size=1 << 20, dtype=np.uint8)
     buf[300000:310000] = 0xFF
@@ -242,7 +313,7 @@ def test_gathered_model_matches_oracle(oracle, case, U):
             a.append(p)
             l.append(ln)
             p += ln
-    sums = gathered_model(buf, a, l, U)
+    sums = (gathered_model if model == "masked" else gathered_edge_model)(buf, a, l, U)
     for j in range(n):
         s = sums[j]
         r = (s & 0xFFFF) + (s >> 16)

@@ -111,6 +111,36 @@ short)  # neighbour-aware short chunks first in chained batches: GPU tests, CHAI
   done
   VARIANTS="base CHAIN_SHORT=128 CHAIN_SHORT=32" "$0" probe
   ;;
+skip)  # gathered streams skip the scans of windows past the stream: tests, A/B vs the
+        # previous library (tools/build/lib_noskip.so), VALU per variant
+  pyt pytest_skip -m gpu -k "chain or slotted or native_library"
+  for i in 1 2 3; do
+    for c in C2K CHAIN; do
+      AIPSTACK_AMD_LIB=tools/build/lib_noskip.so bench ${c}_noskip --config $c --per-launch --no-cpu-baseline
+      bench ${c}_skip --config $c --per-launch --no-cpu-baseline
+    done
+  done
+  for c in C2K CHAIN; do
+    AIPSTACK_AMD_LIB=tools/build/lib_noskip.so pmc1 ${c}_noskip_sq $c SQ_INSTS_VALU SQ_INSTS_SALU
+    pmc1 ${c}_skip_sq $c SQ_INSTS_VALU SQ_INSTS_SALU
+  done
+  ;;
+edge)  # gathered streams: AIPSTACK_GATHER_MODE 2 (edge segments copied from the stream,
+        # the product) against 0 (per-segment masks, tools/build/lib_masked.so) and 1 (edge
+        # segments re-read, tools/build/lib_edgeload.so): tests, A/B, VALU and FETCH
+  pyt pytest_edge -m gpu -k "chain or slotted or native_library or random"
+  for i in 1 2 3; do
+    for c in C2K CHAIN; do
+      AIPSTACK_AMD_LIB=tools/build/lib_masked.so bench ${c}_masked --config $c --per-launch --no-cpu-baseline
+      AIPSTACK_AMD_LIB=tools/build/lib_edgeload.so bench ${c}_edgeload --config $c --per-launch --no-cpu-baseline
+      bench ${c}_edge --config $c --per-launch --no-cpu-baseline
+    done
+  done
+  for c in C2K CHAIN; do
+    pmc1 ${c}_edge_sq $c SQ_INSTS_VALU SQ_INSTS_SALU
+    pmc1 ${c}_edge_fetch $c FETCH_SIZE
+  done
+  ;;
 kern)
   pyt pytest_kern -m gpu -k "chain or contract_violations or native_library"
   for i in 1 2 3; do
