@@ -1012,17 +1012,18 @@ __device__ __forceinline__ uint32_t sum_gathered_chunks(uint64_t a, uint32_t l, 
     // The lane reads its chunk's two edge segments itself (they lie inside the chunk's
     // segments, so they are mapped) before the stream's first group, at the default cache
     // policy (the stream reads the same lines later).
+    // (none where the chunk starts or ends on a segment boundary: nothing foreign there)
     u32x4 fseg = {0u, 0u, 0u, 0u}, lseg = {0u, 0u, 0u, 0u};
-    if (ns) {
+    const uint32_t te = ((rs + l - 1u) & 15u) + 1u;  // the chunk's end in its last segment
+    {
         typedef __attribute__((address_space(1))) const u32x4 gseg;
-        fseg = *(const gseg *)(a & ~(uint64_t)15);
-        lseg = *(const gseg *)((a + l - 1u) & ~(uint64_t)15);
+        if (ns && rs != 0u) fseg = *(const gseg *)(a & ~(uint64_t)15);
+        if (ns && te != 16u) lseg = *(const gseg *)((a + l - 1u) & ~(uint64_t)15);
     }
 #endif
     ld.issue(0, va, ka);
 #if AIPSTACK_GATHER_MODE == 1
-    const uint32_t foreign =
-        ns ? foreign_halves(fseg, lseg, (int)rs, (int)(((rs + l - 1u) & 15u) + 1u)) : 0u;
+    const uint32_t foreign = ns ? foreign_halves(fseg, lseg, (int)rs, (int)te) : 0u;
 #endif
     uint32_t g = 0;
     for (; g + 2u < groups; g += 2u) {

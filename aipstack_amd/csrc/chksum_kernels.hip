@@ -521,12 +521,14 @@ int launch(const Desc &desc, uint64_t n, uint32_t max_len, uint16_t *d_out, uint
     if (cus <= 0) return AIPSTACK_CHKSUM_EHIP;
     Shape sh = pick_shape(n, cus);
     if constexpr (!Desc::kStream) {
-        // Ring slots: the gathered stream, 4 windows per group, 16-packet chunks, one chunk
+        // Ring slots: the gathered stream, 4 windows per group, 8-packet chunks, one chunk
         // per wave ("stream" tunable: 2 = 2 windows, -1 = the per-packet wave mode). C2K
         // (profiles/r03/ssweep): 263 us against 278 with 64-packet chunks and runs of chunks
-        // per wave, and 265 for the wave mode in the same shape.
+        // per wave, and 265 for the wave mode in the same shape; round 4, once the stream
+        // summed whole segments (fewer VGPRs): 8-packet chunks 244.2 us, 16 248.8, 4 291.9
+        // (A2K 224.2 / 225.8 / 221.9; profiles/r04/shape2).
         if (!sh.small && tuning().chunk_packets.load(std::memory_order_relaxed) == 0)
-            sh.chunk_packets = 16;
+            sh.chunk_packets = 8;
         const int su = tuning_stream_windows(4);
         if (su == 4) return launch_k<Desc, 1, 1, true, SEEDED, 4>(desc, n, sh, d_out, flags, stream);
         if (su != 0) return launch_k<Desc, 1, 1, true, SEEDED, 2>(desc, n, sh, d_out, flags, stream);
@@ -546,7 +548,10 @@ int launch_chain(const uint64_t *d_addr, const uint32_t *d_len, const uint64_t *
                  uint16_t *d_out, uint32_t flags, hipStream_t stream) {
     const int cus = device_cu_count(stream);
     if (cus <= 0) return AIPSTACK_CHKSUM_EHIP;
-    const uint32_t cpg = pick_shape(n, cus).chunk_packets;  // chains per group
+    // chains per group: 32 for large batches (CHAIN 230.8 us against 233.2 at 64 and 231.9 at
+    // 16, profiles/r04/shape2), fewer for small ones, or the chunk_packets tunable
+    uint32_t cpg = pick_shape(n, cus).chunk_packets;
+    if (cpg > 32u && tuning().chunk_packets.load(std::memory_order_relaxed) == 0) cpg = 32u;
     const uint64_t nchunks = (n + cpg - 1) / cpg;
     const uint64_t target_waves = (uint64_t)cus * 2 * kDefaultWavesPerCu;
     uint64_t cpw = (nchunks + target_waves - 1) / target_waves;

@@ -461,8 +461,8 @@ int aipstack_chksum_device_check(int device);
  * issues together in stream mode -- a 64-packet or 64-frame chunk that lies back to back
  * in memory, or chain chunks that lie close together: 2, 4, 8; -1 turns stream mode off,
  * so every packet, frame or chunk is summed on its own), "chunk_packets" (packets, frames
- * or chains per wave chunk: 1, 2, 4, ..., 64; automatic = 64, fewer for small batches so
- * that they spread over more waves), "tx_gather" (where the Tx fills take their header
+ * or chains per wave chunk: 1, 2, 4, ..., 64; automatic = 64 (ring slots 8, chains 32),
+ * fewer for small batches so that they spread over more waves), "tx_gather" (where the Tx fills take their header
  * segments: 0 per-lane loads, 1 captured from the stream, 2 captured + the two field lines
  * touched up front; -1 = by kind of launch), "tx_store" (how the in-place Tx fills write the
  * two checksum fields: 0 = 2-byte stores, 1 = the fields' whole 32-byte sectors from the header

@@ -141,6 +141,35 @@ edge)  # gathered streams: AIPSTACK_GATHER_MODE 2 (edge segments copied from the
     pmc1 ${c}_edge_fetch $c FETCH_SIZE
   done
   ;;
+shape)  # launch shapes again after the edge form (fewer VGPRs): full GPU suite, C2K shapes,
+         # CHAIN at 2 / 4 windows
+  pyt pytest_all -m gpu
+  timeout -k 10 300 python tools/slot_sweep.py --config C2K --rounds 6 --variants \
+      "chunk_packets=16;stream=8,chunk_packets=16;stream=2,chunk_packets=16;chunk_packets=32;stream=8,chunk_packets=32;chunk_packets=8;stream=8,chunk_packets=8" \
+      > "$out/c2k_sweep.jsonl" 2> "$out/c2k_sweep.err"
+  for i in 1 2 3; do
+    bench chain_su4 --config CHAIN --per-launch --no-cpu-baseline
+    AIPSTACK_CHKSUM_STREAM=2 bench chain_su2 --config CHAIN --per-launch --no-cpu-baseline
+    # edge loads only where a chunk has foreign bytes (product) vs always (lib_edgeall.so)
+    AIPSTACK_AMD_LIB=tools/build/lib_edgeall.so bench chain_edgeall --config CHAIN --per-launch --no-cpu-baseline
+    AIPSTACK_AMD_LIB=tools/build/lib_edgeall.so bench c2k_edgeall --config C2K --per-launch --no-cpu-baseline
+    bench c2k --config C2K --per-launch --no-cpu-baseline
+  done
+  pmc1 chain_fetch CHAIN FETCH_SIZE
+  ;;
+shape2)  # slot chunk sizes for C2K and A2K after the conditional edge loads; CHAIN chains per group
+  timeout -k 10 300 python tools/slot_sweep.py --config C2K --rounds 6 --variants \
+      "chunk_packets=8;chunk_packets=4;stream=2,chunk_packets=8;chunk_packets=16;stream=2,chunk_packets=4;stream=8,chunk_packets=4" \
+      > "$out/c2k_sweep.jsonl" 2> "$out/c2k_sweep.err"
+  timeout -k 10 300 python tools/slot_sweep.py --config A2K --rounds 6 --variants \
+      "chunk_packets=16;chunk_packets=8;chunk_packets=4;stream=2,chunk_packets=8;stream=8,chunk_packets=8" \
+      > "$out/a2k_sweep.jsonl" 2> "$out/a2k_sweep.err"
+  for i in 1 2 3; do
+    bench chain_g64 --config CHAIN --per-launch --no-cpu-baseline
+    AIPSTACK_CHKSUM_CHUNK_PACKETS=32 bench chain_g32 --config CHAIN --per-launch --no-cpu-baseline
+    AIPSTACK_CHKSUM_CHUNK_PACKETS=16 bench chain_g16 --config CHAIN --per-launch --no-cpu-baseline
+  done
+  ;;
 kern)
   pyt pytest_kern -m gpu -k "chain or contract_violations or native_library"
   for i in 1 2 3; do

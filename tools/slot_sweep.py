@@ -27,7 +27,7 @@ KEYS = ("waves_per_cu", "chunks_per_wave", "unroll", "packets", "frames", "strea
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", default="C2K", choices=["C2K", "RX2K"])
+    ap.add_argument("--config", default="C2K", choices=["C2K", "A2K", "RX2K"])
     ap.add_argument("--variants", required=True)
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--reps", type=int, default=10)
@@ -42,6 +42,10 @@ def main():
     dev = torch.device("cuda", 0)
     if args.config == "C2K":
         buf, off = synth.mixed_batch(2 << 20)
+    elif args.config == "A2K":  # 1 M x 1500 B in 2048-B slots (bench.py A2K's shape)
+        n0 = 1 << 20
+        buf = synth.random_bytes(42, n0 * 1500)
+        off = np.arange(n0 + 1, dtype=np.int64) * 1500
     else:  # RX's frames, made valid by the frame oracle (as bench.py does; test infra)
         import ctypes
         buf, off = synth.frames_host(1 << 20, seed=synth.SEED_DATA, max_payload=1460)
@@ -56,12 +60,12 @@ def main():
     d_lens = torch.from_numpy(lens.view(np.int32)).to(dev)
     del buf, ring
     n = lens.size
-    out = (torch.empty(n, dtype=torch.uint16, device=dev) if args.config == "C2K"
+    out = (torch.empty(n, dtype=torch.uint16, device=dev) if args.config != "RX2K"
            else torch.empty(n, dtype=torch.uint8, device=dev))
     stream = torch.cuda.current_stream()
 
     def launch():
-        if args.config == "C2K":
+        if args.config != "RX2K":
             A.chksum_batch_slotted(d_ring, 2048, d_lens, out=out, stream=stream)
         else:
             A.rx_verify_slotted(d_ring, 2048, d_lens, out=out, stream=stream)
