@@ -115,6 +115,41 @@ struct StridedDesc {
     bool back_to_back() const { return stride == len && len < (1u << 17); }
 };
 
+// Fixed-length packets at a stride other than their length (gaps between them, as
+// `aipstack_chksum_batch_strided` with stride != len: 1500-B packets in 2048-B slots): not one
+// contiguous run, so they take the gathered stream of just their segments (round 4: config
+// A2K 241.6 us in the per-packet wave mode, ~224 us gathered) -- a ring of slots with one
+// length for all.
+struct GappedDesc {
+    static constexpr bool kCsr = false;
+    static constexpr bool kStream = false;
+    uint64_t base;    // absolute address of packet 0
+    uint64_t stride;  // bytes between packet starts
+    uint32_t len;     // bytes per packet
+
+    struct Chunk {
+        uint64_t s0;  // start of the chunk's first packet
+    };
+    __device__ __forceinline__ Chunk begin_chunk(uint64_t p0, uint64_t, int) const {
+        return Chunk{base + p0 * stride};
+    }
+    __device__ __forceinline__ void bounds(const Chunk &c, int j, uint64_t &S,
+                                           uint64_t &E) const {
+        S = c.s0 + (uint64_t)j * stride;
+        E = S + len;
+    }
+    __device__ __forceinline__ void lane_bounds(const Chunk &c, int lane, uint64_t &S,
+                                                uint64_t &E) const {
+        S = c.s0 + (uint64_t)lane * stride;
+        E = S + len;
+    }
+    __device__ __forceinline__ uint32_t lane_seed(const Chunk &) const { return 0; }
+    bool back_to_back() const { return false; }
+    __device__ __forceinline__ uint64_t chunk_end(const Chunk &c, int cnt) const {
+        return c.s0 + (uint64_t)cnt * stride;
+    }
+};
+
 struct CsrDesc {
     static constexpr bool kCsr = true;
     static constexpr bool kStream = true;

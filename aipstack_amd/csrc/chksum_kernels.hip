@@ -631,6 +631,10 @@ extern "C" int aipstack_chksum_batch_strided(const void *d_base, uint64_t stride
     if (n == 0) return AIPSTACK_CHKSUM_OK;
     if (!d_base || !d_out || len > AIPSTACK_CHKSUM_MAX_LEN) return AIPSTACK_CHKSUM_EINVAL;
     if (n > (1ull << 40)) return AIPSTACK_CHKSUM_EINVAL;
+    if (stride != len) {  // gaps between the packets (or overlap): the gathered stream
+        GappedDesc d{(uint64_t)(uintptr_t)d_base, stride, len};
+        return launch<GappedDesc, false>(d, n, len, d_out, flags, (hipStream_t)stream);
+    }
     StridedDesc d{(uint64_t)(uintptr_t)d_base, stride, len};
     return launch<StridedDesc, false>(d, n, len, d_out, flags, (hipStream_t)stream);
 }

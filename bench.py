@@ -57,8 +57,8 @@ SLOT_STRIDE = {"A2K": 2048, "RX2K": 2048, "TX2K": 2048, "C2K": 2048}  # layouts 
 WORKLOAD_NAMES = {
     "A": "1M x 1500B Ethernet-MTU packets per GPU, IP checksum (BASELINE configs[1]; x8 = configs[4])",
     "B": "256K x 9000B jumbo packets per GPU, IP checksum (BASELINE configs[2])",
-    "A2K": "1M x 1500B packets per GPU in 2048B ring slots (stride != length: one packet per "
-           "wavefront), IP checksum",
+    "A2K": "1M x 1500B packets per GPU in 2048B ring slots (stride != length: the packets' "
+           "segments read as one gathered stream), IP checksum",
     "C": "2M mixed 64-1500B packets per GPU incl. odd lengths/starts, CSR (BASELINE configs[3])",
     "RX": "1M raw Ethernet frames per GPU (TCP/UDP/ICMP/other/ARP/fragments, 0-1460B payload), "
           "Rx verify: IPv4 header + L4 checksum verdicts",
