@@ -240,6 +240,14 @@ struct SlottedDesc {
     }
 };
 
+// CSR packets read by the gathered stream (round 4, the default for the CSR checksum batch):
+// the same descriptor without stream mode. A chunk holding a packet over 65535 bytes (outside
+// the contract; its halves-sum could pass 2^32) takes the per-packet wave mode instead.
+struct GatheredCsrDesc : CsrDesc {
+    static constexpr bool kStream = false;
+    bool back_to_back() const { return false; }
+};
+
 struct SeededCsrDesc : CsrDesc {
     const uint32_t *states;  // n accumulator states (IpChksumAccumulator::State)
 

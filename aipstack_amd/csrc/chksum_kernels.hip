@@ -87,8 +87,10 @@ __global__ __launch_bounds__(kBlock) void chksum_batch_kernel(Desc desc, uint64_
 
     for (; c < c_end; ++c) {
         const uint64_t p0 = c * cpk;
-        const auto chunk = desc.begin_chunk(p0, n, lane);
         const int cnt = (int)min(cpk, n - p0);
+        // the chunk's own table entries only (offsets, lengths, states): lanes past it re-read
+        // entry p0 + cnt, so a wave of a short chunk fetches no other chunk's table lines
+        const auto chunk = desc.begin_chunk(p0, p0 + (uint64_t)cnt, lane);
         // every packet's load parameters at once: lane j <-> packet j (VALU, vectorised)
         uint64_t lS, lE;
         desc.lane_bounds(chunk, lane, lS, lE);
@@ -100,9 +102,12 @@ __global__ __launch_bounds__(kBlock) void chksum_batch_kernel(Desc desc, uint64_
         uint32_t sums = 0;
         bool streamed = false;
         if constexpr (kGathered) {
-            sums = sum_gathered_chunks<SU, NT>(lS, (uint32_t)(lE - lS), lane,
-                                               &gsh.g[wave_in_block], gsh.keep);
-            streamed = true;
+            // (CSR: every packet within the contract, else the wave mode below)
+            if (!Desc::kCsr || __builtin_amdgcn_ballot_w64(lE - lS > (uint64_t)AIPSTACK_CHKSUM_MAX_LEN) == 0) {
+                sums = sum_gathered_chunks<SU, NT>(lS, (uint32_t)(lE - lS), lane,
+                                                   &gsh.g[wave_in_block], gsh.keep);
+                streamed = true;
+            }
         } else if constexpr (SU > 0) {
             if (stream_ok(lS, lE, lane, cnt)) {
                 // back-to-back packets: the chunk read as one contiguous run
@@ -350,6 +355,8 @@ struct Tuning {
                                           // touched up front; else by kind of Tx launch
     std::atomic<int> tx_store{-1};        // in-place Tx fills: 0 = 2-byte field stores, 1 =
                                           // whole sectors; else the default
+    std::atomic<int> gather{0};           // -1: back-to-back strided and CSR batches in stream
+                                          // mode (rounds 1-3); else the gathered stream
     std::atomic<int> chain_short{-1};      // chains: chunks of at most this many bytes first in
                                           // the gathered stream (0 = table order; measured:
                                           // CHAIN 250.0-250.6 us at 128 against 248.0-248.9,
@@ -376,6 +383,7 @@ struct Tuning {
         env("AIPSTACK_CHKSUM_TX_GATHER", tx_gather);
         env("AIPSTACK_CHKSUM_TX_STORE", tx_store);
         env("AIPSTACK_CHKSUM_CHAIN_SHORT", chain_short);
+        env("AIPSTACK_CHKSUM_GATHER", gather);
         env("AIPSTACK_ENGINE_ZERO_COPY", engine_zero_copy);
         env("AIPSTACK_ENGINE_ZERO_COPY_SMALL", engine_zero_copy_small);
         env("AIPSTACK_ENGINE_PAGEABLE_ROWS", engine_pageable_rows);
@@ -631,7 +639,10 @@ extern "C" int aipstack_chksum_batch_strided(const void *d_base, uint64_t stride
     if (n == 0) return AIPSTACK_CHKSUM_OK;
     if (!d_base || !d_out || len > AIPSTACK_CHKSUM_MAX_LEN) return AIPSTACK_CHKSUM_EINVAL;
     if (n > (1ull << 40)) return AIPSTACK_CHKSUM_EINVAL;
-    if (stride != len) {  // gaps between the packets (or overlap): the gathered stream
+    // The gathered stream (round 4), also for packets back to back: config A 217.2 us against
+    // 232.5 in stream mode, B 336.2 / 337.7 (profiles/r04/gatherA); tunable "gather" = -1
+    // keeps stream mode for stride == len.
+    if (stride != len || tuning().gather.load(std::memory_order_relaxed) != -1) {
         GappedDesc d{(uint64_t)(uintptr_t)d_base, stride, len};
         return launch<GappedDesc, false>(d, n, len, d_out, flags, (hipStream_t)stream);
     }
@@ -663,8 +674,15 @@ extern "C" int aipstack_chksum_batch_csr(const void *d_base, const uint64_t *d_o
     if (n == 0) return AIPSTACK_CHKSUM_OK;
     if (!d_base || !d_offsets || !d_out) return AIPSTACK_CHKSUM_EINVAL;
     if (n > (1ull << 40)) return AIPSTACK_CHKSUM_EINVAL;
+    // Typical network packets (<= ~2 KiB) fit one group at U = 2 in the wave mode; longer
+    // ones loop. The gathered stream unless tunable "gather" = -1 (stream mode).
+    if (tuning().gather.load(std::memory_order_relaxed) != -1) {
+        GatheredCsrDesc d;
+        d.base = (uint64_t)(uintptr_t)d_base;
+        d.offsets = d_offsets;
+        return launch<GatheredCsrDesc, false>(d, n, 1500u, d_out, flags, (hipStream_t)stream);
+    }
     CsrDesc d{(uint64_t)(uintptr_t)d_base, d_offsets};
-    // Typical network packets (<= ~2 KiB) fit one group at U = 2; longer ones loop.
     return launch<CsrDesc, false>(d, n, 1500u, d_out, flags, (hipStream_t)stream);
 }
 
@@ -696,6 +714,7 @@ extern "C" int aipstack_chksum_tune(const char *key, int value) {
     else if (!std::strcmp(key, "tx_gather")) t.tx_gather = value;
     else if (!std::strcmp(key, "tx_store")) t.tx_store = value;
     else if (!std::strcmp(key, "chain_short")) t.chain_short = value;
+    else if (!std::strcmp(key, "gather")) t.gather = value;
     else if (!std::strcmp(key, "engine_zero_copy")) t.engine_zero_copy = value;
     else if (!std::strcmp(key, "engine_zero_copy_small")) t.engine_zero_copy_small = value;
     else if (!std::strcmp(key, "engine_pageable_rows")) t.engine_pageable_rows = value;

@@ -170,6 +170,33 @@ shape2)  # slot chunk sizes for C2K and A2K after the conditional edge loads; CH
     AIPSTACK_CHKSUM_CHUNK_PACKETS=16 bench chain_g16 --config CHAIN --per-launch --no-cpu-baseline
   done
   ;;
+gatherA)  # back-to-back strided batches (A, B) through the gathered stream, chunk sizes
+  for i in 1 2 3; do
+    bench A_stream --config A --per-launch --no-cpu-baseline
+    AIPSTACK_CHKSUM_GATHER=1 bench A_g8 --config A --per-launch --no-cpu-baseline
+    AIPSTACK_CHKSUM_GATHER=1 AIPSTACK_CHKSUM_CHUNK_PACKETS=16 bench A_g16 --config A --per-launch --no-cpu-baseline
+    AIPSTACK_CHKSUM_GATHER=1 AIPSTACK_CHKSUM_CHUNK_PACKETS=4 bench A_g4 --config A --per-launch --no-cpu-baseline
+    bench B_stream --config B --per-launch --no-cpu-baseline
+    AIPSTACK_CHKSUM_GATHER=1 bench B_g8 --config B --per-launch --no-cpu-baseline
+    AIPSTACK_CHKSUM_GATHER=1 AIPSTACK_CHKSUM_CHUNK_PACKETS=2 bench B_g2 --config B --per-launch --no-cpu-baseline
+  done
+  ;;
+gather2)  # the gathered stream as the default for strided and CSR checksum batches: the GPU
+          # suite, then A / B / C against stream mode (gather = -1), small batches
+  pyt pytest_all -m gpu
+  for i in 1 2 3; do
+    for c in A B C; do
+      AIPSTACK_CHKSUM_GATHER=-1 bench ${c}_stream --config $c --per-launch --no-cpu-baseline
+      bench ${c}_gather --config $c --per-launch --no-cpu-baseline
+    done
+  done
+  for n in 1024 4096 16384; do
+    AIPSTACK_CHKSUM_GATHER=-1 timeout -k 10 120 python bench.py --config A --small $n >> "$out/small_stream.jsonl" 2>> "$out/small.err"
+    timeout -k 10 120 python bench.py --config A --small $n >> "$out/small_gather.jsonl" 2>> "$out/small.err"
+  done
+  pmc1 A_fetch A FETCH_SIZE
+  pmc1 C_fetch C FETCH_SIZE
+  ;;
 kern)
   pyt pytest_kern -m gpu -k "chain or contract_violations or native_library"
   for i in 1 2 3; do
