@@ -535,8 +535,10 @@ int launch(const Desc &desc, uint64_t n, uint32_t max_len, uint16_t *d_out, uint
         // per wave, and 265 for the wave mode in the same shape; round 4, once the stream
         // summed whole segments (fewer VGPRs): 8-packet chunks 244.2 us, 16 248.8, 4 291.9
         // (A2K 224.2 / 225.8 / 221.9; profiles/r04/shape2).
+        // CSR packets in the gathered stream (config C, 64-1500 B): 16-packet chunks 231.0 us,
+        // 8 242.3, 32 233.6 (profiles/r04/chunks) -- about 12 KiB per chunk, as A's 8 x 1500 B
         if (!sh.small && tuning().chunk_packets.load(std::memory_order_relaxed) == 0)
-            sh.chunk_packets = 8;
+            sh.chunk_packets = Desc::kCsr ? 16 : 8;
         const int su = tuning_stream_windows(4);
         if (su == 4) return launch_k<Desc, 1, 1, true, SEEDED, 4>(desc, n, sh, d_out, flags, stream);
         if (su != 0) return launch_k<Desc, 1, 1, true, SEEDED, 2>(desc, n, sh, d_out, flags, stream);

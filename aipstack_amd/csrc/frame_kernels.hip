@@ -822,8 +822,12 @@ int launch_frames_g(const Desc &desc, uint64_t n, uint8_t *d_status, uint64_t *d
     // Ring slots: 32-frame chunks, one per wave (RX2K, profiles/r03/ssweep: 130 us against
     // 136 with 64-frame chunks in runs per wave; 16-frame chunks 160; 1 segment per lane up
     // front instead of 2: 144, profiles/r03/fsweep)
-    const bool slots = !Desc::kStream && cpk == (uint32_t)kWave && tuning_chunk_packets() == 0;
-    if (slots) cpk = 32;
+    // Back-to-back frames too, since round 4: RX 120.6 us against 123.0 with 64-frame chunks,
+    // the split Tx fill 161.4 against 168.9 (16-frame chunks 141.6 / 179.3;
+    // profiles/r04/chunks).
+    const bool big = cpk == (uint32_t)kWave && tuning_chunk_packets() == 0;
+    const bool slots = !Desc::kStream && big;
+    if (big) cpk = 32;
     const uint64_t nchunks = (n + cpk - 1) / cpk;
     const int su = tuning_stream_windows(8);  // measured: 8 > 4 > off > 2 (RX and TX)
     const uint64_t target_waves =

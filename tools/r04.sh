@@ -197,6 +197,20 @@ gather2)  # the gathered stream as the default for strided and CSR checksum batc
   pmc1 A_fetch A FETCH_SIZE
   pmc1 C_fetch C FETCH_SIZE
   ;;
+chunks)  # chunk sizes: stream mode for A (what made the gathered form faster?), frames for RX / TX
+  for i in 1 2; do
+    for k in 64 32 16 8; do
+      AIPSTACK_CHKSUM_GATHER=-1 AIPSTACK_CHKSUM_CHUNK_PACKETS=$k bench A_stream_$k --config A --per-launch --no-cpu-baseline
+    done
+    for k in 64 32 16; do
+      AIPSTACK_CHKSUM_CHUNK_PACKETS=$k bench RX_$k --config RX --per-launch --no-cpu-baseline
+      AIPSTACK_CHKSUM_CHUNK_PACKETS=$k bench TX_$k --config TX --per-launch --no-cpu-baseline
+    done
+    for k in 16 8 32; do
+      AIPSTACK_CHKSUM_CHUNK_PACKETS=$k bench C_g$k --config C --per-launch --no-cpu-baseline
+    done
+  done
+  ;;
 kern)
   pyt pytest_kern -m gpu -k "chain or contract_violations or native_library"
   for i in 1 2 3; do
