@@ -123,6 +123,7 @@ struct StridedDesc {
 struct GappedDesc {
     static constexpr bool kCsr = false;
     static constexpr bool kStream = false;
+    static constexpr bool kEdge = true;  // gathered stream: edge segments read up front
     uint64_t base;    // absolute address of packet 0
     uint64_t stride;  // bytes between packet starts
     uint32_t len;     // bytes per packet
@@ -208,6 +209,7 @@ struct SlottedDesc {
     static constexpr bool kStream = false;  // slots are not back to back: no contiguous run,
                                             // but the gathered stream (SU > 0) reads just the
                                             // packets' segments as one stream
+    static constexpr bool kEdge = true;     // edge segments read up front (sum_gathered_chunks)
     uint64_t base;          // absolute address of slot 0
     uint64_t stride;        // slot size in bytes
     const uint32_t *lens;   // n packet lengths
@@ -245,7 +247,14 @@ struct SlottedDesc {
 // the contract; its halves-sum could pass 2^32) takes the per-packet wave mode instead.
 struct GatheredCsrDesc : CsrDesc {
     static constexpr bool kStream = false;
+    static constexpr bool kEdge = true;
     bool back_to_back() const { return false; }
+};
+
+// Ring slots the kernel reads over the link from page-locked host memory (the engine's
+// zero-copy pieces): edges masked in the stream, so no segment crosses the link twice.
+struct SlottedHostDesc : SlottedDesc {
+    static constexpr bool kEdge = false;
 };
 
 struct SeededCsrDesc : CsrDesc {
@@ -863,8 +872,8 @@ __device__ __forceinline__ int wave_max_scan(int v) {
 // ds_bpermute of the window's exclusive scan. Those segments also hold bytes that are not the
 // chunk's -- below a_j & 15 in its first segment, from its end on in its last -- and lane j
 // subtracts them: it reads its chunk's two edge segments itself before the stream starts
-// (round 4, AIPSTACK_GATHER_MODE 1; rounds 2-3 masked them off in the stream, every lane of
-// every window looking up a keep mask, mode 0). A segment shared by two chunks is loaded once
+// (round 4, EDGE; rounds 2-3 masked them off in the stream, every lane of every window
+// looking up a keep mask -- kept for bytes read over the link, !EDGE). A segment shared by two chunks is loaded once
 // for each (the second time from L2); bytes outside every chunk's segments are never read,
 // so chunks may sit in separate allocations (a 16-byte segment around a mapped byte is
 // mapped). Lanes past the stream re-read its last segment and count 0, so every address
@@ -876,18 +885,17 @@ __device__ __forceinline__ int wave_max_scan(int v) {
 // every wait is counted (vmcnt(N)), also across the back edge. Windows of the last group
 // past the stream are loaded with it but not summed.
 // ---------------------------------------------------------------------------------
-// How a chunk's first and last segments lose the bytes that are not the chunk's
-// (AIPSTACK_GATHER_MODE, a build switch for A/B runs): 1 (the product since round 4) = the
-// stream sums whole segments, and each lane reads its chunk's two edge segments itself up
-// front and subtracts their foreign bytes; 0 = every loaded segment masked in the stream (a
-// keep-table index per lane and window, rounds 2-3). Round 4 (profiles/r04/edge): mode 0
-// C2K 262.4 / CHAIN 241.2 us, mode 1 256.1 / 236.0 us (VALU -21 / -26 %; CHAIN's FETCH_SIZE
-// +2 %: an edge line read up front is sometimes gone when the stream gets to it). Copying the
-// edge segments out of the stream windows into LDS instead (exec-masked ds_write per window)
-// cut VALU as far but cost SALU and ran 264.6 / 241.8 us.
-#ifndef AIPSTACK_GATHER_MODE
-#define AIPSTACK_GATHER_MODE 1
-#endif
+// How a chunk's first and last segments lose the bytes that are not the chunk's (template
+// flag EDGE): true (round 4, the default) = the stream sums whole segments, and each lane
+// reads its chunk's two edge segments itself up front and subtracts their foreign bytes;
+// false = every loaded segment masked in the stream (a keep-table index per lane and window,
+// rounds 2-3), kept for bytes read over the link from host memory, where an edge segment
+// read twice crosses the link twice (the engine's zero-copy ring slots). Round 4
+// (profiles/r04/edge): masked C2K 262.4 / CHAIN 241.2 us, edge loads 256.1 / 236.0 us
+// (VALU -21 / -26 %; CHAIN's FETCH_SIZE +2 %: an edge line read up front is sometimes gone
+// when the stream gets to it). Copying the edge segments out of the stream windows into LDS
+// instead (exec-masked ds_write per window) cut VALU as far but cost SALU and ran
+// 264.6 / 241.8 us.
 
 // Per-wave LDS scratch of the gathered stream: the owners' load parameters by rank (rank =
 // non-empty chunks before it), and the chunk-start masks of the current group's windows.
@@ -901,15 +909,11 @@ struct GatherLds {
 typedef u32x4 KeepTable[256];
 
 __device__ __forceinline__ void fill_keep_table(KeepTable &t) {
-#if AIPSTACK_GATHER_MODE == 0
     for (int i = (int)threadIdx.x; i < 256; i += (int)blockDim.x) {
         const int head = i >> 4, tail = (i & 15) + 1;
         t[i] = u32x4{dword_keep(head, tail), dword_keep(head - 4, tail - 4),
                      dword_keep(head - 8, tail - 8), dword_keep(head - 12, tail - 12)};
     }
-#else
-    (void)t;  // mode 1 masks only two segments per chunk, once
-#endif
 }
 
 // The bytes of a chunk's first segment below its start (h = start & 15) and of its last
@@ -925,7 +929,7 @@ __device__ __forceinline__ uint32_t foreign_halves(const u32x4 &first, const u32
     return f;
 }
 
-template <int U, bool NT>
+template <int U, bool NT, bool EDGE>
 struct ChunkLoader {
     static_assert(U <= 8, "GatherLds holds 8 window masks");
     uint32_t T;
@@ -935,7 +939,7 @@ struct ChunkLoader {
     int lane;
     GatherLds *g;
 
-    // Windows [w, w + U): loads into v, and (mode 0) each lane's keep-table index into
+    // Windows [w, w + U): loads into v, and (!EDGE) each lane's keep-table index into
     // keep. The owner of compact index 64w + k is the last chunk starting at or before it:
     // its rank is base_w - 1 + (starts at lanes <= k of window w)
     // = base_w + bit0 - 1 + mbcnt(m >> 1).
@@ -966,14 +970,12 @@ struct ChunkLoader {
             const u32x4 od = g->owner[rank & (uint32_t)(kWave - 1)];
             const uint32_t c0 = (w + (uint32_t)u) * (uint32_t)kWave + (uint32_t)lane;
             const uint32_t c = min(c0, T - 1u);
-#if AIPSTACK_GATHER_MODE == 0
-            const uint32_t fi = od[2], li = od[3];
-            const uint32_t head = c == (fi & 0xFFFFFFu) ? fi >> 24 : 0u;
-            const uint32_t tail = c == (li & 0xFFFFFFu) ? li >> 24 : 16u;
-            keep[u] = head * 16u + tail - 1u;
-#else
-            (void)keep;
-#endif
+            if constexpr (!EDGE) {
+                const uint32_t fi = od[2], li = od[3];
+                const uint32_t head = c == (fi & 0xFFFFFFu) ? fi >> 24 : 0u;
+                const uint32_t tail = c == (li & 0xFFFFFFu) ? li >> 24 : 16u;
+                keep[u] = head * 16u + tail - 1u;
+            }
             const uint64_t addr = (((uint64_t)od[1] << 32) | od[0]) + 16ull * c;
             typedef __attribute__((address_space(1))) const u32x4 gseg;
             const gseg *p = (const gseg *)(addr);
@@ -986,9 +988,9 @@ struct ChunkLoader {
 };
 
 // The chain kernel's 64 chunk sums (also the ring slots' chunks). `g`: this wave's LDS
-// scratch; `keep`: the block's mask table (fill_keep_table, mode 0). Returns lane j's exact
-// halves-sum of its chunk.
-template <int U, bool NT>
+// scratch; `keep`: the block's mask table (fill_keep_table, !EDGE only). Returns lane j's
+// exact halves-sum of its chunk.
+template <int U, bool NT, bool EDGE = true>
 __device__ __forceinline__ uint32_t sum_gathered_chunks(uint64_t a, uint32_t l, int lane,
                                                         GatherLds *glds,
                                                         const KeepTable &keep_table) {
@@ -999,7 +1001,7 @@ __device__ __forceinline__ uint32_t sum_gathered_chunks(uint64_t a, uint32_t l, 
     const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)ns_incl, 63);
     if (T == 0) return 0;
     const uint32_t nwin = (T + (uint32_t)kWave - 1u) >> 6;
-    ChunkLoader<U, NT> ld;
+    ChunkLoader<U, NT, EDGE> ld;
     ld.T = T;
     const uint64_t gbase = (a & ~(uint64_t)15) - 16ull * cs;
     // the owners' load parameters, by rank among the non-empty chunks
@@ -1027,14 +1029,15 @@ __device__ __forceinline__ uint32_t sum_gathered_chunks(uint64_t a, uint32_t l, 
             // their loads went out with the group, their scans are skipped (wave-uniform)
             if (wu >= nwin) break;
             const uint32_t c0 = wu * (uint32_t)kWave + (uint32_t)lane;
-#if AIPSTACK_GATHER_MODE == 0
-            const u32x4 km = keep_table[keep[u]];
-            uint32_t s = halves(v[u][0] & km[0],
-                                halves(v[u][1] & km[1],
-                                       halves(v[u][2] & km[2], halves(v[u][3] & km[3], 0u))));
-#else
-            uint32_t s = halves(v[u][0], halves(v[u][1], halves(v[u][2], halves(v[u][3], 0u))));
-#endif
+            uint32_t s;
+            if constexpr (!EDGE) {
+                const u32x4 km = keep_table[keep[u]];
+                s = halves(v[u][0] & km[0],
+                           halves(v[u][1] & km[1],
+                                  halves(v[u][2] & km[2], halves(v[u][3] & km[3], 0u))));
+            } else {
+                s = halves(v[u][0], halves(v[u][1], halves(v[u][2], halves(v[u][3], 0u))));
+            }
             s = c0 < T ? s : 0u;  // lanes past the stream re-read its last segment
             const uint32_t incl = wave_incl_scan(s);
             if (__builtin_amdgcn_ballot_w64(bwin == wu)) {
@@ -1051,23 +1054,19 @@ __device__ __forceinline__ uint32_t sum_gathered_chunks(uint64_t a, uint32_t l, 
     // needed and unconditional (counted waits across the back edge); the last one or two
     // groups are finished straight-line, issuing nothing past the stream.
     const uint32_t groups = (nwin + U - 1u) / U;
-#if AIPSTACK_GATHER_MODE == 1
-    // The lane reads its chunk's two edge segments itself (they lie inside the chunk's
+    // EDGE: the lane reads its chunk's two edge segments itself (they lie inside the chunk's
     // segments, so they are mapped) before the stream's first group, at the default cache
     // policy (the stream reads the same lines later).
     // (none where the chunk starts or ends on a segment boundary: nothing foreign there)
     u32x4 fseg = {0u, 0u, 0u, 0u}, lseg = {0u, 0u, 0u, 0u};
     const uint32_t te = ((rs + l - 1u) & 15u) + 1u;  // the chunk's end in its last segment
-    {
+    if constexpr (EDGE) {
         typedef __attribute__((address_space(1))) const u32x4 gseg;
         if (ns && rs != 0u) fseg = *(const gseg *)(a & ~(uint64_t)15);
         if (ns && te != 16u) lseg = *(const gseg *)((a + l - 1u) & ~(uint64_t)15);
     }
-#endif
     ld.issue(0, va, ka);
-#if AIPSTACK_GATHER_MODE == 1
-    const uint32_t foreign = ns ? foreign_halves(fseg, lseg, (int)rs, (int)te) : 0u;
-#endif
+    const uint32_t foreign = EDGE && ns ? foreign_halves(fseg, lseg, (int)rs, (int)te) : 0u;
     uint32_t g = 0;
     for (; g + 2u < groups; g += 2u) {
         ld.issue((g + 1u) * U, vb, kb);
@@ -1084,11 +1083,7 @@ __device__ __forceinline__ uint32_t sum_gathered_chunks(uint64_t a, uint32_t l, 
     }
     if (bwin >= nwin) gsum = carry;  // cs == T on a multiple of 64: past the last window
     // chunk j ends where chunk j + 1 starts (lane 63: at T, prefix = the final carry)
-#if AIPSTACK_GATHER_MODE == 0
-    return from_next_lane(gsum, carry, lane) - gsum;
-#else
     return from_next_lane(gsum, carry, lane) - gsum - foreign;
-#endif
 }
 
 // Stream mode for one chunk (stream_ok). Lane j < cnt holds packet j = [S, E); returns

@@ -86,6 +86,7 @@ struct Slot {
                               // pinned staging (pageable ring slots, frame bytes only)
     char *dh_stage = nullptr;  // device address of h_stage
     bool zero_copy = false;
+    bool host_bytes = false;  // k_bytes is page-locked host memory the kernel reads over the link
     hipEvent_t done = nullptr;
     bool busy = false;
     void *user_out = nullptr;      // where h_out goes once the slot completes
@@ -524,6 +525,7 @@ int enqueue(aipstack_chksum_engine *e, uint64_t n, void *h_out, uint32_t elem, C
         const bool rows = registered && sp.width != 0 && sp.width < sp.pitch;
         const void *h_src = sp.src;
         s.k_bytes = s.d_bytes;
+        s.host_bytes = in_place || staged_rows;
         if (in_place) {
             // the kernel reads the caller's page-locked bytes over the link itself
             s.k_bytes = const_cast<char *>(reg->dev + (sp.src - reg->p));
@@ -763,8 +765,8 @@ extern "C" int aipstack_chksum_engine_submit_strided(aipstack_chksum_engine *e,
         sp->bytes = (*i1 - i0 - 1) * stride + len;
     };
     auto launch = [&](Slot &s, uint64_t i0, uint64_t i1) {
-        return aipstack_chksum_batch_strided(s.k_bytes, stride, len, i1 - i0, s.k_out, flags,
-                                             s.stream);
+        return batch_strided_from(s.k_bytes, stride, len, i1 - i0, s.k_out, flags, s.stream,
+                                  s.host_bytes);
     };
     std::lock_guard<std::mutex> lock(e->submit_mu);
     return enqueue(e, n, h_out, 2, chunker, launch, ticket);
@@ -875,8 +877,8 @@ extern "C" int aipstack_chksum_engine_submit_csr(aipstack_chksum_engine *e, cons
     if (!e || !h_base || !h_offsets || !h_out || !ticket) return AIPSTACK_CHKSUM_EINVAL;
     return submit_csr_like(e, h_base, h_offsets, n, h_out, 2,
                            [&](Slot &s, uint64_t, uint64_t cnt) {
-                               return aipstack_chksum_batch_csr(s.k_bytes, s.k_off, cnt, s.k_out,
-                                                                flags, s.stream);
+                               return batch_csr_from(s.k_bytes, s.k_off, cnt, s.k_out, flags,
+                                                     s.stream, s.host_bytes);
                            },
                            ticket);
 }
@@ -931,9 +933,9 @@ extern "C" int aipstack_chksum_engine_submit_slotted(aipstack_chksum_engine *e, 
     if (!e || !h_base || !h_len || !h_out || !ticket) return AIPSTACK_CHKSUM_EINVAL;
     return submit_slotted_like(e, h_base, slot_stride, h_len, n, h_out, 2,
                                [&](Slot &s, uint64_t, uint64_t cnt, const uint32_t *d_len) {
-                                   return aipstack_chksum_batch_slotted(s.k_bytes, slot_stride,
-                                                                        d_len, cnt, s.k_out,
-                                                                        flags, s.stream);
+                                   return batch_slotted_from(s.k_bytes, slot_stride, d_len, cnt,
+                                                             s.k_out, flags, s.stream,
+                                                             s.host_bytes);
                                },
                                ticket);
 }

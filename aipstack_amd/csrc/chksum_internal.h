@@ -45,6 +45,17 @@ int tuning_chain_short();
 
 // The contract-violation word of each kernel translation unit on the current device:
 // OR it into *mask, clear it if `clear`.
+// The strided / CSR checksum batches with the caller saying where the packet bytes are:
+// host_bytes = read over the link from page-locked host memory (the engine's zero-copy
+// pieces), where stream mode reads better than the gathered stream, and slots mask their
+// edges in the stream rather than read them twice.
+int batch_strided_from(const void *d_base, uint64_t stride, uint32_t len, uint64_t n,
+                       uint16_t *d_out, uint32_t flags, void *stream, bool host_bytes);
+int batch_csr_from(const void *d_base, const uint64_t *d_offsets, uint64_t n, uint16_t *d_out,
+                   uint32_t flags, void *stream, bool host_bytes);
+int batch_slotted_from(const void *d_base, uint64_t slot_stride, const uint32_t *d_len,
+                       uint64_t n, uint16_t *d_out, uint32_t flags, void *stream,
+                       bool host_bytes);
 int take_violations_batch(uint32_t *mask, bool clear);
 int take_violations_frames(uint32_t *mask, bool clear);
 

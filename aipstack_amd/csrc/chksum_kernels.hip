@@ -81,8 +81,10 @@ __global__ __launch_bounds__(kBlock) void chksum_batch_kernel(Desc desc, uint64_
     };
     __shared__ typename std::conditional<kGathered, GatheredShared, char>::type gsh;
     if constexpr (kGathered) {
-        fill_keep_table(gsh.keep);
-        __syncthreads();
+        if constexpr (!Desc::kEdge) {  // edges masked in the stream: the mask table
+            fill_keep_table(gsh.keep);
+            __syncthreads();
+        }
     }
 
     for (; c < c_end; ++c) {
@@ -104,8 +106,8 @@ __global__ __launch_bounds__(kBlock) void chksum_batch_kernel(Desc desc, uint64_
         if constexpr (kGathered) {
             // (CSR: every packet within the contract, else the wave mode below)
             if (!Desc::kCsr || __builtin_amdgcn_ballot_w64(lE - lS > (uint64_t)AIPSTACK_CHKSUM_MAX_LEN) == 0) {
-                sums = sum_gathered_chunks<SU, NT>(lS, (uint32_t)(lE - lS), lane,
-                                                   &gsh.g[wave_in_block], gsh.keep);
+                sums = sum_gathered_chunks<SU, NT, Desc::kEdge>(lS, (uint32_t)(lE - lS), lane,
+                                                                &gsh.g[wave_in_block], gsh.keep);
                 streamed = true;
             }
         } else if constexpr (SU > 0) {
@@ -198,9 +200,7 @@ __global__ __launch_bounds__(kBlock, SU > 2 ? 4 : 5) void chksum_chain_kernel(
     __shared__ uint64_t lds_acc[kWavesPerBlock][kWave];  // per-chain sum of chunk sums
     __shared__ int lds_mark[kWavesPerBlock][kWave];      // chain starting at chunk lane
     __shared__ GatherLds lds_gather[kWavesPerBlock];                  // gathered stream owners
-    __shared__ KeepTable lds_keep;                                    // its segment masks
-    fill_keep_table(lds_keep);
-    __syncthreads();
+    __shared__ KeepTable lds_keep;  // the mask table, unused: chunk edges are read up front
     const int lane = threadIdx.x & (kWave - 1);
     const uint32_t wave_in_block = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerBlock + wave_in_block;
@@ -635,16 +635,21 @@ int tuning_frames_in_flight() {
 
 using namespace aipstack_amd;
 
-extern "C" int aipstack_chksum_batch_strided(const void *d_base, uint64_t stride, uint32_t len,
-                                             uint64_t n, uint16_t *d_out, uint32_t flags,
-                                             void *stream) {
+namespace aipstack_amd {
+
+int batch_strided_from(const void *d_base, uint64_t stride, uint32_t len, uint64_t n,
+                       uint16_t *d_out, uint32_t flags, void *stream, bool host_bytes) {
     if (n == 0) return AIPSTACK_CHKSUM_OK;
     if (!d_base || !d_out || len > AIPSTACK_CHKSUM_MAX_LEN) return AIPSTACK_CHKSUM_EINVAL;
     if (n > (1ull << 40)) return AIPSTACK_CHKSUM_EINVAL;
     // The gathered stream (round 4), also for packets back to back: config A 217.2 us against
-    // 232.5 in stream mode, B 336.2 / 337.7 (profiles/r04/gatherA); tunable "gather" = -1
-    // keeps stream mode for stride == len.
-    if (stride != len || tuning().gather.load(std::memory_order_relaxed) != -1) {
+    // 232.5 in stream mode, B 336.2 / 337.7 (profiles/r04/gatherA). Stream mode stays for
+    // stride == len where the bytes are read over the link from host memory (the engine's
+    // zero-copy pieces: A end to end 49.7 vs 48.7 GiB/s, profiles/r04/final/e2e.jsonl) or
+    // when tunable "gather" = -1.
+    const bool stream_mode =
+        host_bytes || tuning().gather.load(std::memory_order_relaxed) == -1;
+    if (stride != len || !stream_mode) {
         GappedDesc d{(uint64_t)(uintptr_t)d_base, stride, len};
         return launch<GappedDesc, false>(d, n, len, d_out, flags, (hipStream_t)stream);
     }
@@ -652,9 +657,38 @@ extern "C" int aipstack_chksum_batch_strided(const void *d_base, uint64_t stride
     return launch<StridedDesc, false>(d, n, len, d_out, flags, (hipStream_t)stream);
 }
 
-extern "C" int aipstack_chksum_batch_slotted(const void *d_base, uint64_t slot_stride,
-                                             const uint32_t *d_len, uint64_t n, uint16_t *d_out,
-                                             uint32_t flags, void *stream) {
+int batch_csr_from(const void *d_base, const uint64_t *d_offsets, uint64_t n, uint16_t *d_out,
+                   uint32_t flags, void *stream, bool host_bytes) {
+    if (n == 0) return AIPSTACK_CHKSUM_OK;
+    if (!d_base || !d_offsets || !d_out) return AIPSTACK_CHKSUM_EINVAL;
+    if (n > (1ull << 40)) return AIPSTACK_CHKSUM_EINVAL;
+    // Typical network packets (<= ~2 KiB) fit one group at U = 2 in the wave mode; longer
+    // ones loop. The gathered stream (config C 231.0 us against 251.8 in stream mode), except
+    // for bytes read over the link from host memory (C end to end 48.9 vs 44.9 GiB/s) or
+    // with tunable "gather" = -1.
+    if (!host_bytes && tuning().gather.load(std::memory_order_relaxed) != -1) {
+        GatheredCsrDesc d;
+        d.base = (uint64_t)(uintptr_t)d_base;
+        d.offsets = d_offsets;
+        return launch<GatheredCsrDesc, false>(d, n, 1500u, d_out, flags, (hipStream_t)stream);
+    }
+    CsrDesc d{(uint64_t)(uintptr_t)d_base, d_offsets};
+    return launch<CsrDesc, false>(d, n, 1500u, d_out, flags, (hipStream_t)stream);
+}
+
+}  // namespace aipstack_amd
+
+extern "C" int aipstack_chksum_batch_strided(const void *d_base, uint64_t stride, uint32_t len,
+                                             uint64_t n, uint16_t *d_out, uint32_t flags,
+                                             void *stream) {
+    return batch_strided_from(d_base, stride, len, n, d_out, flags, stream, false);
+}
+
+namespace aipstack_amd {
+
+int batch_slotted_from(const void *d_base, uint64_t slot_stride, const uint32_t *d_len,
+                       uint64_t n, uint16_t *d_out, uint32_t flags, void *stream,
+                       bool host_bytes) {
     if (n == 0) return AIPSTACK_CHKSUM_OK;
     if (!d_base || !d_len || !d_out || slot_stride == 0 || n > (1ull << 40))
         return AIPSTACK_CHKSUM_EINVAL;
@@ -666,26 +700,27 @@ extern "C" int aipstack_chksum_batch_slotted(const void *d_base, uint64_t slot_s
     // U from the typical packet (<= ~2 KiB: one group of 2 segments per lane), not the
     // slot: C2K (64-1500 B in 2048-B slots) U = 1 / 2 / 3: 286 / 277 / 328 us
     // (profiles/r03/slots/sweep_C2K.jsonl); longer packets loop over further groups
-    return launch<SlottedDesc, false>(d, n, d.cap < 2000u ? d.cap : 2000u, d_out, flags,
-                                      (hipStream_t)stream);
+    const uint32_t max_len = d.cap < 2000u ? d.cap : 2000u;
+    if (host_bytes) {  // read over the link: edges masked in the stream (SlottedHostDesc)
+        SlottedHostDesc h;
+        static_cast<SlottedDesc &>(h) = d;
+        return launch<SlottedHostDesc, false>(h, n, max_len, d_out, flags, (hipStream_t)stream);
+    }
+    return launch<SlottedDesc, false>(d, n, max_len, d_out, flags, (hipStream_t)stream);
+}
+
+}  // namespace aipstack_amd
+
+extern "C" int aipstack_chksum_batch_slotted(const void *d_base, uint64_t slot_stride,
+                                             const uint32_t *d_len, uint64_t n, uint16_t *d_out,
+                                             uint32_t flags, void *stream) {
+    return batch_slotted_from(d_base, slot_stride, d_len, n, d_out, flags, stream, false);
 }
 
 extern "C" int aipstack_chksum_batch_csr(const void *d_base, const uint64_t *d_offsets,
                                          uint64_t n, uint16_t *d_out, uint32_t flags,
                                          void *stream) {
-    if (n == 0) return AIPSTACK_CHKSUM_OK;
-    if (!d_base || !d_offsets || !d_out) return AIPSTACK_CHKSUM_EINVAL;
-    if (n > (1ull << 40)) return AIPSTACK_CHKSUM_EINVAL;
-    // Typical network packets (<= ~2 KiB) fit one group at U = 2 in the wave mode; longer
-    // ones loop. The gathered stream unless tunable "gather" = -1 (stream mode).
-    if (tuning().gather.load(std::memory_order_relaxed) != -1) {
-        GatheredCsrDesc d;
-        d.base = (uint64_t)(uintptr_t)d_base;
-        d.offsets = d_offsets;
-        return launch<GatheredCsrDesc, false>(d, n, 1500u, d_out, flags, (hipStream_t)stream);
-    }
-    CsrDesc d{(uint64_t)(uintptr_t)d_base, d_offsets};
-    return launch<CsrDesc, false>(d, n, 1500u, d_out, flags, (hipStream_t)stream);
+    return batch_csr_from(d_base, d_offsets, n, d_out, flags, stream, false);
 }
 
 extern "C" int aipstack_chksum_batch_seeded_csr(const void *d_base, const uint64_t *d_offsets,
