@@ -733,12 +733,20 @@ struct NoStreamHook {
     __device__ __forceinline__ void window(const u32x4 &, uint32_t) {}
 };
 
-template <int U, bool NT, int PRE = U>
+// DB (round 4): the next group of U windows is issued before the current one is summed (two
+// register sets, as the gathered stream does, §5.2 of DESIGN.md), so a wave always has
+// U..2U windows in flight; without it the next group goes out only after the current one is
+// summed.
+#ifndef AIPSTACK_STREAM_DB  // the checksum batches' stream mode with DB (A/B build switch;
+#define AIPSTACK_STREAM_DB 0  // round 4: A 233.2 vs 233.6 us, so off)
+#endif
+template <int U, bool NT, int PRE = U, bool DB = false>
 struct StreamRun {
     uint64_t A, X1;
     uint32_t nseg, nwin;
     __amdgpu_buffer_rsrc_t rsrc;
     u32x4 v[U];
+    u32x4 v2[DB ? U : 1];
 
     // Issues windows [0, PRE) now (the rest of the first U when prefixes() starts): a
     // kernel that overlaps begin() with register-hungry work keeps only PRE in flight.
@@ -760,6 +768,14 @@ struct StreamRun {
 #pragma unroll
         for (int u = U0; u < U1; ++u) {
             v[u] = load_segment<NT>(rsrc, voff, (w + (uint32_t)u) * 1024u);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    template <int N>
+    __device__ __forceinline__ void issue_into(u32x4 (&dst)[N], uint32_t w, uint32_t voff) {
+#pragma unroll
+        for (int u = 0; u < N; ++u) {
+            dst[u] = load_segment<NT>(rsrc, voff, (w + (uint32_t)u) * 1024u);
             __builtin_amdgcn_sched_barrier(0);
         }
     }
@@ -798,13 +814,14 @@ struct StreamRun {
         if constexpr (PRE < U) issue<PRE, U>(0, voff);
         uint32_t carry = 0;  // H(start of the current window), mod 2^32
         uint32_t x_hi = 0;   // halves of the last segment's bytes at or above X1
-        for (uint32_t w = 0; w < nwin;) {
+        // one group of U windows [w, w + U) held in vv
+        auto consume = [&](const u32x4 (&vv)[U], uint32_t w) {
             hook.group(w);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const uint32_t wu = w + (uint32_t)u;
                 const uint32_t s =
-                    halves(v[u][0], halves(v[u][1], halves(v[u][2], halves(v[u][3], 0u))));
+                    halves(vv[u][0], halves(vv[u][1], halves(vv[u][2], halves(vv[u][3], 0u))));
                 const uint32_t incl = wave_incl_scan(s);
                 const uint32_t excl = incl - s;
 #pragma unroll
@@ -815,7 +832,7 @@ struct StreamRun {
 #pragma unroll
                             for (int d = 0; d < 4; ++d)
                                 part = halves((uint32_t)__builtin_amdgcn_ds_bpermute(
-                                                  bsrc[k], (int)v[u][d]) &
+                                                  bsrc[k], (int)vv[u][d]) &
                                                   below[k][d],
                                               part);
                         }
@@ -825,14 +842,37 @@ struct StreamRun {
                 if (wu == xwin && xt != 0) {  // wave-uniform: X1 falls inside this segment
                     uint32_t hh = 0;
 #pragma unroll
-                    for (int d = 0; d < 4; ++d) hh = halves(v[u][d] & xabove[d], hh);
+                    for (int d = 0; d < 4; ++d) hh = halves(vv[u][d] & xabove[d], hh);
                     x_hi = (uint32_t)__builtin_amdgcn_readlane((int)hh, xlane);
                 }
                 carry += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-                hook.window(v[u], wu);
+                hook.window(vv[u], wu);
             }
-            w += U;
-            if (w < nwin) issue<0, U>(w, voff);
+        };
+        if constexpr (DB) {
+            // as the gathered stream: group g + 1 is issued before group g is summed; the loop
+            // runs while at least three groups remain (both issues needed and unconditional,
+            // so every wait is counted), the last one or two groups straight-line
+            const uint32_t groups = (nwin + U - 1u) / U;
+            uint32_t g = 0;
+            for (; g + 2u < groups; g += 2u) {
+                issue_into(v2, (g + 1u) * U, voff);
+                consume(v, g * U);
+                issue<0, U>((g + 2u) * U, voff);
+                consume(v2, (g + 1u) * U);
+            }
+            if (g + 2u == groups) {
+                issue_into(v2, (g + 1u) * U, voff);
+                consume(v, g * U);
+                consume(v2, (g + 1u) * U);
+            } else {
+                consume(v, g * U);
+            }
+        } else {
+            for (uint32_t w = 0; w < nwin; w += U) {
+                consume(v, w);
+                if (w + U < nwin) issue<0, U>(w + U, voff);
+            }
         }
         hx = carry - x_hi;  // H(X1)
 #pragma unroll
@@ -1101,7 +1141,7 @@ __device__ __forceinline__ uint32_t sum_stream_chunk(uint64_t S, uint64_t E, int
         ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(S >> 32)) << 32) |
         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)S);
     // the run spans <= 64 * 2^17 + 15 bytes (stream_ok)
-    StreamRun<U, NT> run;
+    StreamRun<U, NT, U, AIPSTACK_STREAM_DB != 0> run;
     run.begin(S0 & ~(uint64_t)15, X1, voff);
     const uint64_t bs[1] = {S};
     uint32_t hb[1], hx;

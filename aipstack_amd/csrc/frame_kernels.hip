@@ -529,6 +529,13 @@ __device__ __forceinline__ FieldSectors pick_sectors(const u32x4 (&seg)[kHdrSegs
 #ifndef AIPSTACK_FRAME_PREFETCH
 #define AIPSTACK_FRAME_PREFETCH(SU) ((SU) / 2)
 #endif
+// Frames whose headers are captured from the stream: the next group of windows issued before
+// the current one is summed (StreamRun's DB; round 4, profiles/r04/fdb: RX 120.1 -> 117.6 us,
+// split Tx fill 161.2 -> 155.8, records pass 129.2 -> 127.6; 128 VGPRs at 8 windows, no
+// spill, the same 4 waves per SIMD). A/B build switch: -DAIPSTACK_FRAME_DB=0.
+#ifndef AIPSTACK_FRAME_DB
+#define AIPSTACK_FRAME_DB 1
+#endif
 // GATHER: where the parse's header segments come from (launch_frames picks it):
 //   kHdrLoads    per-lane loads before the stream (default policy);
 //   kHdrCapture  copied out of the stream windows as they pass (Rx, the records-only pass);
@@ -625,7 +632,7 @@ __device__ __forceinline__ FrameOut process_chunk(const Desc &desc, uint64_t p0,
                 touch1 = __builtin_amdgcn_raw_buffer_load_b32(
                     hrsrc, act ? (fo + 50u) & ~3u : 0xFFFFFFF0u, 0u, 0);
             }
-            StreamRun<SU, NT> run;
+            StreamRun<SU, NT, SU, AIPSTACK_FRAME_DB != 0> run;
             run.begin(base, X1, voff);
             // compact slot of r0: the union segments below it. Regions start and end in
             // lane order, so region j adds [max(r0_j, r1_{j-1}), r1_j) to the union.

@@ -217,6 +217,20 @@ e2eh)  # the engine's zero-copy strided / CSR pieces back in stream mode: engine
     timeout -k 10 300 python bench.py --e2e --config $c --steps 5 --warmup 1 >> "$out/e2e.jsonl" 2>> "$out/e2e.err"
   done
   ;;
+fdb)  # double-buffered stream mode (tools/build/lib_fdb.so: frames' captured stream and the
+      # batches' stream mode issue the next group before summing the current one)
+  for i in 1 2 3; do
+    for c in RX TX TXREC; do
+      bench ${c}_base --config $c --per-launch --no-cpu-baseline
+      AIPSTACK_AMD_LIB=tools/build/lib_fdb.so bench ${c}_db8 --config $c --per-launch --no-cpu-baseline
+      AIPSTACK_AMD_LIB=tools/build/lib_fdb.so AIPSTACK_CHKSUM_STREAM=4 bench ${c}_db4 --config $c --per-launch --no-cpu-baseline
+    done
+    AIPSTACK_CHKSUM_GATHER=-1 bench A_stream --config A --per-launch --no-cpu-baseline
+    AIPSTACK_AMD_LIB=tools/build/lib_fdb.so AIPSTACK_CHKSUM_GATHER=-1 bench A_streamdb --config A --per-launch --no-cpu-baseline
+  done
+  AIPSTACK_AMD_LIB=tools/build/lib_fdb.so timeout -k 10 600 python -u -m pytest tests -x -q --timeout 120 \
+      --timeout-method thread -m gpu -k "rx_verify or tx_fill or frames or random" > "$out/pytest_fdb.log" 2>&1
+  ;;
 kern)
   pyt pytest_kern -m gpu -k "chain or contract_violations or native_library"
   for i in 1 2 3; do
