@@ -1028,12 +1028,13 @@ struct ChunkLoader {
 };
 
 // The chain kernel's 64 chunk sums (also the ring slots' chunks). `g`: this wave's LDS
-// scratch; `keep`: the block's mask table (fill_keep_table, !EDGE only). Returns lane j's
+// scratch; `keep_table`: the block's mask table (fill_keep_table; !EDGE only, else unused and
+// may be null). Returns lane j's
 // exact halves-sum of its chunk.
 template <int U, bool NT, bool EDGE = true>
 __device__ __forceinline__ uint32_t sum_gathered_chunks(uint64_t a, uint32_t l, int lane,
                                                         GatherLds *glds,
-                                                        const KeepTable &keep_table) {
+                                                        const KeepTable *keep_table) {
     const uint32_t rs = (uint32_t)a & 15u;
     const uint32_t ns = l ? (rs + l + 15u) >> 4 : 0u;
     const uint32_t ns_incl = wave_incl_scan(ns);
@@ -1071,7 +1072,7 @@ __device__ __forceinline__ uint32_t sum_gathered_chunks(uint64_t a, uint32_t l, 
             const uint32_t c0 = wu * (uint32_t)kWave + (uint32_t)lane;
             uint32_t s;
             if constexpr (!EDGE) {
-                const u32x4 km = keep_table[keep[u]];
+                const u32x4 km = (*keep_table)[keep[u]];
                 s = halves(v[u][0] & km[0],
                            halves(v[u][1] & km[1],
                                   halves(v[u][2] & km[2], halves(v[u][3] & km[3], 0u))));

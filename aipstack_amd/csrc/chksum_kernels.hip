@@ -107,7 +107,7 @@ __global__ __launch_bounds__(kBlock) void chksum_batch_kernel(Desc desc, uint64_
             // (CSR: every packet within the contract, else the wave mode below)
             if (!Desc::kCsr || __builtin_amdgcn_ballot_w64(lE - lS > (uint64_t)AIPSTACK_CHKSUM_MAX_LEN) == 0) {
                 sums = sum_gathered_chunks<SU, NT, Desc::kEdge>(lS, (uint32_t)(lE - lS), lane,
-                                                                &gsh.g[wave_in_block], gsh.keep);
+                                                                &gsh.g[wave_in_block], &gsh.keep);
                 streamed = true;
             }
         } else if constexpr (SU > 0) {
@@ -200,7 +200,6 @@ __global__ __launch_bounds__(kBlock, SU > 2 ? 4 : 5) void chksum_chain_kernel(
     __shared__ uint64_t lds_acc[kWavesPerBlock][kWave];  // per-chain sum of chunk sums
     __shared__ int lds_mark[kWavesPerBlock][kWave];      // chain starting at chunk lane
     __shared__ GatherLds lds_gather[kWavesPerBlock];                  // gathered stream owners
-    __shared__ KeepTable lds_keep;  // the mask table, unused: chunk edges are read up front
     const int lane = threadIdx.x & (kWave - 1);
     const uint32_t wave_in_block = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerBlock + wave_in_block;
@@ -298,11 +297,11 @@ __global__ __launch_bounds__(kBlock, SU > 2 ? 4 : 5) void chksum_chain_kernel(
                 const uint32_t a_hi = (uint32_t)__builtin_amdgcn_ds_permute(to, (int)(uint32_t)(a >> 32));
                 const uint32_t l_p = (uint32_t)__builtin_amdgcn_ds_permute(to, (int)lv);
                 const uint32_t s_p = sum_gathered_chunks<SU, NT>(
-                    ((uint64_t)a_hi << 32) | a_lo, l_p, lane, &lds_gather[wave_in_block], lds_keep);
+                    ((uint64_t)a_hi << 32) | a_lo, l_p, lane, &lds_gather[wave_in_block], nullptr);
                 sums = (uint32_t)__builtin_amdgcn_ds_bpermute(to, (int)s_p);
             } else {
                 sums = sum_gathered_chunks<SU, NT>(a, lv, lane, &lds_gather[wave_in_block],
-                                                   lds_keep);
+                                                   nullptr);
             }
             uint32_t r = fold16(sums);
             if ((uint32_t)(a & 1) == q)

@@ -536,6 +536,11 @@ __device__ __forceinline__ FieldSectors pick_sectors(const u32x4 (&seg)[kHdrSegs
 #ifndef AIPSTACK_FRAME_DB
 #define AIPSTACK_FRAME_DB 1
 #endif
+// Ring slots: the L4 bytes past the header blocks read as one gathered stream of the chunk's
+// frames (1) or one frame per wave instruction pair (0, rounds 3-4), an A/B build switch.
+#ifndef AIPSTACK_FRAME_SLOT_GATHER
+#define AIPSTACK_FRAME_SLOT_GATHER 1
+#endif
 // GATHER: where the parse's header segments come from (launch_frames picks it):
 //   kHdrLoads    per-lane loads before the stream (default policy);
 //   kHdrCapture  copied out of the stream windows as they pass (Rx, the records-only pass);
@@ -548,9 +553,10 @@ template <class Desc, bool TX, int U, int P, bool NT, int SU, int GATHER, bool S
 __device__ __forceinline__ FrameOut process_chunk(const Desc &desc, uint64_t p0, uint64_t n,
                                                   uint32_t cpk, int lane, uint32_t voff,
                                                   uint32_t not_lane0, FrameLds *lds,
-                                                  int &cnt_out) {
-    const auto chunk = desc.begin_chunk(p0, n, lane);
+                                                  GatherLds *glds, int &cnt_out) {
     const int cnt = (int)min((uint64_t)cpk, n - p0);
+    // the chunk's own table entries only (lanes past it re-read entry p0 + cnt)
+    const auto chunk = desc.begin_chunk(p0, p0 + (uint64_t)cnt, lane);
     cnt_out = cnt;
     uint64_t S, E;
     desc.lane_bounds(chunk, lane, S, E);
@@ -747,12 +753,20 @@ __device__ __forceinline__ FrameOut process_chunk(const Desc &desc, uint64_t p0,
         // sector stores: ring slots (this is their only path), not the rare CSR chunks that
         // are not back to back (16 more VGPRs through the per-frame loop)
         if constexpr (SECT && !Desc::kStream) fsec = pick_sectors(seg, S, E, fl);
-        const bool need = fl.ce != fl.cs;
-        const LaneMeta meta = lane_meta(fl.cs, fl.ce);
-        // (C) the remaining L4 bytes, one frame per wave, P frames' loads in flight
-        NoMaskHook hook;
-        const uint32_t sums = sum_lane_packets<U, P, AIPSTACK_ROWS_FRAMES, NT>(
-            meta, __builtin_amdgcn_ballot_w64(need), lane, voff, not_lane0, hook);
+        uint32_t sums;
+        if constexpr (!Desc::kStream && AIPSTACK_FRAME_SLOT_GATHER) {
+            // (C) ring slots: the remaining L4 bytes of the chunk's frames as one gathered
+            // stream of just their segments (chksum_device.h; round 4)
+            const uint32_t l4rest = lane < cnt ? (uint32_t)(fl.ce - fl.cs) : 0u;
+            sums = sum_gathered_chunks<4, NT>(fl.cs, l4rest, lane, glds, nullptr);
+        } else {
+            const bool need = fl.ce != fl.cs;
+            const LaneMeta meta = lane_meta(fl.cs, fl.ce);
+            // (C) the remaining L4 bytes, one frame per wave, P frames' loads in flight
+            NoMaskHook hook;
+            sums = sum_lane_packets<U, P, AIPSTACK_ROWS_FRAMES, NT>(
+                meta, __builtin_amdgcn_ballot_w64(need), lane, voff, not_lane0, hook);
+        }
         // both parts (< 2^24 + 2^17), folded
         r = fold16(sums + fold16(fl.part));
     }
@@ -799,11 +813,14 @@ __global__ __launch_bounds__(kBlock, AIPSTACK_FRAME_WAVES_PER_SIMD) void frame_k
     constexpr bool kGather = SU > 0 && GATHER != kHdrLoads;
     __shared__ FrameLds lds[kGather ? kWavesPerBlock : 1];  // 9 KiB per wave (gathered stream)
     FrameLds *my = &lds[kGather ? wave_in_block : 0];
+    constexpr bool kSlotGather = !Desc::kStream && AIPSTACK_FRAME_SLOT_GATHER;
+    __shared__ GatherLds glds[kSlotGather ? kWavesPerBlock : 1];  // ring slots' L4 stream
+    GatherLds *mg = &glds[kSlotGather ? wave_in_block : 0];
     for (; c < c_end; ++c) {
         const uint64_t p0 = c * cpk;
         int cnt;
         const FrameOut o = process_chunk<Desc, TX, U, P, NT, SU, GATHER, SECT>(
-            desc, p0, n, (uint32_t)cpk, lane, voff, not_lane0, my, cnt);
+            desc, p0, n, (uint32_t)cpk, lane, voff, not_lane0, my, mg, cnt);
         if (lane < cnt) {
             if constexpr (SPLIT)
 #if AIPSTACK_EXP_NO_RECORDS  // experiment: price of the record stores (wrong output)

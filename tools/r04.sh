@@ -231,6 +231,19 @@ fdb)  # double-buffered stream mode (tools/build/lib_fdb.so: frames' captured st
   AIPSTACK_AMD_LIB=tools/build/lib_fdb.so timeout -k 10 600 python -u -m pytest tests -x -q --timeout 120 \
       --timeout-method thread -m gpu -k "rx_verify or tx_fill or frames or random" > "$out/pytest_fdb.log" 2>&1
   ;;
+slotg)  # ring-slot frames: the L4 bytes past the header blocks as one gathered stream (product)
+        # vs one frame per wave instruction pair (tools/build/lib_noslot.so)
+  pyt pytest_slotg -m gpu -k "slotted or frames or rx_verify or tx_fill or random or engine"
+  for i in 1 2 3; do
+    for c in RX2K TX2K; do
+      AIPSTACK_AMD_LIB=tools/build/lib_noslot.so bench ${c}_wave --config $c --per-launch --no-cpu-baseline
+      bench ${c}_gather --config $c --per-launch --no-cpu-baseline
+    done
+  done
+  for i in 1 2; do
+    sweep tx2k --config TX2K --variants "split=0;split=1;split=0,frames=4"
+  done
+  ;;
 kern)
   pyt pytest_kern -m gpu -k "chain or contract_violations or native_library"
   for i in 1 2 3; do
