@@ -244,6 +244,11 @@ slotg)  # ring-slot frames: the L4 bytes past the header blocks as one gathered 
     sweep tx2k --config TX2K --variants "split=0;split=1;split=0,frames=4"
   done
   ;;
+slotg2)  # slotted frames' chunk size with the gathered L4 stream
+  timeout -k 10 300 python tools/slot_sweep.py --config RX2K --rounds 6 --variants \
+      "chunk_packets=32;chunk_packets=16;chunk_packets=64;chunk_packets=8" > "$out/rx2k_sweep.jsonl" 2> "$out/rx2k_sweep.err"
+  sweep tx2k --config TX2K --variants "split=0,chunk_packets=32;split=0,chunk_packets=16;split=0,chunk_packets=64;split=0,chunk_packets=8"
+  ;;
 kern)
   pyt pytest_kern -m gpu -k "chain or contract_violations or native_library"
   for i in 1 2 3; do
