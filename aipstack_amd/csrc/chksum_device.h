@@ -89,6 +89,7 @@ __device__ __forceinline__ uint32_t from_next_lane(uint32_t v, uint32_t last, in
 struct StridedDesc {
     static constexpr bool kCsr = false;
     static constexpr bool kStream = true;  // SU > 0: stream mode for back-to-back chunks
+    static constexpr bool kEdge = true;    // (gathered descriptors only)
     uint64_t base;    // absolute address of packet 0
     uint64_t stride;  // bytes between packet starts
     uint32_t len;     // bytes per packet
@@ -154,6 +155,7 @@ struct GappedDesc {
 struct CsrDesc {
     static constexpr bool kCsr = true;
     static constexpr bool kStream = true;
+    static constexpr bool kEdge = true;  // (gathered descriptors only)
     uint64_t base;            // absolute address offsets are relative to
     const uint64_t *offsets;  // n+1 byte offsets
 

@@ -948,9 +948,10 @@ extern "C" int aipstack_chksum_engine_submit_rx_verify_slotted(
         return AIPSTACK_CHKSUM_EINVAL;
     return submit_slotted_like(e, h_base, slot_stride, h_len, n, h_verdicts, 1,
                                [&](Slot &s, uint64_t, uint64_t cnt, const uint32_t *d_len) {
-                                   return aipstack_chksum_rx_verify_slotted(
+                                   return rx_verify_slotted_from(
                                        s.k_bytes, slot_stride, d_len, cnt,
-                                       reinterpret_cast<uint8_t *>(s.k_out), s.stream);
+                                       reinterpret_cast<uint8_t *>(s.k_out), s.stream,
+                                       s.host_bytes);
                                },
                                ticket);
 }
@@ -968,9 +969,10 @@ extern "C" int aipstack_chksum_engine_submit_tx_fill_slotted(
                                    s.tx_offs = nullptr;
                                    s.tx_stride = slot_stride;
                                    s.tx_status = h_status + i0;
-                                   return aipstack_chksum_tx_fill_records_slotted(
+                                   return tx_fill_records_slotted_from(
                                        s.k_bytes, slot_stride, d_len, cnt,
-                                       reinterpret_cast<uint64_t *>(s.k_out), s.stream);
+                                       reinterpret_cast<uint64_t *>(s.k_out), s.stream,
+                                       s.host_bytes);
                                },
                                ticket);
 }

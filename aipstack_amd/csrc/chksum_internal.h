@@ -56,6 +56,10 @@ int batch_csr_from(const void *d_base, const uint64_t *d_offsets, uint64_t n, ui
 int batch_slotted_from(const void *d_base, uint64_t slot_stride, const uint32_t *d_len,
                        uint64_t n, uint16_t *d_out, uint32_t flags, void *stream,
                        bool host_bytes);
+int rx_verify_slotted_from(const void *d_base, uint64_t slot_stride, const uint32_t *d_len,
+                           uint64_t n, uint8_t *d_verdict, void *stream, bool host_bytes);
+int tx_fill_records_slotted_from(const void *d_base, uint64_t slot_stride, const uint32_t *d_len,
+                                 uint64_t n, uint64_t *d_records, void *stream, bool host_bytes);
 int take_violations_batch(uint32_t *mask, bool clear);
 int take_violations_frames(uint32_t *mask, bool clear);
 

@@ -754,7 +754,7 @@ __device__ __forceinline__ FrameOut process_chunk(const Desc &desc, uint64_t p0,
         // are not back to back (16 more VGPRs through the per-frame loop)
         if constexpr (SECT && !Desc::kStream) fsec = pick_sectors(seg, S, E, fl);
         uint32_t sums;
-        if constexpr (!Desc::kStream && AIPSTACK_FRAME_SLOT_GATHER) {
+        if constexpr (!Desc::kStream && AIPSTACK_FRAME_SLOT_GATHER && Desc::kEdge) {
             // (C) ring slots: the remaining L4 bytes of the chunk's frames as one gathered
             // stream of just their segments (chksum_device.h; round 4)
             const uint32_t l4rest = lane < cnt ? (uint32_t)(fl.ce - fl.cs) : 0u;
@@ -813,7 +813,7 @@ __global__ __launch_bounds__(kBlock, AIPSTACK_FRAME_WAVES_PER_SIMD) void frame_k
     constexpr bool kGather = SU > 0 && GATHER != kHdrLoads;
     __shared__ FrameLds lds[kGather ? kWavesPerBlock : 1];  // 9 KiB per wave (gathered stream)
     FrameLds *my = &lds[kGather ? wave_in_block : 0];
-    constexpr bool kSlotGather = !Desc::kStream && AIPSTACK_FRAME_SLOT_GATHER;
+    constexpr bool kSlotGather = !Desc::kStream && AIPSTACK_FRAME_SLOT_GATHER && Desc::kEdge;
     __shared__ GatherLds glds[kSlotGather ? kWavesPerBlock : 1];  // ring slots' L4 stream
     GatherLds *mg = &glds[kSlotGather ? wave_in_block : 0];
     for (; c < c_end; ++c) {
@@ -939,11 +939,26 @@ int launch_frames(const void *d_base, const uint64_t *d_offsets, uint64_t n, uin
 
 }  // namespace
 
-// Ring slots (SlottedDesc): per-lane header loads and the per-frame L4 loop; no stream mode,
-// so the header capture does not apply either.
+// Ring slots (SlottedDesc): per-lane header loads, then the L4 bytes past the header blocks as
+// one gathered stream of the chunk's frames -- or, for slots read over the link from host
+// memory (the engine's zero-copy pieces, host_bytes), one frame per wave instruction pair
+// (SlottedHostDesc), where the gathered stream's second read of an edge segment would cross
+// the link again. No stream mode, so the header capture does not apply either.
+template <bool TX, bool SPLIT, class D>
+int launch_frames_slotted_d(const D &desc, uint64_t n, uint8_t *d_status, uint64_t *d_records,
+                            hipStream_t stream, int cus) {
+    if constexpr (TX && !SPLIT) {
+        if (tuning_tx_store(kTxStoreDefault) == kTxStoreSectors)
+            return launch_frames_g<D, true, false, kHdrLoads, true>(desc, n, d_status, d_records,
+                                                                  stream, cus);
+    }
+    return launch_frames_g<D, TX, SPLIT, kHdrLoads>(desc, n, d_status, d_records, stream, cus);
+}
+
 template <bool TX, bool SPLIT>
 int launch_frames_slotted(const void *d_base, uint64_t slot_stride, const uint32_t *d_len,
-                          uint64_t n, uint8_t *d_status, uint64_t *d_records, hipStream_t stream) {
+                          uint64_t n, uint8_t *d_status, uint64_t *d_records, hipStream_t stream,
+                          bool host_bytes = false) {
     const int cus = device_cu_count(stream);
     if (cus <= 0) return AIPSTACK_CHKSUM_EHIP;
     SlottedDesc desc;
@@ -951,13 +966,14 @@ int launch_frames_slotted(const void *d_base, uint64_t slot_stride, const uint32
     desc.stride = slot_stride;
     desc.lens = d_len;
     desc.cap = (uint32_t)(slot_stride < AIPSTACK_CHKSUM_MAX_LEN ? slot_stride : AIPSTACK_CHKSUM_MAX_LEN);
-    if constexpr (TX && !SPLIT) {
-        if (tuning_tx_store(kTxStoreDefault) == kTxStoreSectors)
-            return launch_frames_g<SlottedDesc, true, false, kHdrLoads, true>(desc, n, d_status,
-                                                                            d_records, stream, cus);
+    int st;
+    if (host_bytes) {
+        SlottedHostDesc h;
+        static_cast<SlottedDesc &>(h) = desc;
+        st = launch_frames_slotted_d<TX, SPLIT>(h, n, d_status, d_records, stream, cus);
+    } else {
+        st = launch_frames_slotted_d<TX, SPLIT>(desc, n, d_status, d_records, stream, cus);
     }
-    const int st = launch_frames_g<SlottedDesc, TX, SPLIT, kHdrLoads>(desc, n, d_status, d_records,
-                                                                     stream, cus);
     if (st != AIPSTACK_CHKSUM_OK || !SPLIT || !d_status) return st;
     // the split slotted fill's scatter pass (records pass above: d_status is null for the
     // records-only call)
@@ -969,6 +985,27 @@ int launch_frames_slotted(const void *d_base, uint64_t slot_stride, const uint32
 
 int take_violations_frames(uint32_t *mask, bool clear) {
     return take_violations_here(mask, clear);
+}
+
+int rx_verify_slotted_from(const void *d_base, uint64_t slot_stride, const uint32_t *d_len,
+                           uint64_t n, uint8_t *d_verdict, void *stream, bool host_bytes) {
+    if (n == 0) return AIPSTACK_CHKSUM_OK;
+    if (!d_base || !d_len || !d_verdict || slot_stride == 0 ||
+        slot_stride > kMaxSlotStride || n > (1ull << 40))
+        return AIPSTACK_CHKSUM_EINVAL;
+    return launch_frames_slotted<false, false>(d_base, slot_stride, d_len, n, d_verdict, nullptr,
+                                               (hipStream_t)stream, host_bytes);
+}
+
+int tx_fill_records_slotted_from(const void *d_base, uint64_t slot_stride, const uint32_t *d_len,
+                                 uint64_t n, uint64_t *d_records, void *stream, bool host_bytes) {
+    if (n == 0) return AIPSTACK_CHKSUM_OK;
+    if (!d_base || !d_len || !d_records || slot_stride == 0 ||
+        slot_stride > kMaxSlotStride || n > (1ull << 40) ||
+        ((uintptr_t)d_records & 7u) != 0)
+        return AIPSTACK_CHKSUM_EINVAL;
+    return launch_frames_slotted<true, true>(d_base, slot_stride, d_len, n, nullptr, d_records,
+                                             (hipStream_t)stream, host_bytes);
 }
 
 }  // namespace aipstack_amd
@@ -1018,12 +1055,7 @@ extern "C" int aipstack_chksum_tx_fill_split(void *d_base, const uint64_t *d_off
 extern "C" int aipstack_chksum_rx_verify_slotted(const void *d_base, uint64_t slot_stride,
                                                  const uint32_t *d_len, uint64_t n,
                                                  uint8_t *d_verdict, void *stream) {
-    if (n == 0) return AIPSTACK_CHKSUM_OK;
-    if (!d_base || !d_len || !d_verdict || slot_stride == 0 ||
-        slot_stride > kMaxSlotStride || n > (1ull << 40))
-        return AIPSTACK_CHKSUM_EINVAL;
-    return launch_frames_slotted<false, false>(d_base, slot_stride, d_len, n, d_verdict, nullptr,
-                                               (hipStream_t)stream);
+    return rx_verify_slotted_from(d_base, slot_stride, d_len, n, d_verdict, stream, false);
 }
 
 extern "C" int aipstack_chksum_tx_fill_slotted(void *d_base, uint64_t slot_stride,
@@ -1055,11 +1087,5 @@ extern "C" int aipstack_chksum_tx_fill_slotted_split(void *d_base, uint64_t slot
 extern "C" int aipstack_chksum_tx_fill_records_slotted(const void *d_base, uint64_t slot_stride,
                                                        const uint32_t *d_len, uint64_t n,
                                                        uint64_t *d_records, void *stream) {
-    if (n == 0) return AIPSTACK_CHKSUM_OK;
-    if (!d_base || !d_len || !d_records || slot_stride == 0 ||
-        slot_stride > kMaxSlotStride || n > (1ull << 40) ||
-        ((uintptr_t)d_records & 7u) != 0)
-        return AIPSTACK_CHKSUM_EINVAL;
-    return launch_frames_slotted<true, true>(d_base, slot_stride, d_len, n, nullptr, d_records,
-                                             (hipStream_t)stream);
+    return tx_fill_records_slotted_from(d_base, slot_stride, d_len, n, d_records, stream, false);
 }

@@ -212,8 +212,8 @@ chunks)  # chunk sizes: stream mode for A (what made the gathered form faster?),
   done
   ;;
 e2eh)  # the engine's zero-copy strided / CSR pieces back in stream mode: engine tests, e2e A / C
-  pyt pytest_engine -m gpu -k "engine or group or slotted or chain"
-  for c in A C C2K; do
+  pyt pytest_engine -m gpu -k "engine or group or slotted or chain or ring_loop"
+  for c in ${E2E_CONFIGS:-A C C2K}; do
     timeout -k 10 300 python bench.py --e2e --config $c --steps 5 --warmup 1 >> "$out/e2e.jsonl" 2>> "$out/e2e.err"
   done
   ;;
