@@ -468,8 +468,10 @@ int aipstack_chksum_device_check(int device);
  * two checksum fields: 0 = 2-byte stores, 1 = the fields' whole 32-byte sectors from the header
  * bytes the kernel holds; -1 = the default), "chain_short" (chained batches: chunks of at most
  * this many bytes that share no 128-byte line with their neighbours in the table are read
- * first in each 64-chunk group; 0 = the table's order, -1 = the default, 128). Process-wide;
- * results never depend on them.
+ * first in each 64-chunk group; 0 = the table's order, -1 = the default, 128), "gather"
+ * (strided and CSR checksum batches: 0 = the gathered stream of the packets' segments, the
+ * default since round 4; -1 = stream mode, one contiguous run per 64-packet chunk, for
+ * packets back to back). Process-wide; results never depend on them.
  * Returns _OK or _EINVAL for an unknown key. */
 int aipstack_chksum_tune(const char *key, int value);
 

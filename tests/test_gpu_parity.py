@@ -301,6 +301,28 @@ def test_stream_mode_mixed_chunks(oracle):
     assert np.array_equal(got, want), np.nonzero(got != want)[0][:8]
 
 
+@pytest.mark.parametrize("gather", [0, -1])
+def test_strided_and_csr_in_both_read_forms(oracle, gather):
+    """The gathered stream (default) and stream mode (tunable gather = -1) give the same
+    sums on back-to-back strided and CSR batches, odd starts and lengths included."""
+    _tune("gather", gather)
+    try:
+        buf = torch.empty(1 << 22, dtype=torch.uint8, device=DEV)
+        synth.fill_device(buf, 31)
+        hb = _np(buf)
+        for plen in (1, 63, 1500, 9000):
+            n = min(3000, (buf.numel() - 3) // plen)
+            got = _np(A.chksum_batch_strided(buf, plen, plen, n, byte_offset=3))
+            assert np.array_equal(got, oracle.batch_strided(hb[3:], plen, plen, n)), plen
+        rng = np.random.default_rng(32)
+        lens = rng.integers(0, 1600, 20000)
+        off = np.concatenate([[5], 5 + np.cumsum(lens)]).astype(np.int64)
+        got = _np(A.chksum_batch_csr(buf, _d(off)))
+        assert np.array_equal(got, oracle.batch_csr(hb, off.astype(np.uint64)))
+    finally:
+        _tune("gather", 0)
+
+
 def test_overlapping_and_zero_stride(oracle):
     buf = torch.empty(70000, dtype=torch.uint8, device=DEV)
     synth.fill_device(buf, 77)
