@@ -538,8 +538,13 @@ int launch(const Desc &desc, uint64_t n, uint32_t max_len, uint16_t *d_out, uint
         // 8 242.3, 32 233.6 (profiles/r04/chunks) -- about 12 KiB per chunk, as A's 8 x 1500 B
         if (!sh.small && tuning().chunk_packets.load(std::memory_order_relaxed) == 0)
             sh.chunk_packets = Desc::kCsr ? 16 : 8;
-        const int su = tuning_stream_windows(4);
+        // 4 windows per group; 8 for fixed-length packets of 1 KiB or more (A 213.4 against
+        // 217.1 us at 4; C and C2K, mixed lengths, lose at 8: 233.3 / 267.1 against 229.9 /
+        // 243.4; profiles/r04/su8)
+        const int su = tuning_stream_windows(
+            std::is_same<Desc, GappedDesc>::value && max_len >= 1024u ? 8 : 4);
         if (su == 4) return launch_k<Desc, 1, 1, true, SEEDED, 4>(desc, n, sh, d_out, flags, stream);
+        if (su == 8) return launch_k<Desc, 1, 1, true, SEEDED, 8>(desc, n, sh, d_out, flags, stream);
         if (su != 0) return launch_k<Desc, 1, 1, true, SEEDED, 2>(desc, n, sh, d_out, flags, stream);
     }
     switch (pick_unroll(max_len)) {

@@ -249,6 +249,22 @@ slotg2)  # slotted frames' chunk size with the gathered L4 stream
       "chunk_packets=32;chunk_packets=16;chunk_packets=64;chunk_packets=8" > "$out/rx2k_sweep.jsonl" 2> "$out/rx2k_sweep.err"
   sweep tx2k --config TX2K --variants "split=0,chunk_packets=32;split=0,chunk_packets=16;split=0,chunk_packets=64;split=0,chunk_packets=8"
   ;;
+su8)  # the gathered stream at 8 windows per group (SU = 8) against 4
+  for i in 1 2 3; do
+    for c in A C C2K; do
+      bench ${c}_su4 --config $c --per-launch --no-cpu-baseline
+      AIPSTACK_CHKSUM_STREAM=8 bench ${c}_su8 --config $c --per-launch --no-cpu-baseline
+    done
+  done
+  ;;
+su8b)  # A2K and B at 8 windows (the new default for fixed lengths >= 1 KiB) against 4
+  for i in 1 2 3; do
+    for c in A2K B A; do
+      bench ${c}_su8 --config $c --per-launch --no-cpu-baseline
+      AIPSTACK_CHKSUM_STREAM=4 bench ${c}_su4 --config $c --per-launch --no-cpu-baseline
+    done
+  done
+  ;;
 kern)
   pyt pytest_kern -m gpu -k "chain or contract_violations or native_library"
   for i in 1 2 3; do
