@@ -265,6 +265,13 @@ su8b)  # A2K and B at 8 windows (the new default for fixed lengths >= 1 KiB) aga
     done
   done
   ;;
+chain8)  # chains at 8 windows per group against 4
+  pyt pytest_chain8 -m gpu -k "chain_bench_shape or chain_golden"
+  for i in 1 2 3; do
+    bench chain_su4 --config CHAIN --per-launch --no-cpu-baseline
+    AIPSTACK_CHKSUM_STREAM=8 bench chain_su8 --config CHAIN --per-launch --no-cpu-baseline
+  done
+  ;;
 kern)
   pyt pytest_kern -m gpu -k "chain or contract_violations or native_library"
   for i in 1 2 3; do
