@@ -858,7 +858,9 @@ class ChksumEngineGroup:
         return t, out
 
     def submit_csr(self, buf, offsets, *, out=None, final=False):
-        o = _host_u64(offsets)
+        # a copy: a range may be submitted later on its device's worker thread, after this
+        # returns, and must not see the caller refill its offsets (the bounds checked here)
+        o = _host_u64(offsets).copy()
         n = o.size - 1
         if n > 0 and int(o[-1]) > buf.nbytes:
             raise ValueError("offsets exceed buf")
@@ -869,7 +871,7 @@ class ChksumEngineGroup:
         return t, out
 
     def submit_rx_verify(self, frames, offsets, *, out=None):
-        o = _host_u64(offsets)
+        o = _host_u64(offsets).copy()  # (as submit_csr)
         n = o.size - 1
         if n > 0 and int(o[-1]) > frames.nbytes:
             raise ValueError("offsets exceed frames")
@@ -887,6 +889,7 @@ class ChksumEngineGroup:
 
     def submit_slotted(self, buf, slot_stride: int, lens, *, out=None, final=False):
         ln, n = ChksumEngine._slot_args(buf, slot_stride, lens)
+        ln = ln.copy()  # (as submit_csr: the lengths are read again on a worker thread)
         out = ChksumEngine._host_args(buf, out, n)
         t = self._submit("aipstack_chksum_engine_group_submit_slotted", (buf, ln, out),
                          buf.ctypes.data, slot_stride, ln.ctypes.data, n, out.ctypes.data,
@@ -895,6 +898,7 @@ class ChksumEngineGroup:
 
     def submit_rx_verify_slotted(self, frames, slot_stride: int, lens, *, out=None):
         ln, n = ChksumEngine._slot_args(frames, slot_stride, lens)
+        ln = ln.copy()  # (as submit_slotted)
         out = ChksumEngine._host_args(frames, out, n, np.uint8)
         t = self._submit("aipstack_chksum_engine_group_submit_rx_verify_slotted",
                          (frames, ln, out), frames.ctypes.data, slot_stride, ln.ctypes.data, n,
@@ -905,6 +909,7 @@ class ChksumEngineGroup:
         if not frames.flags.writeable:
             raise ValueError("frames must be writable (filled in place)")
         ln, n = ChksumEngine._slot_args(frames, slot_stride, lens)
+        ln = ln.copy()  # (as submit_slotted)
         status = ChksumEngine._host_args(frames, status, n, np.uint8)
         t = self._submit("aipstack_chksum_engine_group_submit_tx_fill_slotted",
                          (frames, ln, status), frames.ctypes.data, slot_stride, ln.ctypes.data,

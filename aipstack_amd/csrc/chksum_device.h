@@ -1131,9 +1131,16 @@ __device__ __forceinline__ uint32_t sum_gathered_chunks(uint64_t a, uint32_t l, 
 
 // Stream mode for one chunk (stream_ok). Lane j < cnt holds packet j = [S, E); returns
 // lane j's exact halves-sum (0 on lanes >= cnt).
-template <int U, bool NT>
+// SU <= 8: SU windows issued together, the next group after the current one is summed (rounds
+// 1-4). SU > 8 (round 5, the strided default): groups of SU / 2 windows, double-buffered -- the
+// next group goes out before the current one is summed, so a wave of one short chunk issues
+// all of its ~12 KiB before it sums the first window (the gathered stream's issue pattern,
+// without its per-window owner lookup and address arithmetic).
+template <int SU, bool NT>
 __device__ __forceinline__ uint32_t sum_stream_chunk(uint64_t S, uint64_t E, int lane, int cnt,
                                                      uint32_t voff) {
+    constexpr bool kDb = SU > 8 || AIPSTACK_STREAM_DB != 0;
+    constexpr int U = SU > 8 ? SU / 2 : SU;
     // X1 = end of the chunk's last packet; lanes past the batch sit at X1 (empty)
     const int lastl = cnt - 1;
     const uint64_t X1 =
@@ -1144,7 +1151,7 @@ __device__ __forceinline__ uint32_t sum_stream_chunk(uint64_t S, uint64_t E, int
         ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(S >> 32)) << 32) |
         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)S);
     // the run spans <= 64 * 2^17 + 15 bytes (stream_ok)
-    StreamRun<U, NT, U, AIPSTACK_STREAM_DB != 0> run;
+    StreamRun<U, NT, U, kDb> run;
     run.begin(S0 & ~(uint64_t)15, X1, voff);
     const uint64_t bs[1] = {S};
     uint32_t hb[1], hx;

@@ -54,6 +54,7 @@ struct Part {
     int submit_status = AIPSTACK_CHKSUM_OK;
     uint64_t eng_ticket = 0;  // the engine's ticket (0: nothing was enqueued)
     bool done = false;
+    bool waiting = false;     // a group _wait owns its engine ticket: _poll leaves it alone
     int status = AIPSTACK_CHKSUM_OK;
 };
 
@@ -154,11 +155,12 @@ int group_submit(aipstack_chksum_engine_group *g, uint64_t n, const void *span_p
     const size_t parts = (size_t)std::max<uint64_t>(
         1, std::min<uint64_t>(m, span_bytes / kSplitMin));
     const std::vector<uint64_t> cut = split(n, parts, bytes_before);
-    const bool inline_submit = span_bytes <= kInlineMax || in_group_region(g, span_p, span_bytes);
+    bool inline_submit;
     uint64_t t;
     std::vector<size_t> dev(parts);
     {
-        std::lock_guard<std::mutex> lock(g->mu);
+        std::lock_guard<std::mutex> lock(g->mu);  // (regions change under it)
+        inline_submit = span_bytes <= kInlineMax || in_group_region(g, span_p, span_bytes);
         t = g->next_ticket++;
         Batch &b = g->batches[t];
         b.parts.resize(m);
@@ -352,7 +354,7 @@ extern "C" int aipstack_chksum_engine_group_poll(aipstack_chksum_engine_group *g
     for (size_t k = 0; k < it->second.parts.size(); ++k) {
         Part &p = it->second.parts[k];
         if (!p.used || p.done) continue;
-        if (!p.submitted) {
+        if (!p.submitted || p.waiting) {  // (a wait consumes that engine ticket's result)
             pending = true;
             continue;
         }
@@ -375,17 +377,23 @@ extern "C" int aipstack_chksum_engine_group_wait(aipstack_chksum_engine_group *g
         if (it == g->batches.end())
             return ticket != 0 && ticket < g->next_ticket ? AIPSTACK_CHKSUM_OK
                                                           : AIPSTACK_CHKSUM_EINVAL;
+        // every range submitted, and none owned by another thread's wait
         g->submitted.wait(lock, [&] {
             it = g->batches.find(ticket);
             if (it == g->batches.end()) return true;
             for (const Part &p : it->second.parts)
-                if (p.used && !p.submitted) return false;
+                if (p.used && (!p.submitted || (p.waiting && !p.done))) return false;
             return true;
         });
         if (it == g->batches.end()) return AIPSTACK_CHKSUM_OK;  // completed by another thread
+        // this wait owns the open parts: a concurrent _poll treats them as pending, so an
+        // engine failure this wait consumes is reported here, once
         for (size_t k = 0; k < it->second.parts.size(); ++k) {
-            const Part &p = it->second.parts[k];
-            if (p.used && !p.done) todo.emplace_back(k, p.eng_ticket);
+            Part &p = it->second.parts[k];
+            if (p.used && !p.done) {
+                p.waiting = true;
+                todo.emplace_back(k, p.eng_ticket);
+            }
         }
     }
     std::vector<int> res(todo.size(), AIPSTACK_CHKSUM_OK);
@@ -393,13 +401,17 @@ extern "C" int aipstack_chksum_engine_group_wait(aipstack_chksum_engine_group *g
         if (todo[j].second)
             res[j] = aipstack_chksum_engine_wait(g->engines[todo[j].first], todo[j].second);
     std::lock_guard<std::mutex> lock(g->mu);
+    // still there if this wait owns a part (no one else settles it); with nothing owned (every
+    // part already done), a concurrent poll may have completed it meanwhile
     const auto it = g->batches.find(ticket);
     if (it == g->batches.end()) return AIPSTACK_CHKSUM_OK;
     for (size_t j = 0; j < todo.size(); ++j) {
         Part &p = it->second.parts[todo[j].first];
         if (!p.done) settle(p, res[j]);
     }
-    return finish_batch(g, it, dev_status);
+    const int r = finish_batch(g, it, dev_status);
+    g->submitted.notify_all();  // other waits of this ticket: it is gone now
+    return r;
 }
 
 // ---- submits ----------------------------------------------------------------------------

@@ -354,8 +354,10 @@ struct Tuning {
                                           // touched up front; else by kind of Tx launch
     std::atomic<int> tx_store{-1};        // in-place Tx fills: 0 = 2-byte field stores, 1 =
                                           // whole sectors; else the default
-    std::atomic<int> gather{0};           // -1: back-to-back strided and CSR batches in stream
-                                          // mode (rounds 1-3); else the gathered stream
+    std::atomic<int> gather{1};           // back-to-back batches: -1 stream mode with 64-packet
+                                          // chunks (rounds 1-3), 0 the gathered stream (round
+                                          // 4), 1 default (strided: short runs; CSR: gathered),
+                                          // 2 short runs for CSR too (launch_short_runs)
     std::atomic<int> chain_short{-1};      // chains: chunks of at most this many bytes first in
                                           // the gathered stream (0 = table order; measured:
                                           // CHAIN 250.0-250.6 us at 128 against 248.0-248.9,
@@ -463,13 +465,14 @@ int pick_stream_for(bool csr, const Shape &sh) {
 
 template <class Desc, int U, int P, bool NT, bool SEEDED, int SU>
 int launch_k(const Desc &desc, uint64_t n, const Shape &sh, uint16_t *d_out, uint32_t flags,
-             hipStream_t stream) {
+             hipStream_t stream, bool one_per_wave = false) {
     const uint64_t nchunks = (n + sh.chunk_packets - 1) / sh.chunk_packets;
     const int cus = device_cu_count(stream);
     if (cus <= 0) return AIPSTACK_CHKSUM_EHIP;
     uint64_t cpw = (uint64_t)tuning().chunks_per_wave.load(std::memory_order_relaxed);
-    if (cpw == 0 && !Desc::kStream && tuning().waves_per_cu.load(std::memory_order_relaxed) == 0)
-        cpw = 1;  // ring slots: one chunk per wave, the waves scheduled as CUs free up
+    if (cpw == 0 && (one_per_wave || !Desc::kStream) &&
+        tuning().waves_per_cu.load(std::memory_order_relaxed) == 0)
+        cpw = 1;  // short chunks: one per wave, the waves scheduled as CUs free up
     if (cpw == 0) {
         int wpc = tuning().waves_per_cu.load(std::memory_order_relaxed);
         if (wpc <= 0) wpc = Desc::kCsr ? 2 * kDefaultWavesPerCu : kDefaultWavesPerCu;
@@ -554,6 +557,31 @@ int launch(const Desc &desc, uint64_t n, uint32_t max_len, uint16_t *d_out, uint
         case 4: return launch_u<Desc, 4, SEEDED>(desc, n, sh, d_out, flags, stream);
     }
     return AIPSTACK_CHKSUM_EINVAL;
+}
+
+// Short runs (round 5, the default for back-to-back strided packets): stream mode on chunks of
+// about 12 KiB (8 x 1500 B; one 9000-B packet), one chunk per wave, groups of 8 windows
+// double-buffered (SU = 16), so a wave has all of its chunk's loads out before it sums the first
+// window -- the round-4 gathered stream's issue pattern at stream mode's instruction count.
+// Config A, driver protocol (--steps 20 --warmup 5): the gathered stream's higher VALU rate
+// brings a clock dip ~3 ms into a run (launches 14-45 at 250-273 us against 220 after it,
+// profiles/r05/driver); stream mode with 64-packet chunks has none but runs 233 us.
+template <class Desc, bool SEEDED>
+int launch_short_runs(const Desc &desc, uint64_t n, uint32_t len, uint16_t *d_out, uint32_t flags,
+                      hipStream_t stream) {
+    if (n == 0) return AIPSTACK_CHKSUM_OK;
+    const int cus = device_cu_count(stream);
+    if (cus <= 0) return AIPSTACK_CHKSUM_EHIP;
+    if (tuning_stream_windows(2) == 0)  // tunable stream = -1: the per-packet wave mode
+        return launch<Desc, SEEDED>(desc, n, len, d_out, flags, stream);
+    Shape sh = pick_shape(n, cus);  // (tunable chunk_packets: short runs of that many)
+    if (tuning().chunk_packets.load(std::memory_order_relaxed) == 0) {
+        if (sh.small) return launch<Desc, SEEDED>(desc, n, len, d_out, flags, stream);
+        uint32_t cp = 1;  // the largest power of two with cp * len <= 12 KiB (at least 1)
+        while (cp < (uint32_t)kWave && (uint64_t)(2 * cp) * len <= 12288u) cp <<= 1;
+        sh.chunk_packets = cp;
+    }
+    return launch_k<Desc, 1, 1, true, SEEDED, 16>(desc, n, sh, d_out, flags, stream, true);
 }
 
 template <bool NT, int SU>
@@ -651,13 +679,16 @@ int batch_strided_from(const void *d_base, uint64_t stride, uint32_t len, uint64
     // stride == len where the bytes are read over the link from host memory (the engine's
     // zero-copy pieces: A end to end 49.7 vs 48.7 GiB/s, profiles/r04/final/e2e.jsonl) or
     // when tunable "gather" = -1.
-    const bool stream_mode =
-        host_bytes || tuning().gather.load(std::memory_order_relaxed) == -1;
-    if (stride != len || !stream_mode) {
+    // Round 5: back-to-back packets in device memory take short runs (launch_short_runs);
+    // tunable "gather" 0 = the round-4 gathered stream, -1 = rounds 1-3 stream mode.
+    const int gm = tuning().gather.load(std::memory_order_relaxed);
+    if (stride != len || (!host_bytes && gm == 0)) {
         GappedDesc d{(uint64_t)(uintptr_t)d_base, stride, len};
         return launch<GappedDesc, false>(d, n, len, d_out, flags, (hipStream_t)stream);
     }
     StridedDesc d{(uint64_t)(uintptr_t)d_base, stride, len};
+    if (!host_bytes && gm != -1 && len >= 64u)
+        return launch_short_runs<StridedDesc, false>(d, n, len, d_out, flags, (hipStream_t)stream);
     return launch<StridedDesc, false>(d, n, len, d_out, flags, (hipStream_t)stream);
 }
 
@@ -670,7 +701,12 @@ int batch_csr_from(const void *d_base, const uint64_t *d_offsets, uint64_t n, ui
     // ones loop. The gathered stream (config C 231.0 us against 251.8 in stream mode), except
     // for bytes read over the link from host memory (C end to end 48.9 vs 44.9 GiB/s) or
     // with tunable "gather" = -1.
-    if (!host_bytes && tuning().gather.load(std::memory_order_relaxed) != -1) {
+    const int gm = tuning().gather.load(std::memory_order_relaxed);
+    if (!host_bytes && gm == 2) {  // short runs (launch_short_runs), 16-packet chunks at ~760 B
+        CsrDesc d{(uint64_t)(uintptr_t)d_base, d_offsets};
+        return launch_short_runs<CsrDesc, false>(d, n, 768u, d_out, flags, (hipStream_t)stream);
+    }
+    if (!host_bytes && gm != -1) {
         GatheredCsrDesc d;
         d.base = (uint64_t)(uintptr_t)d_base;
         d.offsets = d_offsets;

@@ -13,6 +13,8 @@
 #include <deque>
 #include <mutex>
 #include <thread>
+#include <memory>
+#include <type_traits>
 #include <vector>
 
 namespace aipstack_amd {
@@ -69,7 +71,10 @@ public:
             for (unsigned p = 0; p < parts; ++p) fn(p);
             return;
         }
-        Job job{[](void *f, unsigned p) { (*static_cast<F *>(f))(p); }, &fn, parts - 1};
+        // (F may deduce to an lvalue reference, possibly const: point at the object itself)
+        using Fn = std::remove_reference_t<F>;
+        Job job{[](void *f, unsigned p) { (*static_cast<Fn *>(f))(p); },
+                const_cast<void *>(static_cast<const void *>(std::addressof(fn))), parts - 1};
         {
             std::lock_guard<std::mutex> lock(mu_);
             for (unsigned p = 1; p < parts; ++p) tasks_.push_back(Task{&job, p});

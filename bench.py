@@ -134,7 +134,18 @@ def parse():
                         "(aipstack_chksum_engine_group_*; devices 0..N-1, or all "
                         "AIPSTACK_BENCH_FORCE_DEVICE), the batch split into N ranges")
     p.add_argument("--e2e-chunk-mib", type=int, default=64)
+    p.add_argument("--no-ceiling", action="store_true",
+                   help="skip the measured streaming-read ceiling (roofline.measured_peak)")
+    p.add_argument("--rotate", type=int, default=3, metavar="R",
+                   help="A, B, C, A2K: R distinct resident batches, step k reads batch k mod R "
+                        "(3 x 1.5 GB for A: no launch can find its bytes in the 256 MiB "
+                        "Infinity Cache); 1 = one batch read by every step")
     return p.parse_args()
+
+
+def rotation_count(args, layout):
+    """Batches the timed loop rotates over: the checksum batches only."""
+    return max(1, args.rotate) if layout in ("strided", "csr") else 1
 
 
 def shard_spec(config, rank, world, n=None):
@@ -185,7 +196,7 @@ def host_shard(spec):
             lib.oracle_tx_fill_batch(buf.ctypes.data, o.ctypes.data, spec["n"], st.ctypes.data)
         return buf
     host = np.empty(spec["total"], dtype=np.uint8)
-    synth.fill_host(host, synth.SEED_DATA, spec["byte_offset"])
+    synth.fill_host(host, spec.get("data_seed", synth.SEED_DATA), spec["byte_offset"])
     if spec["layout"] in ("csr", "csrslot"):
         synth.apply_classes_host(host, spec["offsets"], first_packet=spec["first_packet"])
     return host
@@ -599,20 +610,34 @@ def main():
     byte_offset = spec["byte_offset"]
     total = spec["total"]
     stride = spec.get("stride", plen)
+    # Rotation: R distinct resident batches, step k reads batch k mod R, so no
+    # launch finds the previous launch's bytes in the 256 MiB Infinity Cache. Batch r is the
+    # shard's packets over data seed SEED_DATA + r (same lengths / offsets); each is checked.
+    rot = rotation_count(args, layout)
+    bufs, outs = [], []
     if layout in ("strided", "csr"):
-        buf = torch.empty(total, dtype=torch.uint8, device=dev)
-        synth.fill_device(buf, synth.SEED_DATA, byte_offset)
-    if layout == "csr":
-        d_off = torch.from_numpy(off_host).to(dev)
-        synth.apply_classes_device(buf, d_off, first_packet=spec["first_packet"])
-    out = torch.empty(n, dtype=torch.uint16, device=dev)
+        if layout == "csr":
+            d_off = torch.from_numpy(off_host).to(dev)
+        for r in range(rot):
+            b = torch.empty(total, dtype=torch.uint8, device=dev)
+            synth.fill_device(b, synth.SEED_DATA + r, byte_offset)
+            if layout == "csr":
+                synth.apply_classes_device(b, d_off, first_packet=spec["first_packet"])
+            bufs.append(b)
+            outs.append(torch.empty(n, dtype=torch.uint16, device=dev))
+        buf = bufs[0]
+    out = outs[0] if outs else torch.empty(n, dtype=torch.uint16, device=dev)
     torch.cuda.synchronize()
+    step_no = [0]
 
     def step():
+        k = step_no[0]
+        step_no[0] = k + 1
         if layout == "strided":
-            A.chksum_batch_strided(buf, stride, plen, n, out=out, stream=stream)
+            A.chksum_batch_strided(bufs[k % rot], stride, plen, n, out=outs[k % rot],
+                                   stream=stream)
         elif layout == "csr":
-            A.chksum_batch_csr(buf, d_off, out=out, stream=stream)
+            A.chksum_batch_csr(bufs[k % rot], d_off, out=outs[k % rot], stream=stream)
         elif layout == "rx":
             A.rx_verify(buf, d_off, out=status, stream=stream)
         elif layout == "txrec":
@@ -690,6 +715,7 @@ def main():
     # oracle / the reference; then (after a barrier, so that no other rank's check competes
     # for the host cores) rank 0 times the CPU baseline on its shard
     parity = None
+    rot_parity = None
     cpu = None
     baseline = None  # rank 0's CPU baseline, run after every rank's check
     if layout in ("rx", "tx", "txrec"):
@@ -721,7 +747,19 @@ def main():
                       else chain_check(chain, out.cpu().numpy()))
         baseline = lambda: cpu_baseline_chain(chain)
     else:
+        # every rotation batch was read at least once (outside the timing if the run was
+        # shorter than the rotation), and each is checked below
+        while step_no[0] < rot:
+            step()
+        torch.cuda.synchronize()
         host_out = out.cpu().numpy()
+        rot_parity = None
+        if rot > 1 and not args.no_parity:
+            thr = max(1, _affinity_cores() // world)
+            checks = [oracle_check(dict(spec, data_seed=synth.SEED_DATA + r),
+                                   outs[r].cpu().numpy(), threads=thr) for r in range(1, rot)]
+            rot_parity = (f"rotation batches 1..{rot - 1} bit-exact" if
+                          all(c.startswith("bit-exact") for c in checks) else "MISMATCH")
         if world == 1 and not args.no_cpu_baseline:
             # one rank: the baseline's own output (the reference over the whole shard) is
             # the check
@@ -740,6 +778,9 @@ def main():
         dist.barrier()
     if rank == 0 and not args.no_cpu_baseline and baseline is not None:
         cpu = baseline()
+    if rot_parity is not None and parity is not None:
+        parity = "MISMATCH (a rotation batch)" if rot_parity == "MISMATCH" else \
+            f"{parity}; {rot_parity}"
     # which device each rank ran on, gathered on the control plane with its parity
     props = torch.cuda.get_device_properties(device)
     mine_info = {"rank": rank, "device": device,
@@ -759,6 +800,11 @@ def main():
 
     traffic, traffic_stale = _pmc_traffic(args.config)
     slot_ceiling_fields = {}
+    if layout in ("strided", "csr") and rank == 0 and not args.no_ceiling:
+        ceil = hbm_read_ceiling()
+        if ceil:
+            slot_ceiling_fields["measured_peak"] = dict(
+                ceil, frac=round(alg / avg_kernel_s / 1e9 / ceil["GBps"], 4))
     if layout in ("rxslot", "csrslot", "txslot") and rank == 0:
         ceil = slot_read_ceiling(args.config, spec)
         if ceil:
@@ -796,6 +842,10 @@ def main():
             "payload_bytes_per_gpu": payload,
             "layout": layout,
             "parallelism": f"disjoint packet shards x{world}, no collective",
+            "rotation": {"batches": rot, "resident_bytes_per_gpu": int(rot * total),
+                         "note": ("step k reads batch k mod R (data seeds 42..42+R-1), every "
+                                  "batch checked" if rot > 1 else
+                                  "one batch, read by every step")},
             **({"tx_fill": "in-place, one pass" if args.tx_inplace else
                 "split: read pass + scatter pass (both timed)"} if layout == "tx" else {}),
             **({"chain_fill": "checksum also stored big-endian into each header node"}
@@ -1172,6 +1222,21 @@ def slot_read_ceiling(config, spec):
         d = json.loads(r.stdout.strip().splitlines()[-1])
         d["source"] = "tools/build/slot_peak " + " ".join(args)
         return d
+    except (OSError, ValueError, IndexError, subprocess.SubprocessError):
+        return None
+
+
+def hbm_read_ceiling():
+    """tools/build/hbm_peak ceiling (a child process, after the timed region): the best GB/s a
+    pure 16-byte streaming read reaches on this GPU over 3 rotated 1.57 GB buffers, in the
+    kernel's own load shapes -- the measured roofline beside the 8 TB/s spec peak."""
+    import subprocess
+    exe = os.path.join(ROOT, "tools", "build", "hbm_peak")
+    if not os.path.exists(exe):
+        return None
+    try:
+        r = subprocess.run([exe, "ceiling"], capture_output=True, text=True, timeout=120)
+        return json.loads(r.stdout.strip().splitlines()[-1])
     except (OSError, ValueError, IndexError, subprocess.SubprocessError):
         return None
 

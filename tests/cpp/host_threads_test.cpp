@@ -42,6 +42,16 @@ int main() {
             for (auto &h : hit) ok &= h.load() == 1;
             EXPECT(ok, "every part once (%u workers, %u parts)", workers, parts);
         }
+        {  // a named callable (F deduces to an lvalue reference), and a const one
+            std::vector<std::atomic<int>> hit(9);
+            auto named = [&](unsigned p) { hit[p].fetch_add(1); };
+            pool.run(9, named);
+            const auto cnamed = [&](unsigned p) { hit[p].fetch_add(1); };
+            pool.run(9, cnamed);
+            bool ok = true;
+            for (auto &h : hit) ok &= h.load() == 2;
+            EXPECT(ok, "lvalue callables (%u workers)", workers);
+        }
         // several callers at once, many rounds
         std::vector<std::thread> callers;
         std::atomic<long> total{0};

@@ -301,16 +301,20 @@ def test_stream_mode_mixed_chunks(oracle):
     assert np.array_equal(got, want), np.nonzero(got != want)[0][:8]
 
 
-@pytest.mark.parametrize("gather", [0, -1])
-def test_strided_and_csr_in_both_read_forms(oracle, gather):
-    """The gathered stream (default) and stream mode (tunable gather = -1) give the same
-    sums on back-to-back strided and CSR batches, odd starts and lengths included."""
+@pytest.mark.parametrize("chunk", [0, 1, 8, 64])
+@pytest.mark.parametrize("gather", [0, -1, 1, 2])
+def test_strided_and_csr_in_every_read_form(oracle, gather, chunk):
+    """The read forms of back-to-back batches give the same sums, odd starts and lengths
+    included: short runs (gather 1, the strided default since round 5; 2 also for CSR), the
+    gathered stream (0, round 4) and stream mode with long chunks (-1). chunk_packets forces
+    the short-run shape on these small batches (0: the automatic shape)."""
     _tune("gather", gather)
+    _tune("chunk_packets", chunk)
     try:
         buf = torch.empty(1 << 22, dtype=torch.uint8, device=DEV)
         synth.fill_device(buf, 31)
         hb = _np(buf)
-        for plen in (1, 63, 1500, 9000):
+        for plen in (1, 63, 64, 1500, 1501, 9000):
             n = min(3000, (buf.numel() - 3) // plen)
             got = _np(A.chksum_batch_strided(buf, plen, plen, n, byte_offset=3))
             assert np.array_equal(got, oracle.batch_strided(hb[3:], plen, plen, n)), plen
@@ -321,7 +325,18 @@ def test_strided_and_csr_in_both_read_forms(oracle, gather):
         got = _np(A.chksum_batch_csr(buf, _d(off)))
         assert np.array_equal(got, oracle.batch_csr(hb, off.astype(np.uint64)))
     finally:
-        _tune("gather", 0)
+        _tune("gather", 1)
+        _tune("chunk_packets", 0)
+
+
+@pytest.mark.parametrize("plen,n", [(64, 300000), (1500, 270000), (9000, 40000)])
+def test_short_runs_large_batches(oracle, plen, n):
+    """Back-to-back strided batches large enough for the default short-run shape (one chunk of
+    ~12 KiB per wave, SU = 16), at an odd base, against the oracle."""
+    buf = torch.empty(n * plen + 7, dtype=torch.uint8, device=DEV)
+    synth.fill_device(buf, 41 + plen)
+    got = _np(A.chksum_batch_strided(buf, plen, plen, n, byte_offset=7, final=True))
+    assert np.array_equal(got, oracle.batch_strided(_np(buf)[7:], plen, plen, n, final=True))
 
 
 def test_overlapping_and_zero_stride(oracle):
