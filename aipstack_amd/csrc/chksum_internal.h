@@ -36,7 +36,7 @@ int tuning_tx_header_mode(int family_default);
 
 // How the in-place Tx fills store the checksum fields (frame_kernels.hip FieldSectors): the
 // tunable "tx_store" (0 = 2-byte field stores, 1 = whole sectors), else `family_default`.
-constexpr int kTxStoreFields = 0, kTxStoreSectors = 1;
+constexpr int kTxStoreFields = 0, kTxStoreSectors = 1, kTxStoreLines = 2;
 int tuning_tx_store(int family_default);
 
 // Chains: chunks of at most this many bytes are read first in a group's gathered stream

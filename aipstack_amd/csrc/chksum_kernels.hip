@@ -358,6 +358,8 @@ struct Tuning {
                                           // chunks (rounds 1-3), 0 the gathered stream (round
                                           // 4), 1 default (strided: short runs; CSR: gathered),
                                           // 2 short runs for CSR too (launch_short_runs)
+    std::atomic<int> lds_pad{0};          // bytes of dynamic LDS per batch block (occupancy
+                                          // experiments; 0 = none)
     std::atomic<int> chain_short{-1};      // chains: chunks of at most this many bytes first in
                                           // the gathered stream (0 = table order; measured:
                                           // CHAIN 250.0-250.6 us at 128 against 248.0-248.9,
@@ -399,10 +401,21 @@ Tuning &tuning() {
 
 constexpr int kDefaultWavesPerCu = 64;
 
+// The product build compiles the launch shapes the pick_* functions choose, plus the runtime
+// forms the tests exercise (stream windows 2 / 4 / 8 / off, the gathered stream's window
+// counts, chunk sizes): about 60 batch kernels. tools/build_variant.sh NAME -DAIPSTACK_ALL_VARIANTS
+// builds every U x P x NT combination as well (the "unroll", "packets" and "nontemporal"
+// tunables of tools/sweep.py; round 4's product build held all of them, 565 kernels).
+#ifdef AIPSTACK_ALL_VARIANTS
+constexpr bool kAllVariants = true;
+#else
+constexpr bool kAllVariants = false;
+#endif
+
 // U: enough segments per lane to cover a typical packet in one group.
 int pick_unroll(uint32_t max_len) {
     const int t = tuning().unroll.load(std::memory_order_relaxed);
-    if (t >= 1 && t <= 4) return t;
+    if (kAllVariants && t >= 1 && t <= 4) return t;
     const uint32_t max_seg = (max_len + 30u) / 16u;           // worst-case alignment
     const uint32_t q = (max_seg + kWave - 1) / kWave;         // groups of 64 segments
     if (q <= 1) return 1;
@@ -414,7 +427,7 @@ int pick_unroll(uint32_t max_len) {
 // P: packets whose loads a wave keeps in flight. Measured (tools/sweep.py, MI355X,
 // profiles/r01/sweep_*.jsonl): 1500 B strided best at P = 8, 9000 B at P = 1 (U = 3
 // already has 3 KiB in flight per wave), mixed 64-1500 B CSR at P = 4.
-int pick_packets(int u, bool csr) {
+[[maybe_unused]] int pick_packets(int u, bool csr) {
     const int t = tuning().packets.load(std::memory_order_relaxed);
     if (t == 1 || t == 2 || t == 4 || t == 8) return t;
     if (csr) return 4;
@@ -483,44 +496,62 @@ int launch_k(const Desc &desc, uint64_t n, const Shape &sh, uint16_t *d_out, uin
     const uint64_t waves = (nchunks + cpw - 1) / cpw;
     const uint64_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
     if (blocks > 0x7FFFFFFFull || cpw > 0xFFFFFFFFull) return AIPSTACK_CHKSUM_EINVAL;
+    // (tunable lds_pad: dynamic LDS per block, so that fewer blocks fit a CU -- occupancy
+    // experiments only; 0 by default)
+    const int pad = tuning().lds_pad.load(std::memory_order_relaxed);
     hipLaunchKernelGGL((chksum_batch_kernel<Desc, U, P, NT, SEEDED, SU>), dim3((unsigned)blocks),
-                       dim3(kBlock), 0, stream, desc, n, (uint32_t)cpw, sh.chunk_packets, d_out,
-                       flags);
+                       dim3(kBlock), (unsigned)(pad > 0 && pad <= 65536 ? pad : 0), stream, desc,
+                       n, (uint32_t)cpw, sh.chunk_packets, d_out, flags);
     return check_hip(hipGetLastError());
 }
 
 template <class Desc, int U, int P, bool SEEDED>
 int launch_s(const Desc &desc, uint64_t n, const Shape &sh, uint16_t *d_out, uint32_t flags,
              hipStream_t stream) {
-    if constexpr (!Desc::kStream)  // ring slots, per-packet wave mode (launch: gathered)
+    if constexpr (!Desc::kStream) {  // ring slots, per-packet wave mode (launch: gathered)
         return launch_k<Desc, U, P, true, SEEDED, 0>(desc, n, sh, d_out, flags, stream);
-    if (tuning().nontemporal.load(std::memory_order_relaxed) == 0)  // sweeps only
-        return launch_k<Desc, U, P, false, SEEDED, 0>(desc, n, sh, d_out, flags, stream);
-    switch (pick_stream_for(Desc::kCsr, sh)) {
-        case 0: return launch_k<Desc, U, P, true, SEEDED, 0>(desc, n, sh, d_out, flags, stream);
-        case 2: return launch_k<Desc, U, P, true, SEEDED, 2>(desc, n, sh, d_out, flags, stream);
-        case 8: return launch_k<Desc, U, P, true, SEEDED, 8>(desc, n, sh, d_out, flags, stream);
-        default: return launch_k<Desc, U, P, true, SEEDED, 4>(desc, n, sh, d_out, flags, stream);
+    } else if constexpr (!kAllVariants && std::is_same<Desc, StridedDesc>::value &&
+                         (U != 1 || P != 1)) {
+        // fixed-length packets back to back: stream mode runs at U = P = 1 (launch), so the
+        // U / P forms are the per-packet wave mode only (tunable stream = -1)
+        return launch_k<Desc, U, P, true, SEEDED, 0>(desc, n, sh, d_out, flags, stream);
+    } else {
+        if constexpr (kAllVariants) {
+            if (tuning().nontemporal.load(std::memory_order_relaxed) == 0)  // sweeps only
+                return launch_k<Desc, U, P, false, SEEDED, 0>(desc, n, sh, d_out, flags, stream);
+        }
+        switch (pick_stream_for(Desc::kCsr, sh)) {
+            case 0: return launch_k<Desc, U, P, true, SEEDED, 0>(desc, n, sh, d_out, flags, stream);
+            case 2: return launch_k<Desc, U, P, true, SEEDED, 2>(desc, n, sh, d_out, flags, stream);
+            case 8: return launch_k<Desc, U, P, true, SEEDED, 8>(desc, n, sh, d_out, flags, stream);
+            default: return launch_k<Desc, U, P, true, SEEDED, 4>(desc, n, sh, d_out, flags, stream);
+        }
     }
 }
 
 template <class Desc, int U, bool SEEDED>
 int launch_u(const Desc &desc, uint64_t n, const Shape &sh, uint16_t *d_out, uint32_t flags,
              hipStream_t stream) {
-    int p = pick_packets(U, Desc::kCsr);
-    // Every chunk takes stream mode: the per-packet path is never run, so give it the
-    // fewest registers (the kernel's occupancy is set by the larger of the two paths).
-    if (Desc::kStream && desc.back_to_back() && pick_stream_for(Desc::kCsr, sh) > 0 &&
-        tuning().nontemporal.load(std::memory_order_relaxed) != 0 &&
-        tuning().packets.load(std::memory_order_relaxed) == 0)
-        p = 1;
-    switch (p) {
-        case 1: return launch_s<Desc, U, 1, SEEDED>(desc, n, sh, d_out, flags, stream);
-        case 2: return launch_s<Desc, U, 2, SEEDED>(desc, n, sh, d_out, flags, stream);
-        case 4: return launch_s<Desc, U, 4, SEEDED>(desc, n, sh, d_out, flags, stream);
-        case 8: return launch_s<Desc, U, 8, SEEDED>(desc, n, sh, d_out, flags, stream);
+    if constexpr (!kAllVariants) {
+        // P for this U: pick_packets' measured choice, except P = 4 for U <= 2 where it took 8
+        // (the per-packet wave mode is a fallback since round 4 -- tunable stream = -1 -- and
+        // at P = 8 it spilled 62-65 SGPRs)
+        return launch_s<Desc, U, (Desc::kCsr || U <= 2) ? 4 : 1, SEEDED>(desc, n, sh, d_out,
+                                                                        flags, stream);
+    } else {
+        int p = pick_packets(U, Desc::kCsr);
+        if (Desc::kStream && desc.back_to_back() && pick_stream_for(Desc::kCsr, sh) > 0 &&
+            tuning().nontemporal.load(std::memory_order_relaxed) != 0 &&
+            tuning().packets.load(std::memory_order_relaxed) == 0)
+            p = 1;
+        switch (p) {
+            case 1: return launch_s<Desc, U, 1, SEEDED>(desc, n, sh, d_out, flags, stream);
+            case 2: return launch_s<Desc, U, 2, SEEDED>(desc, n, sh, d_out, flags, stream);
+            case 4: return launch_s<Desc, U, 4, SEEDED>(desc, n, sh, d_out, flags, stream);
+            case 8: return launch_s<Desc, U, 8, SEEDED>(desc, n, sh, d_out, flags, stream);
+        }
+        return AIPSTACK_CHKSUM_EINVAL;
     }
-    return AIPSTACK_CHKSUM_EINVAL;
 }
 
 template <class Desc, bool SEEDED>
@@ -550,13 +581,28 @@ int launch(const Desc &desc, uint64_t n, uint32_t max_len, uint16_t *d_out, uint
         if (su == 8) return launch_k<Desc, 1, 1, true, SEEDED, 8>(desc, n, sh, d_out, flags, stream);
         if (su != 0) return launch_k<Desc, 1, 1, true, SEEDED, 2>(desc, n, sh, d_out, flags, stream);
     }
-    switch (pick_unroll(max_len)) {
-        case 1: return launch_u<Desc, 1, SEEDED>(desc, n, sh, d_out, flags, stream);
-        case 2: return launch_u<Desc, 2, SEEDED>(desc, n, sh, d_out, flags, stream);
-        case 3: return launch_u<Desc, 3, SEEDED>(desc, n, sh, d_out, flags, stream);
-        case 4: return launch_u<Desc, 4, SEEDED>(desc, n, sh, d_out, flags, stream);
+    if constexpr (!kAllVariants && std::is_same<Desc, StridedDesc>::value) {
+        // Every chunk takes stream mode: the per-packet path never runs, so it is built with the
+        // fewest registers (U = P = 1; the kernel's occupancy is set by the larger path).
+        if (desc.back_to_back() && pick_stream_for(false, sh) > 0)
+            return launch_s<Desc, 1, 1, SEEDED>(desc, n, sh, d_out, flags, stream);
     }
-    return AIPSTACK_CHKSUM_EINVAL;
+    if constexpr (!kAllVariants && Desc::kCsr) {
+        // CSR entry points pass max_len 1500: U = 2 (pick_unroll)
+        return launch_u<Desc, 2, SEEDED>(desc, n, sh, d_out, flags, stream);
+    } else if constexpr (!kAllVariants && std::is_base_of<SlottedDesc, Desc>::value) {
+        // ring slots pass max_len <= 2000: U <= 2 (batch_slotted_from)
+        if (pick_unroll(max_len) <= 1) return launch_u<Desc, 1, SEEDED>(desc, n, sh, d_out, flags, stream);
+        return launch_u<Desc, 2, SEEDED>(desc, n, sh, d_out, flags, stream);
+    } else {
+        switch (pick_unroll(max_len)) {
+            case 1: return launch_u<Desc, 1, SEEDED>(desc, n, sh, d_out, flags, stream);
+            case 2: return launch_u<Desc, 2, SEEDED>(desc, n, sh, d_out, flags, stream);
+            case 3: return launch_u<Desc, 3, SEEDED>(desc, n, sh, d_out, flags, stream);
+            case 4: return launch_u<Desc, 4, SEEDED>(desc, n, sh, d_out, flags, stream);
+        }
+        return AIPSTACK_CHKSUM_EINVAL;
+    }
 }
 
 // Short runs (round 5, the default for back-to-back strided packets): stream mode on chunks of
@@ -655,7 +701,8 @@ int tuning_chain_short() {
 
 int tuning_tx_store(int family_default) {
     const int t = tuning().tx_store.load(std::memory_order_relaxed);
-    return (t == kTxStoreFields || t == kTxStoreSectors) ? t : family_default;
+    return (t == kTxStoreFields || t == kTxStoreSectors || t == kTxStoreLines) ? t
+                                                                                : family_default;
 }
 
 int tuning_frames_in_flight() {
@@ -782,16 +829,19 @@ extern "C" int aipstack_chksum_tune(const char *key, int value) {
     Tuning &t = tuning();
     if (!std::strcmp(key, "waves_per_cu")) t.waves_per_cu = value;
     else if (!std::strcmp(key, "chunks_per_wave")) t.chunks_per_wave = value;
-    else if (!std::strcmp(key, "unroll")) t.unroll = value;
-    else if (!std::strcmp(key, "packets")) t.packets = value;
-    else if (!std::strcmp(key, "nontemporal")) t.nontemporal = value;
-    else if (!std::strcmp(key, "frames")) t.frames = value;
+    // sweep-only tunables: their non-default values need a -DAIPSTACK_ALL_VARIANTS build
+    else if (!std::strcmp(key, "unroll") && (kAllVariants || value == 0)) t.unroll = value;
+    else if (!std::strcmp(key, "packets") && (kAllVariants || value == 0)) t.packets = value;
+    else if (!std::strcmp(key, "nontemporal") && (kAllVariants || value == 1)) t.nontemporal = value;
+    else if (!std::strcmp(key, "frames") && (kAllVariants || value == 0 || value == 4))
+        t.frames = value;
     else if (!std::strcmp(key, "stream")) t.stream = value;
     else if (!std::strcmp(key, "chunk_packets")) t.chunk_packets = value;
     else if (!std::strcmp(key, "tx_gather")) t.tx_gather = value;
     else if (!std::strcmp(key, "tx_store")) t.tx_store = value;
     else if (!std::strcmp(key, "chain_short")) t.chain_short = value;
     else if (!std::strcmp(key, "gather")) t.gather = value;
+    else if (!std::strcmp(key, "lds_pad")) t.lds_pad = value;
     else if (!std::strcmp(key, "engine_zero_copy")) t.engine_zero_copy = value;
     else if (!std::strcmp(key, "engine_zero_copy_small")) t.engine_zero_copy_small = value;
     else if (!std::strcmp(key, "engine_pageable_rows")) t.engine_pageable_rows = value;
@@ -820,7 +870,8 @@ int chain_batch(const uint64_t *d_chunk_addr, const uint32_t *d_chunk_len,
 #define AIPSTACK_LAUNCH_CHAIN(NT, SU)                                                       \
     return launch_chain<NT, SU>(d_chunk_addr, d_chunk_len, d_chunk_index, d_states, d_fields, \
                                 n, d_out, flags, (hipStream_t)stream)
-    if (!tuning().nontemporal.load(std::memory_order_relaxed)) AIPSTACK_LAUNCH_CHAIN(false, 2);
+    if constexpr (kAllVariants)
+        if (!tuning().nontemporal.load(std::memory_order_relaxed)) AIPSTACK_LAUNCH_CHAIN(false, 2);
     // 4 windows in flight (round 4, once the SU = 4 kernel no longer spilled): CHAIN 242.0-242.4
     // against 248.3-248.4 us with 2, alternating processes (profiles/r04/calib)
     if (tuning_stream_windows(4) == 2) AIPSTACK_LAUNCH_CHAIN(true, 2);

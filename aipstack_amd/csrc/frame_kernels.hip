@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 #include "aipstack_amd/chksum.h"
 #include "chksum_device.h"
@@ -549,11 +550,12 @@ __device__ __forceinline__ FieldSectors pick_sectors(const u32x4 (&seg)[kHdrSegs
 //                field, so that the in-place field stores find those lines in the caches
 //                (split fill 168 vs 178 us, one pass 174 vs 186).
 constexpr int kHdrLoads = 0, kHdrCapture = 1, kHdrCaptureTouch = 2;
-template <class Desc, bool TX, int U, int P, bool NT, int SU, int GATHER, bool SECT>
+template <class Desc, bool TX, int U, int P, bool NT, int SU, int GATHER, int STORE>
 __device__ __forceinline__ FrameOut process_chunk(const Desc &desc, uint64_t p0, uint64_t n,
                                                   uint32_t cpk, int lane, uint32_t voff,
                                                   uint32_t not_lane0, FrameLds *lds,
-                                                  GatherLds *glds, int &cnt_out) {
+                                                  GatherLds *glds, u32x4 *lines, int &cnt_out) {
+    constexpr bool SECT = STORE == kTxStoreSectors;
     const int cnt = (int)min((uint64_t)cpk, n - p0);
     // the chunk's own table entries only (lanes past it re-read entry p0 + cnt)
     const auto chunk = desc.begin_chunk(p0, p0 + (uint64_t)cnt, lane);
@@ -749,6 +751,12 @@ __device__ __forceinline__ FrameOut process_chunk(const Desc &desc, uint64_t p0,
     }
     if (!streamed) {
         if (!have_headers) load_headers();
+        if constexpr (STORE == kTxStoreLines) {
+            // line stores: this lane's first 128 bytes (its header blocks: A0 = S on a
+            // 128-byte-aligned slot) kept in LDS until the checksums are known
+#pragma unroll
+            for (int i = 0; i < kHdrSegs; ++i) lines[lane * kHdrSegs + i] = seg[i];
+        }
         fl = parse_lane<TX, false>(seg, S, len, hb_end);
         // sector stores: ring slots (this is their only path), not the rare CSR chunks that
         // are not back to back (16 more VGPRs through the per-frame loop)
@@ -795,7 +803,58 @@ __device__ __forceinline__ FrameOut process_chunk(const Desc &desc, uint64_t p0,
 #ifndef AIPSTACK_FRAME_WAVES_PER_SIMD  // occupancy the register budget is fitted to
 #define AIPSTACK_FRAME_WAVES_PER_SIMD 4
 #endif
-template <class Desc, bool TX, int U, int P, bool NT, int SU, bool SPLIT, int GATHER, bool SECT>
+// Line stores (round 5, the send ring's in-place fill, tx_store = 2): a 2-byte field store
+// leaves a partly written line that the memory side merges with the bytes around it (TX2K:
+// ~49 us of its 170 for 2 M field stores, WRITE_SIZE ~52 B per frame). On a ring of slots
+// that start on 128-byte boundaries, a frame's first line [S, S + 128) is its own and holds
+// both fields of a 20-byte IPv4 header (bytes 24 and 36 / 40 / 50); the kernel loaded it
+// whole for the parse. It is kept in LDS, the fields are patched in there, and the line is
+// written back whole: eight lanes store one frame's line as 8 x 16 contiguous bytes in one
+// wave instruction. Bytes of the line past a short frame are the slot's own slack, rewritten
+// with the values just read. A field past byte 127 (IPv4 options) keeps its 2-byte store.
+__device__ __forceinline__ void store_frame_lines(const FrameOut &o, uint32_t fld_line_ok,
+                                                 uint64_t slot0, uint64_t stride, int cnt,
+                                                 int lane, u32x4 *lines,
+                                                 uint8_t *__restrict__ status, uint64_t i) {
+    const bool act = lane < cnt;
+    const bool wi = act && (o.w1 & 0x100u) != 0, wl = act && (o.w1 & 0x200u) != 0;
+    const uint32_t fld = o.w1 & 0xFFu;
+    typedef __attribute__((address_space(3))) uint16_t lds16;
+    lds16 *lb = reinterpret_cast<lds16 *>(reinterpret_cast<uintptr_t>(lines)) +
+                (uint32_t)lane * (kHdrSegs * 8u);
+    const bool l_in = wl && fld + 2u <= 16u * kHdrSegs && fld_line_ok;
+    if (wi && fld_line_ok) lb[12] = (uint16_t)bswap16(o.w0);  // byte 24
+    if (l_in) lb[fld >> 1] = (uint16_t)bswap16(o.w0 >> 16);    // (fld is even)
+    if (act) status[i] = (uint8_t)(o.w1 >> 16);
+    if (!fld_line_ok) {  // slots off the 128-byte grid: the 2-byte stores
+        if (wi) store_be16(o.S + 24, o.w0);
+        if (wl) store_be16(o.S + fld, o.w0 >> 16);
+        return;
+    }
+    if (wl && !l_in) store_be16(o.S + fld, o.w0 >> 16);
+    const bool mine = wi || wl;  // this frame's line is written
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t sub = (uint32_t)lane & 7u;
+    for (int f0 = 0; f0 < cnt; f0 += 8) {
+        const int f = f0 + (lane >> 3);
+        const int src = f < kWave ? f : 0;
+        const bool w = __builtin_amdgcn_ds_bpermute(src << 2, mine ? 1 : 0) != 0;
+        if (f < cnt && w) {
+            const u32x4 x = lines[f * kHdrSegs + sub];
+            *reinterpret_cast<u32x4 *>(slot0 + (uint64_t)f * stride + 16u * sub) = x;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
+// The classic kernel: a wave walks its chunks and stores each chunk's results right after
+// it. SPLIT (Tx only): lane j writes frame j's record (w0 | w1 << 32) to a workspace
+// instead, and tx_scatter_kernel stores the fields after the whole read pass.
+#ifndef AIPSTACK_FRAME_WAVES_PER_SIMD  // occupancy the register budget is fitted to
+#define AIPSTACK_FRAME_WAVES_PER_SIMD 4
+#endif
+template <class Desc, bool TX, int U, int P, bool NT, int SU, bool SPLIT, int GATHER, int STORE>
 __global__ __launch_bounds__(kBlock, AIPSTACK_FRAME_WAVES_PER_SIMD) void frame_kernel(Desc desc, uint64_t n,
                                                        uint32_t chunks_per_wave,
                                                        uint32_t chunk_packets,
@@ -816,19 +875,27 @@ __global__ __launch_bounds__(kBlock, AIPSTACK_FRAME_WAVES_PER_SIMD) void frame_k
     constexpr bool kSlotGather = !Desc::kStream && AIPSTACK_FRAME_SLOT_GATHER && Desc::kEdge;
     __shared__ GatherLds glds[kSlotGather ? kWavesPerBlock : 1];  // ring slots' L4 stream
     GatherLds *mg = &glds[kSlotGather ? wave_in_block : 0];
+    constexpr bool kLines = STORE == kTxStoreLines;  // ring slots only (launch_frames_slotted_d)
+    __shared__ u32x4 line_lds[kLines ? kWavesPerBlock * kWave * kHdrSegs : 1];  // 8 KiB per wave
+    u32x4 *ml = &line_lds[kLines ? wave_in_block * kWave * kHdrSegs : 0];
     for (; c < c_end; ++c) {
         const uint64_t p0 = c * cpk;
         int cnt;
-        const FrameOut o = process_chunk<Desc, TX, U, P, NT, SU, GATHER, SECT>(
-            desc, p0, n, (uint32_t)cpk, lane, voff, not_lane0, my, mg, cnt);
-        if (lane < cnt) {
+        const FrameOut o = process_chunk<Desc, TX, U, P, NT, SU, GATHER, STORE>(
+            desc, p0, n, (uint32_t)cpk, lane, voff, not_lane0, my, mg, ml, cnt);
+        if constexpr (kLines && !Desc::kStream) {
+            const uint64_t slot0 = desc.begin_chunk(p0, p0, lane).s0;
+            const bool grid = ((slot0 | desc.stride) & 127u) == 0;  // wave-uniform
+            store_frame_lines(o, grid ? 1u : 0u, slot0, desc.stride, cnt, lane, ml, status,
+                              p0 + lane);
+        } else if (lane < cnt) {
             if constexpr (SPLIT)
 #if AIPSTACK_EXP_NO_RECORDS  // experiment: price of the record stores (wrong output)
                 asm volatile("" ::"v"(o.w0), "v"(o.w1));
 #else
                 records[p0 + lane] = (uint64_t)o.w0 | (uint64_t)o.w1 << 32;
 #endif
-            else if constexpr (SECT)
+            else if constexpr (STORE == kTxStoreSectors)
                 store_frame_sectors(o.S, o.w0, o.w1, o.fs, status, p0 + lane);
             else
                 store_frame<TX>(o.S, o.w0, o.w1, status, p0 + lane);
@@ -836,7 +903,7 @@ __global__ __launch_bounds__(kBlock, AIPSTACK_FRAME_WAVES_PER_SIMD) void frame_k
     }
 }
 
-template <class Desc, bool TX, bool SPLIT, int GATHER, bool SECT = false>
+template <class Desc, bool TX, bool SPLIT, int GATHER, int STORE = kTxStoreFields>
 int launch_frames_g(const Desc &desc, uint64_t n, uint8_t *d_status, uint64_t *d_records,
                     hipStream_t stream, int cus) {
     // small batches: fewer frames per chunk, so that they spread over many waves (as the
@@ -863,7 +930,7 @@ int launch_frames_g(const Desc &desc, uint64_t n, uint8_t *d_status, uint64_t *d
     if (blocks > 0x7FFFFFFFull || cpw > 0xFFFFFFFFull) return AIPSTACK_CHKSUM_EINVAL;
 #define AIPSTACK_LAUNCH_FRAMES(P, SU)                                                          \
     hipLaunchKernelGGL((frame_kernel<Desc, TX, 2, P, AIPSTACK_FRAME_NT != 0, SU, SPLIT, GATHER,  \
-                                     SECT>),                                                     \
+                                     STORE>),                                                    \
                        dim3((unsigned)blocks), dim3(kBlock), 0, stream, desc, n, (uint32_t)cpw, \
                        cpk, d_status, d_records)
 #define AIPSTACK_LAUNCH_FRAMES_SU(P)                  \
@@ -877,11 +944,15 @@ int launch_frames_g(const Desc &desc, uint64_t n, uint8_t *d_status, uint64_t *d
             default: AIPSTACK_LAUNCH_FRAMES(P, 4);     \
         }                                             \
     }
+#ifdef AIPSTACK_ALL_VARIANTS  // frames in flight 2 / 8: sweep builds only (tools/build_variant.sh)
     switch (tuning_frames_in_flight()) {
         case 2: AIPSTACK_LAUNCH_FRAMES_SU(2); break;
         case 8: AIPSTACK_LAUNCH_FRAMES_SU(8); break;
         default: AIPSTACK_LAUNCH_FRAMES_SU(4);
     }
+#else
+    AIPSTACK_LAUNCH_FRAMES_SU(4);
+#endif
 #undef AIPSTACK_LAUNCH_FRAMES_SU
 #undef AIPSTACK_LAUNCH_FRAMES
     return check_hip(hipGetLastError());
@@ -904,10 +975,10 @@ int launch_frames(const void *d_base, const uint64_t *d_offsets, uint64_t n, uin
       if (tuning_tx_store(kTxStoreDefault) == kTxStoreSectors) {
         // whole sectors need no line in the caches: captured headers, no touches by default
         if (tuning_tx_header_mode(kHdrCapture) == kHdrCaptureTouch)
-            st = launch_frames_g<CsrDesc, true, false, kHdrCaptureTouch, true>(
+            st = launch_frames_g<CsrDesc, true, false, kHdrCaptureTouch, kTxStoreSectors>(
                 desc, n, d_status, d_records, stream, cus);
         else
-            st = launch_frames_g<CsrDesc, true, false, kHdrCapture, true>(
+            st = launch_frames_g<CsrDesc, true, false, kHdrCapture, kTxStoreSectors>(
                 desc, n, d_status, d_records, stream, cus);
         return st;
       }
@@ -948,9 +1019,15 @@ template <bool TX, bool SPLIT, class D>
 int launch_frames_slotted_d(const D &desc, uint64_t n, uint8_t *d_status, uint64_t *d_records,
                             hipStream_t stream, int cus) {
     if constexpr (TX && !SPLIT) {
-        if (tuning_tx_store(kTxStoreDefault) == kTxStoreSectors)
-            return launch_frames_g<D, true, false, kHdrLoads, true>(desc, n, d_status, d_records,
-                                                                  stream, cus);
+        const int ts = tuning_tx_store(kTxStoreDefault);
+        if (ts == kTxStoreSectors)
+            return launch_frames_g<D, true, false, kHdrLoads, kTxStoreSectors>(
+                desc, n, d_status, d_records, stream, cus);
+        // line stores: device-memory rings (over the link a line store is no cheaper)
+        if constexpr (!std::is_same<D, SlottedHostDesc>::value)
+            if (ts == kTxStoreLines)
+                return launch_frames_g<D, true, false, kHdrLoads, kTxStoreLines>(
+                    desc, n, d_status, d_records, stream, cus);
     }
     return launch_frames_g<D, TX, SPLIT, kHdrLoads>(desc, n, d_status, d_records, stream, cus);
 }

@@ -13,9 +13,14 @@
 //   6. _wait does not hold the engine while it waits: _poll from another thread returns
 //   7. a submit waiting for a busy slot (back-pressure) does not hold the engine either: _poll
 //      of an earlier batch from another thread answers at once (round 4)
-//   8. an engine group (two engines on device 0): a group ticket with one failing device
-//      reports that device's failure (dev_status) and the other's results are exact; group
-//      tickets in flight completed out of order; the group's own destroy with a batch pending
+//   8. an engine group (two engines: on devices 0 and 0, or on the devices listed in
+//      AIPSTACK_FAULT_GROUP_DEVICES, e.g. "0,1" on a box with two GPUs): a group ticket with one
+//      failing device reports that device's failure (dev_status) and the other's results are
+//      exact; group tickets in flight completed out of order; the group's own destroy with a
+//      batch pending
+//   9. the same group, _wait and _poll of one failing ticket from two threads: while the wait
+//      owns the ticket the poll answers "pending", and the failure is reported once, by the
+//      wait
 // Needs a GPU (exit 3 without one). Exit 0 = pass.
 #include <atomic>
 #include <chrono>
@@ -243,8 +248,16 @@ void poll_answers_while_submit_is_back_pressured() {
     aipstack_chksum_engine_destroy(e);
 }
 
+// The group's two devices: AIPSTACK_FAULT_GROUP_DEVICES ("a,b"), else device 0 twice.
+void group_devices(int (&devs)[2]) {
+    devs[0] = devs[1] = 0;
+    if (const char *s = std::getenv("AIPSTACK_FAULT_GROUP_DEVICES"))
+        if (std::sscanf(s, "%d,%d", &devs[0], &devs[1]) != 2) devs[0] = devs[1] = 0;
+}
+
 void group_ticket_with_one_failing_device() {
-    const int devs[2] = {0, 0};
+    int devs[2];
+    group_devices(devs);
     aipstack_chksum_engine_group *g = nullptr;
     EXPECT(aipstack_chksum_engine_group_create(devs, 2, kChunk, kStreams, &g) == 0, "group create");
     if (!g) return;
@@ -290,6 +303,40 @@ void group_ticket_with_one_failing_device() {
     EXPECT(oa2 == want_a, "group destroy completes the pending batch");
 }
 
+void group_wait_and_poll_of_one_ticket() {
+    int devs[2];
+    group_devices(devs);
+    aipstack_chksum_engine_group *g = nullptr;
+    EXPECT(aipstack_chksum_engine_group_create(devs, 2, kChunk, kStreams, &g) == 0, "group create");
+    if (!g) return;
+    const uint64_t n = 8000;  // 12 MB: split over both engines
+    std::vector<unsigned char> a(n * kLen);
+    aipstack_synth_fill_host(a.data(), a.size(), 24, 0);
+    std::vector<uint16_t> oa(n);
+    aipstack_chksum_engine_test_inject_only(aipstack_chksum_engine_group_engine(g, 1));
+    aipstack_chksum_engine_test_inject(0, bit(1));  // engine 1's first piece fails
+    aipstack_chksum_engine_test_wait_delay(200000);  // the wait sleeps 200 ms before it waits
+    uint64_t t = 0;
+    EXPECT(aipstack_chksum_engine_group_submit_strided(g, a.data(), kLen, kLen, n, oa.data(), 0,
+                                                       &t) == 0, "group submit");
+    int ds_w[2] = {-100, -100};
+    std::atomic<int> w{1};
+    std::thread waiter([&] { w = aipstack_chksum_engine_group_wait(g, t, ds_w); });
+    std::this_thread::sleep_for(std::chrono::milliseconds(50));
+    int ds_p[2] = {-100, -100};
+    const int p_during = aipstack_chksum_engine_group_poll(g, t, ds_p);
+    waiter.join();
+    const int p_after = aipstack_chksum_engine_group_poll(g, t, ds_p);
+    aipstack_chksum_engine_test_wait_delay(0);
+    aipstack_chksum_engine_test_inject(0, 0);
+    aipstack_chksum_engine_test_inject_only(nullptr);
+    EXPECT(p_during == 1, "a poll while the wait owns the ticket answers pending (%d)", p_during);
+    EXPECT(w.load() < 0 && ds_w[0] == 0 && ds_w[1] < 0,
+           "the wait reports device 1's failure (%d; %d / %d)", w.load(), ds_w[0], ds_w[1]);
+    EXPECT(p_after == 0, "the completed ticket polls OK afterwards (%d)", p_after);
+    aipstack_chksum_engine_group_destroy(g);
+}
+
 }  // namespace
 
 int main() {
@@ -305,6 +352,7 @@ int main() {
     wait_does_not_hold_the_engine();
     poll_answers_while_submit_is_back_pressured();
     group_ticket_with_one_failing_device();
+    group_wait_and_poll_of_one_ticket();
     if (failures) std::fprintf(stderr, "%d failures\n", failures);
     else std::printf("engine_fault_test: OK\n");
     std::fflush(nullptr);

@@ -143,7 +143,9 @@ def test_random_frames(oracle, seed):
     fr, off = synth.frames_host(n, seed=4000 + seed, max_payload=int(rng.choice([0, 46, 600, 1460, 8000])))
     want = fr.copy()
     want_st = oracle.tx_fill_batch(want, off)
-    store = int(rng.integers(0, 2))  # in-place field stores: 2-byte (0) or whole sectors (1)
+    # in-place field stores: 2-byte (0), whole sectors (1), whole lines (2: ring slots on the
+    # 128-byte grid; elsewhere the 2-byte stores)
+    store = int(rng.integers(0, 3))
     _tune("tx_store", store)
     try:
         for split in (False, True):

@@ -53,6 +53,34 @@ short)  # round-5 short runs (gather 1, the strided default) vs the round-4 gath
       -k "every_read_form or short_runs or full_size or config_d or stream_mode or ragged or lengths" \
       > "$out/pytest.log" 2>&1
   ;;
+shape)  # A's loaders at steady state, interleaved in one process (tools/ab.py), occupancy via
+        # lds_pad; their instruction mix; TX2K's line stores (tx_store 2) against 2-byte stores
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+      -k "slotted_tx or tx_line or random_frames or every_read_form or short_runs" \
+      > "$out/pytest.log" 2>&1
+  timeout -k 10 300 python3 tools/ab.py --config A --variants \
+      "gather=0;gather=1;gather=1,lds_pad=33792;gather=1,lds_pad=41984;gather=0,lds_pad=33000;gather=1,chunk_packets=4;gather=1,chunk_packets=16;gather=-1" \
+      > "$out/ab_A.jsonl" 2> "$out/ab_A.err"
+  for g in 0 1; do
+    AIPSTACK_CHKSUM_GATHER=$g timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv \
+        -d "$out/pmc_A_g$g" -o run --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD \
+        SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES -- python3 bench.py --config A \
+        --no-cpu-baseline --no-parity --no-ceiling --steps 5 --warmup 2 > "$out/pmc_A_g$g.log" 2>&1
+  done
+  for i in 1 2; do
+    for st in 0 2; do
+      AIPSTACK_CHKSUM_TX_STORE=$st bench TX2K_st$st --config TX2K --steps 20 --warmup 5 --per-launch --no-cpu-baseline
+    done
+  done
+  for st in 0 2; do
+    AIPSTACK_CHKSUM_TX_STORE=$st timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv \
+        -d "$out/pmc_TX2K_st$st" -o run --pmc WRITE_SIZE GRBM_GUI_ACTIVE -- python3 bench.py \
+        --config TX2K --no-cpu-baseline --no-parity --steps 5 --warmup 2 > "$out/pmc_TX2K_st$st.log" 2>&1
+    AIPSTACK_CHKSUM_TX_STORE=$st timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv \
+        -d "$out/pmcf_TX2K_st$st" -o run --pmc FETCH_SIZE -- python3 bench.py \
+        --config TX2K --no-cpu-baseline --no-parity --steps 5 --warmup 2 > "$out/pmcf_TX2K_st$st.log" 2>&1
+  done
+  ;;
 *)
   echo "unknown mode $mode"; exit 2 ;;
 esac
