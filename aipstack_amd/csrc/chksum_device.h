@@ -742,13 +742,27 @@ struct NoStreamHook {
 #ifndef AIPSTACK_STREAM_DB  // the checksum batches' stream mode with DB (A/B build switch;
 #define AIPSTACK_STREAM_DB 0  // round 4: A 233.2 vs 233.6 us, so off)
 #endif
-template <int U, bool NT, int PRE = U, bool DB = false>
+// GL (round 5, the short runs' experiment switch): global_load_dwordx4 from the wave-uniform
+// run start plus a 32-bit lane offset (the gathered stream's load form) instead of a buffer
+// descriptor; segments past the run re-read its last segment and are summed as 0.
+template <int U, bool NT, int PRE = U, bool DB = false, bool GL = false>
 struct StreamRun {
     uint64_t A, X1;
     uint32_t nseg, nwin;
     __amdgpu_buffer_rsrc_t rsrc;
     u32x4 v[U];
     u32x4 v2[DB ? U : 1];
+
+    __device__ __forceinline__ u32x4 load_win(uint32_t voff, uint32_t w) const {
+        if constexpr (GL) {
+            const uint32_t k = min(w * 64u + (voff >> 4), nseg - 1u);
+            typedef __attribute__((address_space(1))) const u32x4 gseg;
+            const gseg *p = (const gseg *)(A + 16ull * k);
+            return NT ? __builtin_nontemporal_load(p) : *p;
+        } else {
+            return load_segment<NT>(rsrc, voff, w * 1024u);
+        }
+    }
 
     // Issues windows [0, PRE) now (the rest of the first U when prefixes() starts): a
     // kernel that overlaps begin() with register-hungry work keeps only PRE in flight.
@@ -769,7 +783,7 @@ struct StreamRun {
     __device__ __forceinline__ void issue(uint32_t w, uint32_t voff) {
 #pragma unroll
         for (int u = U0; u < U1; ++u) {
-            v[u] = load_segment<NT>(rsrc, voff, (w + (uint32_t)u) * 1024u);
+            v[u] = load_win(voff, w + (uint32_t)u);
             __builtin_amdgcn_sched_barrier(0);
         }
     }
@@ -777,7 +791,7 @@ struct StreamRun {
     __device__ __forceinline__ void issue_into(u32x4 (&dst)[N], uint32_t w, uint32_t voff) {
 #pragma unroll
         for (int u = 0; u < N; ++u) {
-            dst[u] = load_segment<NT>(rsrc, voff, (w + (uint32_t)u) * 1024u);
+            dst[u] = load_win(voff, w + (uint32_t)u);
             __builtin_amdgcn_sched_barrier(0);
         }
     }
@@ -822,8 +836,10 @@ struct StreamRun {
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const uint32_t wu = w + (uint32_t)u;
-                const uint32_t s =
+                uint32_t s =
                     halves(vv[u][0], halves(vv[u][1], halves(vv[u][2], halves(vv[u][3], 0u))));
+                if constexpr (GL)  // past the run: a re-read of its last segment, counted 0
+                    s = wu * 64u + (voff >> 4) < nseg ? s : 0u;
                 const uint32_t incl = wave_incl_scan(s);
                 const uint32_t excl = incl - s;
 #pragma unroll
@@ -1140,7 +1156,8 @@ template <int SU, bool NT>
 __device__ __forceinline__ uint32_t sum_stream_chunk(uint64_t S, uint64_t E, int lane, int cnt,
                                                      uint32_t voff) {
     constexpr bool kDb = SU > 8 || AIPSTACK_STREAM_DB != 0;
-    constexpr int U = SU > 8 ? SU / 2 : SU;
+    constexpr int U = SU > 8 ? 8 : SU;
+    constexpr bool kGl = SU == 32;  // (SU 32: SU 16 through global loads, StreamRun GL)
     // X1 = end of the chunk's last packet; lanes past the batch sit at X1 (empty)
     const int lastl = cnt - 1;
     const uint64_t X1 =
@@ -1151,7 +1168,7 @@ __device__ __forceinline__ uint32_t sum_stream_chunk(uint64_t S, uint64_t E, int
         ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(S >> 32)) << 32) |
         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)S);
     // the run spans <= 64 * 2^17 + 15 bytes (stream_ok)
-    StreamRun<U, NT, U, kDb> run;
+    StreamRun<U, NT, U, kDb, kGl> run;
     run.begin(S0 & ~(uint64_t)15, X1, voff);
     const uint64_t bs[1] = {S};
     uint32_t hb[1], hx;

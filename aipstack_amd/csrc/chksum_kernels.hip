@@ -358,6 +358,7 @@ struct Tuning {
                                           // chunks (rounds 1-3), 0 the gathered stream (round
                                           // 4), 1 default (strided: short runs; CSR: gathered),
                                           // 2 short runs for CSR too (launch_short_runs)
+    std::atomic<int> short_loads{0};      // short runs: 0 buffer loads, 1 global loads
     std::atomic<int> lds_pad{0};          // bytes of dynamic LDS per batch block (occupancy
                                           // experiments; 0 = none)
     std::atomic<int> chain_short{-1};      // chains: chunks of at most this many bytes first in
@@ -387,6 +388,7 @@ struct Tuning {
         env("AIPSTACK_CHKSUM_TX_STORE", tx_store);
         env("AIPSTACK_CHKSUM_CHAIN_SHORT", chain_short);
         env("AIPSTACK_CHKSUM_GATHER", gather);
+        env("AIPSTACK_CHKSUM_SHORT_LOADS", short_loads);
         env("AIPSTACK_ENGINE_ZERO_COPY", engine_zero_copy);
         env("AIPSTACK_ENGINE_ZERO_COPY_SMALL", engine_zero_copy_small);
         env("AIPSTACK_ENGINE_PAGEABLE_ROWS", engine_pageable_rows);
@@ -627,6 +629,8 @@ int launch_short_runs(const Desc &desc, uint64_t n, uint32_t len, uint16_t *d_ou
         while (cp < (uint32_t)kWave && (uint64_t)(2 * cp) * len <= 12288u) cp <<= 1;
         sh.chunk_packets = cp;
     }
+    if (tuning().short_loads.load(std::memory_order_relaxed) == 1)  // global loads (SU 32)
+        return launch_k<Desc, 1, 1, true, SEEDED, 32>(desc, n, sh, d_out, flags, stream, true);
     return launch_k<Desc, 1, 1, true, SEEDED, 16>(desc, n, sh, d_out, flags, stream, true);
 }
 
@@ -842,6 +846,7 @@ extern "C" int aipstack_chksum_tune(const char *key, int value) {
     else if (!std::strcmp(key, "chain_short")) t.chain_short = value;
     else if (!std::strcmp(key, "gather")) t.gather = value;
     else if (!std::strcmp(key, "lds_pad")) t.lds_pad = value;
+    else if (!std::strcmp(key, "short_loads")) t.short_loads = value;
     else if (!std::strcmp(key, "engine_zero_copy")) t.engine_zero_copy = value;
     else if (!std::strcmp(key, "engine_zero_copy_small")) t.engine_zero_copy_small = value;
     else if (!std::strcmp(key, "engine_pageable_rows")) t.engine_pageable_rows = value;

@@ -33,6 +33,29 @@ __global__ __launch_bounds__(256) void read_kernel(const u32x4 *__restrict__ p, 
     if (acc == 0x12345678u) out[wave] = acc;  // practically never: keeps loads live
 }
 
+// The same read through global_load_dwordx4 with a 64-bit address per lane (the gathered
+// checksum loader's form) instead of a buffer descriptor.
+template <int UNROLL>
+__global__ __launch_bounds__(256) void read_kernel_global(const u32x4 *__restrict__ p, uint64_t n16,
+                                                          uint64_t per_wave, uint32_t *out) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t wave = (uint64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint64_t i = wave * per_wave;
+    const uint64_t end = min(i + per_wave, n16);
+    uint32_t acc = 0;
+    for (uint64_t off = 0; i + off < end; off += 64 * UNROLL) {
+        u32x4 v[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            const uint64_t k = min(i + off + (uint64_t)(lane + u * 64), end - 1);
+            v[u] = __builtin_nontemporal_load(p + k);
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) acc ^= v[u][0] + v[u][1] + v[u][2] + v[u][3];
+    }
+    if (acc == 0x12345678u) out[wave] = acc;
+}
+
 // Slotted read: packets of `len` bytes at a `stride` (MTU packets in 2048-byte ring slots),
 // one packet per wave instruction pair (segments lane and lane + 64 of the packet), P
 // packets in flight: the access pattern of the checksum kernel's per-packet wave mode,
@@ -90,7 +113,7 @@ float run(const u32x4 *d, uint64_t n16, uint64_t per_wave, uint32_t *out, int re
 // Shapes: long runs per wave (32 KiB, 2 or 4 windows in flight: the rounds 1-3 probe) and the
 // gathered checksum loader's shape (one short run per wave, ~12 KiB, every window issued up
 // front). Prints one JSON line; "GBps" is the best shape.
-template <int U, bool NT>
+template <int U, bool NT, bool GLOBAL = false>
 float run_rot(u32x4 *const *d, int nbuf, uint64_t n16, uint64_t per_wave, uint32_t *out) {
     uint64_t waves = (n16 + per_wave - 1) / per_wave;
     dim3 grid((unsigned)((waves + 3) / 4));
@@ -99,7 +122,10 @@ float run_rot(u32x4 *const *d, int nbuf, uint64_t n16, uint64_t per_wave, uint32
     std::vector<float> t;
     for (int r = 0; r < 45; ++r) {
         (void)hipEventRecord(a);
-        hipLaunchKernelGGL((read_kernel<U, NT>), grid, dim3(256), 0, 0, d[r % nbuf], n16, per_wave, out);
+        if (GLOBAL)
+            hipLaunchKernelGGL((read_kernel_global<U>), grid, dim3(256), 0, 0, d[r % nbuf], n16, per_wave, out);
+        else
+            hipLaunchKernelGGL((read_kernel<U, NT>), grid, dim3(256), 0, 0, d[r % nbuf], n16, per_wave, out);
         (void)hipEventRecord(b);
         (void)hipEventSynchronize(b);
         float ms; (void)hipEventElapsedTime(&ms, a, b);
@@ -126,15 +152,19 @@ int ceiling() {
     const float t_g12 = run_rot<12, true>(d, R, n16, 768, out);   // 12 KiB per wave, up front
     const float t_g16 = run_rot<16, true>(d, R, n16, 1024, out);  // 16 KiB per wave, up front
     const float t_g8 = run_rot<8, true>(d, R, n16, 768, out);     // 12 KiB, 8 windows then 4
-    const float best = std::min(std::min(std::min(t_2, t_4), std::min(t_g12, t_g16)), t_g8);
+    const float t_gg12 = run_rot<12, true, true>(d, R, n16, 768, out);  // global loads
+    const float t_gg8 = run_rot<8, true, true>(d, R, n16, 768, out);
+    const float best = std::min(std::min(std::min(t_2, t_4), std::min(t_g12, t_g16)),
+                                std::min(t_g8, std::min(t_gg12, t_gg8)));
     auto gbps = [&](float ms) { return bytes / ms / 1e6; };
     printf("{\"GBps\": %.1f, \"us\": %.2f, \"rotation\": %d, \"bytes_per_launch\": %lu, "
            "\"shapes_GBps\": {\"run32K_u2\": %.1f, \"run32K_u4\": %.1f, \"run12K_upfront\": %.1f, "
-           "\"run16K_upfront\": %.1f, \"run12K_u8\": %.1f}, \"source\": \"tools/build/hbm_peak "
+           "\"run16K_upfront\": %.1f, \"run12K_u8\": %.1f, \"run12K_upfront_global\": %.1f, "
+           "\"run12K_u8_global\": %.1f}, \"source\": \"tools/build/hbm_peak "
            "ceiling: 16-B nontemporal reads, median of 30 launches over 3 rotated 1.57 GB "
            "buffers\"}\n",
            gbps(best), best * 1e3, R, (unsigned long)bytes, gbps(t_2), gbps(t_4), gbps(t_g12),
-           gbps(t_g16), gbps(t_g8));
+           gbps(t_g16), gbps(t_g8), gbps(t_gg12), gbps(t_gg8));
     for (int r = 0; r < R; ++r) CK(hipFree(d[r]));
     CK(hipFree(out));
     return 0;

@@ -81,6 +81,16 @@ shape)  # A's loaders at steady state, interleaved in one process (tools/ab.py),
         --config TX2K --no-cpu-baseline --no-parity --steps 5 --warmup 2 > "$out/pmcf_TX2K_st$st.log" 2>&1
   done
   ;;
+occ)  # A at fewer waves per CU (lds_pad), short runs' chunk sizes and load forms
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+      -k "every_read_form or short_runs" > "$out/pytest.log" 2>&1
+  AIPSTACK_CHKSUM_SHORT_LOADS=1 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 \
+      --timeout-method thread -k "every_read_form or short_runs or full_size" > "$out/pytest_gl.log" 2>&1
+  timeout -k 10 600 python3 tools/ab.py --config A --rounds 16 --variants \
+      "gather=0;gather=1,lds_pad=41984;gather=1,lds_pad=54000;gather=1,chunk_packets=4,lds_pad=41984;gather=1,chunk_packets=16,lds_pad=41984;gather=1,chunk_packets=16,lds_pad=54000;gather=1,short_loads=1;gather=1,short_loads=1,lds_pad=41984;gather=0,lds_pad=54000;gather=1,chunk_packets=32,lds_pad=54000;gather=1,chunk_packets=4,lds_pad=54000" \
+      > "$out/ab_A.jsonl" 2> "$out/ab_A.err"
+  timeout -k 10 120 tools/build/hbm_peak ceiling > "$out/ceiling.jsonl"
+  ;;
 *)
   echo "unknown mode $mode"; exit 2 ;;
 esac
