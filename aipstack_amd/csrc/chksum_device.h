@@ -704,6 +704,14 @@ __device__ __forceinline__ uint32_t halves(uint32_t x, uint32_t acc) {
     return __builtin_amdgcn_sad_u16(x, 0u, acc);  // (x & 0xFFFF) + (x >> 16) + acc
 }
 
+// Halves-sum of bytes [0, o) of one aligned 16-byte segment (o < 16).
+__device__ __forceinline__ uint32_t halves_below_seg(const u32x4 &x, uint32_t o) {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) acc = halves(x[d] & dword_keep(0, (int)o - 4 * d), acc);
+    return acc;
+}
+
 // Inclusive prefix sum over the 64 lanes (row scan + row broadcasts).
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xF, 0xF, false);
@@ -1175,6 +1183,120 @@ __device__ __forceinline__ uint32_t sum_stream_chunk(uint64_t S, uint64_t E, int
     run.prefixes(bs, hb, hx, voff);
     const uint32_t hn = from_next_lane(hb[0], hx, lane);  // H(S_{j+1}); lane 63: H(X1)
     return lane < cnt ? hn - hb[0] : 0u;
+}
+
+// Column runs (round 5, SU = 64): a short chunk of back-to-back packets (at most
+// kColMaxPackets) read as one run of 16-byte segments, 64 per wave instruction (lane L of
+// window w loads segment 64w + L), groups of 8 windows double-buffered -- and no cross-lane
+// work per window. Each lane keeps the sum of its own column (its segments of the windows
+// consumed so far, C). Boundary j of the chunk (packet starts S_0..S_{cnt-1} and the run's end
+// X1, lane j holding b_j) lies in segment g_j = 64 W + B; when window W is consumed, every lane
+// writes X_{j,L} = C_L + (L < B ? s_L : 0) to row j of an LDS table, so that the sum over L of
+// X_{j,L} is the halves-sum of the whole segments before b_j. The bytes of segment g_j below
+// b_j (P_j) come from one segment load per lane at the start (default cache policy; the stream
+// reads that line again later). Packet j's exact halves-sum is then
+//     sum over L of (X_{j+1,L} - X_{j,L}) + P_{j+1} - P_j   (mod 2^32, exact: < 2^17 bytes),
+// the column differences added by 64 / cp lanes per packet from the table, then a butterfly.
+// Per window: 4 v_sad_u16 and one add per lane; per boundary a select, an add and an LDS write
+// (stream mode: a 6-step DPP scan per window and 5 ds_bpermute per boundary).
+constexpr int kColMaxPackets = 16;
+typedef uint32_t ColRows[(kColMaxPackets + 1) * kWave];
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+}
+
+template <bool NT>
+__device__ __forceinline__ uint32_t sum_column_chunk(uint64_t S, uint64_t E, int lane, int cnt,
+                                                     uint32_t voff, uint32_t cpk, uint32_t *rows) {
+    const uint64_t X1 = readlane64(E, cnt - 1);  // end of the chunk's last packet
+    if (lane >= cnt) S = X1;                      // lane cnt: boundary X1; past it: unused
+    const uint64_t A =
+        (((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(S >> 32)) << 32) |
+         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)S)) & ~(uint64_t)15;
+    const uint32_t nseg = ((uint32_t)(X1 - A) + 15u) >> 4;  // the run < 17 * 2^17 bytes
+    const uint32_t nwin = (nseg + (uint32_t)kWave - 1u) >> 6;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void *>(A), (short)0, (int)(nseg * 16u), 0x00020000);
+    const uint32_t rel = (uint32_t)(S - A);
+    const uint32_t g = rel >> 4, o = rel & 15u;
+    // P_j: boundary j's segment below it (lanes 0..cnt; none on a segment edge)
+    u32x4 bseg = {0u, 0u, 0u, 0u};
+    if (lane <= cnt && o != 0u) bseg = load_segment<false>(rsrc, g * 16u, 0u);
+    constexpr int U = 8;
+    u32x4 va[U], vb[U];
+    auto issue = [&](u32x4 (&v)[U], uint32_t w) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            v[u] = load_segment<NT>(rsrc, voff, (w + (uint32_t)u) * 1024u);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+    uint32_t C = 0;                                                 // this lane's column sum
+    uint32_t jb = 0;                                                // next boundary (uniform)
+    uint32_t gj = (uint32_t)__builtin_amdgcn_readlane((int)g, 0);  // its segment
+    auto consume = [&](const u32x4 (&v)[U], uint32_t w) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t wu = w + (uint32_t)u;
+            if (wu >= nwin) break;
+            const uint32_t s =
+                halves(v[u][0], halves(v[u][1], halves(v[u][2], halves(v[u][3], 0u))));
+            while (jb <= (uint32_t)cnt && (gj >> 6) == wu) {
+                rows[jb * kWave + (uint32_t)lane] = C + ((uint32_t)lane < (gj & 63u) ? s : 0u);
+                ++jb;
+                gj = jb <= (uint32_t)cnt ? (uint32_t)__builtin_amdgcn_readlane((int)g, (int)jb)
+                                         : ~0u;
+            }
+            C += s;
+        }
+    };
+    const uint32_t groups = (nwin + U - 1u) / U;
+    issue(va, 0);
+    uint32_t gi = 0;
+    for (; gi + 2u < groups; gi += 2u) {
+        issue(vb, (gi + 1u) * U);
+        consume(va, gi * U);
+        issue(va, (gi + 2u) * U);
+        consume(vb, (gi + 1u) * U);
+    }
+    if (gi + 2u == groups) {
+        issue(vb, (gi + 1u) * U);
+        consume(va, gi * U);
+        consume(vb, (gi + 1u) * U);
+    } else {
+        consume(va, gi * U);
+    }
+    for (; jb <= (uint32_t)cnt; ++jb) rows[jb * kWave + (uint32_t)lane] = C;  // at the run's end
+    const uint32_t P = halves_below_seg(bseg, o);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    // packet j = lane >> ql: its 2^ql lanes add cpk column differences each
+    const uint32_t ql = 6u - (uint32_t)__builtin_ctz(cpk);  // cpk: a power of two <= 16
+    const uint32_t j = (uint32_t)lane >> ql, part = (uint32_t)lane & ((1u << ql) - 1u);
+    uint32_t acc = 0;
+    if (j < (uint32_t)cnt) {
+        const uint32_t *r0 = rows + j * kWave + part * cpk;
+        const uint32_t *r1 = r0 + kWave;
+        if (cpk >= 4u) {
+            for (uint32_t i = 0; i < cpk; i += 4u) {
+                const u32x4 a = *reinterpret_cast<const u32x4 *>(r0 + i);
+                const u32x4 b = *reinterpret_cast<const u32x4 *>(r1 + i);
+                acc += (b[0] - a[0]) + (b[1] - a[1]) + (b[2] - a[2]) + (b[3] - a[3]);
+            }
+        } else {
+            for (uint32_t i = 0; i < cpk; ++i) acc += r1[i] - r0[i];
+        }
+    }
+    for (uint32_t m = 1; m < (1u << ql); m <<= 1)
+        acc += (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((uint32_t)lane ^ m) << 2), (int)acc);
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t col = (uint32_t)__builtin_amdgcn_ds_bpermute(
+        (int)((((uint32_t)lane << ql) & 63u) << 2), (int)acc);
+    const uint32_t pn = from_next_lane(P, 0u, lane);  // P_{j+1} (lane cnt: X1's)
+    __builtin_amdgcn_wave_barrier();  // (the table is rewritten by the next chunk)
+    return lane < cnt ? col + pn - P : 0u;
 }
 
 // Sum over the 64 lanes (DPP row scan + row broadcasts); result valid in lane 63,

@@ -70,6 +70,9 @@ int tuning_frames_in_flight();
 uint32_t frames_per_chunk(uint64_t n, int cus);
 // The "chunk_packets" tunable (0 = automatic).
 int tuning_chunk_packets();
+// Dynamic LDS per block for a launch whose own default is `family_default` bytes (tunable
+// lds_pad: > 0 that many bytes, -1 none): fewer blocks fit a CU, so fewer waves run per SIMD.
+unsigned tuning_lds_pad(int family_default);
 
 // Resident-wave budget per CU the grids are sized to (tunable "waves_per_cu"; 0 = each
 // kernel's default).

@@ -80,6 +80,8 @@ __global__ __launch_bounds__(kBlock) void chksum_batch_kernel(Desc desc, uint64_
         KeepTable keep;
     };
     __shared__ typename std::conditional<kGathered, GatheredShared, char>::type gsh;
+    constexpr bool kColumns = Desc::kStream && SU == 64;  // column runs (sum_column_chunk)
+    __shared__ typename std::conditional<kColumns, ColRows[kWavesPerBlock], char>::type col_rows;
     if constexpr (kGathered) {
         if constexpr (!Desc::kEdge) {  // edges masked in the stream: the mask table
             fill_keep_table(gsh.keep);
@@ -113,7 +115,11 @@ __global__ __launch_bounds__(kBlock) void chksum_batch_kernel(Desc desc, uint64_
         } else if constexpr (SU > 0) {
             if (stream_ok(lS, lE, lane, cnt)) {
                 // back-to-back packets: the chunk read as one contiguous run
-                sums = sum_stream_chunk<SU, NT>(lS, lE, lane, cnt, voff);
+                if constexpr (kColumns)
+                    sums = sum_column_chunk<NT>(lS, lE, lane, cnt, voff, chunk_packets,
+                                                col_rows[wave_in_block]);
+                else
+                    sums = sum_stream_chunk<SU, NT>(lS, lE, lane, cnt, voff);
                 streamed = true;
             }
         }
@@ -356,11 +362,11 @@ struct Tuning {
                                           // whole sectors; else the default
     std::atomic<int> gather{1};           // back-to-back batches: -1 stream mode with 64-packet
                                           // chunks (rounds 1-3), 0 the gathered stream (round
-                                          // 4), 1 default (strided: short runs; CSR: gathered),
-                                          // 2 short runs for CSR too (launch_short_runs)
-    std::atomic<int> short_loads{0};      // short runs: 0 buffer loads, 1 global loads
-    std::atomic<int> lds_pad{0};          // bytes of dynamic LDS per batch block (occupancy
-                                          // experiments; 0 = none)
+                                          // 4), 1 (or 2) short runs (round 5, launch_short_runs)
+    std::atomic<int> short_loads{0};      // short runs: 0 stream prefixes (buffer loads), 1 the
+                                          // same through global loads, 2 column runs
+    std::atomic<int> lds_pad{0};          // bytes of dynamic LDS per batch block (occupancy;
+                                          // 0 = the launch's own, -1 = none)
     std::atomic<int> chain_short{-1};      // chains: chunks of at most this many bytes first in
                                           // the gathered stream (0 = table order; measured:
                                           // CHAIN 250.0-250.6 us at 128 against 248.0-248.9,
@@ -389,6 +395,7 @@ struct Tuning {
         env("AIPSTACK_CHKSUM_CHAIN_SHORT", chain_short);
         env("AIPSTACK_CHKSUM_GATHER", gather);
         env("AIPSTACK_CHKSUM_SHORT_LOADS", short_loads);
+        env("AIPSTACK_CHKSUM_LDS_PAD", lds_pad);
         env("AIPSTACK_ENGINE_ZERO_COPY", engine_zero_copy);
         env("AIPSTACK_ENGINE_ZERO_COPY_SMALL", engine_zero_copy_small);
         env("AIPSTACK_ENGINE_PAGEABLE_ROWS", engine_pageable_rows);
@@ -402,6 +409,7 @@ Tuning &tuning() {
 }
 
 constexpr int kDefaultWavesPerCu = 64;
+constexpr int kShortRunLds = 0;  // dynamic LDS per short-run block (none: 5 waves per SIMD)
 
 // The product build compiles the launch shapes the pick_* functions choose, plus the runtime
 // forms the tests exercise (stream windows 2 / 4 / 8 / off, the gathered stream's window
@@ -480,7 +488,7 @@ int pick_stream_for(bool csr, const Shape &sh) {
 
 template <class Desc, int U, int P, bool NT, bool SEEDED, int SU>
 int launch_k(const Desc &desc, uint64_t n, const Shape &sh, uint16_t *d_out, uint32_t flags,
-             hipStream_t stream, bool one_per_wave = false) {
+             hipStream_t stream, bool one_per_wave = false, int dyn_lds = 0) {
     const uint64_t nchunks = (n + sh.chunk_packets - 1) / sh.chunk_packets;
     const int cus = device_cu_count(stream);
     if (cus <= 0) return AIPSTACK_CHKSUM_EHIP;
@@ -500,10 +508,9 @@ int launch_k(const Desc &desc, uint64_t n, const Shape &sh, uint16_t *d_out, uin
     if (blocks > 0x7FFFFFFFull || cpw > 0xFFFFFFFFull) return AIPSTACK_CHKSUM_EINVAL;
     // (tunable lds_pad: dynamic LDS per block, so that fewer blocks fit a CU -- occupancy
     // experiments only; 0 by default)
-    const int pad = tuning().lds_pad.load(std::memory_order_relaxed);
     hipLaunchKernelGGL((chksum_batch_kernel<Desc, U, P, NT, SEEDED, SU>), dim3((unsigned)blocks),
-                       dim3(kBlock), (unsigned)(pad > 0 && pad <= 65536 ? pad : 0), stream, desc,
-                       n, (uint32_t)cpw, sh.chunk_packets, d_out, flags);
+                       dim3(kBlock), tuning_lds_pad(dyn_lds), stream, desc, n, (uint32_t)cpw,
+                       sh.chunk_packets, d_out, flags);
     return check_hip(hipGetLastError());
 }
 
@@ -629,9 +636,21 @@ int launch_short_runs(const Desc &desc, uint64_t n, uint32_t len, uint16_t *d_ou
         while (cp < (uint32_t)kWave && (uint64_t)(2 * cp) * len <= 12288u) cp <<= 1;
         sh.chunk_packets = cp;
     }
+    // Occupancy: the 5 waves per SIMD its 96 VGPRs allow. At 3 (tunable lds_pad = 41984: 3
+    // blocks of 4 waves per CU's 160 KiB) config A's steady state is 222.5 us against 230.1
+    // (tools/ab.py, one process, rotated batches, profiles/r05/occ), but the faster kernel
+    // draws the clock dip described above into the driver's 25-launch protocol: 243-247 us
+    // there against 228-229 (profiles/r05/driver2). B loses at 3 (366.9 vs 331.8 us).
+    if (tuning().short_loads.load(std::memory_order_relaxed) == 2) {  // column runs (SU 64)
+        if (sh.chunk_packets > (uint32_t)kColMaxPackets) sh.chunk_packets = kColMaxPackets;
+        return launch_k<Desc, 1, 1, true, SEEDED, 64>(desc, n, sh, d_out, flags, stream, true,
+                                                      kShortRunLds);
+    }
     if (tuning().short_loads.load(std::memory_order_relaxed) == 1)  // global loads (SU 32)
-        return launch_k<Desc, 1, 1, true, SEEDED, 32>(desc, n, sh, d_out, flags, stream, true);
-    return launch_k<Desc, 1, 1, true, SEEDED, 16>(desc, n, sh, d_out, flags, stream, true);
+        return launch_k<Desc, 1, 1, true, SEEDED, 32>(desc, n, sh, d_out, flags, stream, true,
+                                                      kShortRunLds);
+    return launch_k<Desc, 1, 1, true, SEEDED, 16>(desc, n, sh, d_out, flags, stream, true,
+                                                  kShortRunLds);
 }
 
 template <bool NT, int SU>
@@ -651,8 +670,8 @@ int launch_chain(const uint64_t *d_addr, const uint32_t *d_len, const uint64_t *
     const uint64_t waves = (nchunks + cpw - 1) / cpw;
     const uint64_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
     if (blocks > 0x7FFFFFFFull || cpw > 0xFFFFFFFFull) return AIPSTACK_CHKSUM_EINVAL;
-    hipLaunchKernelGGL((chksum_chain_kernel<NT, SU>), dim3((unsigned)blocks), dim3(kBlock), 0,
-                       stream, d_addr, d_len, d_index, d_states, n, (uint32_t)cpw, cpg, d_out,
+    hipLaunchKernelGGL((chksum_chain_kernel<NT, SU>), dim3((unsigned)blocks), dim3(kBlock),
+                       tuning_lds_pad(0), stream, d_addr, d_len, d_index, d_states, n, (uint32_t)cpw, cpg, d_out,
                        flags, (uint32_t)tuning_chain_short());
     if (d_fields) {  // chain fill: the field stores as a pass of their own
         const int st = check_hip(hipGetLastError());
@@ -692,6 +711,12 @@ int tuning_stream_windows(int family_default) {
 uint32_t frames_per_chunk(uint64_t n, int cus) { return pick_shape(n, cus).chunk_packets; }
 
 int tuning_chunk_packets() { return tuning().chunk_packets.load(std::memory_order_relaxed); }
+
+unsigned tuning_lds_pad(int family_default) {
+    int pad = tuning().lds_pad.load(std::memory_order_relaxed);
+    if (pad == 0) pad = family_default;
+    return (unsigned)(pad > 0 && pad <= 65536 ? pad : 0);
+}
 
 int tuning_tx_header_mode(int family_default) {
     const int t = tuning().tx_gather.load(std::memory_order_relaxed);
@@ -748,12 +773,12 @@ int batch_csr_from(const void *d_base, const uint64_t *d_offsets, uint64_t n, ui
     if (n == 0) return AIPSTACK_CHKSUM_OK;
     if (!d_base || !d_offsets || !d_out) return AIPSTACK_CHKSUM_EINVAL;
     if (n > (1ull << 40)) return AIPSTACK_CHKSUM_EINVAL;
-    // Typical network packets (<= ~2 KiB) fit one group at U = 2 in the wave mode; longer
-    // ones loop. The gathered stream (config C 231.0 us against 251.8 in stream mode), except
-    // for bytes read over the link from host memory (C end to end 48.9 vs 44.9 GiB/s) or
-    // with tunable "gather" = -1.
+    // CSR packets are back to back: short runs (round 5; config C 236.8 us against 241.7 for
+    // the round-4 gathered stream, tools/ab.py, profiles/r05/driver2), except for bytes read
+    // over the link from host memory (C end to end 48.9 vs 44.9 GiB/s in stream mode) or with
+    // tunable "gather" 0 (gathered) / -1 (stream mode, 64-packet chunks).
     const int gm = tuning().gather.load(std::memory_order_relaxed);
-    if (!host_bytes && gm == 2) {  // short runs (launch_short_runs), 16-packet chunks at ~760 B
+    if (!host_bytes && gm >= 1) {  // short runs (launch_short_runs), 16-packet chunks at ~760 B
         CsrDesc d{(uint64_t)(uintptr_t)d_base, d_offsets};
         return launch_short_runs<CsrDesc, false>(d, n, 768u, d_out, flags, (hipStream_t)stream);
     }

@@ -931,7 +931,8 @@ int launch_frames_g(const Desc &desc, uint64_t n, uint8_t *d_status, uint64_t *d
 #define AIPSTACK_LAUNCH_FRAMES(P, SU)                                                          \
     hipLaunchKernelGGL((frame_kernel<Desc, TX, 2, P, AIPSTACK_FRAME_NT != 0, SU, SPLIT, GATHER,  \
                                      STORE>),                                                    \
-                       dim3((unsigned)blocks), dim3(kBlock), 0, stream, desc, n, (uint32_t)cpw, \
+                       dim3((unsigned)blocks), dim3(kBlock), tuning_lds_pad(0), stream, desc, n, \
+                       (uint32_t)cpw,                                                           \
                        cpk, d_status, d_records)
 #define AIPSTACK_LAUNCH_FRAMES_SU(P)                  \
     if constexpr (!Desc::kStream) {                   \

@@ -329,14 +329,50 @@ def test_strided_and_csr_in_every_read_form(oracle, gather, chunk):
         _tune("chunk_packets", 0)
 
 
+@pytest.mark.parametrize("mode", [0, 1, 2])
 @pytest.mark.parametrize("plen,n", [(64, 300000), (1500, 270000), (9000, 40000)])
-def test_short_runs_large_batches(oracle, plen, n):
+def test_short_runs_large_batches(oracle, plen, n, mode):
     """Back-to-back strided batches large enough for the default short-run shape (one chunk of
-    ~12 KiB per wave, SU = 16), at an odd base, against the oracle."""
-    buf = torch.empty(n * plen + 7, dtype=torch.uint8, device=DEV)
-    synth.fill_device(buf, 41 + plen)
-    got = _np(A.chksum_batch_strided(buf, plen, plen, n, byte_offset=7, final=True))
-    assert np.array_equal(got, oracle.batch_strided(_np(buf)[7:], plen, plen, n, final=True))
+    ~12 KiB per wave), at an odd base, against the oracle: stream prefixes through buffer loads
+    (tunable short_loads 0) or global loads (1), and column runs (2)."""
+    _tune("short_loads", mode)
+    try:
+        buf = torch.empty(n * plen + 7, dtype=torch.uint8, device=DEV)
+        synth.fill_device(buf, 41 + plen)
+        got = _np(A.chksum_batch_strided(buf, plen, plen, n, byte_offset=7, final=True))
+        assert np.array_equal(got, oracle.batch_strided(_np(buf)[7:], plen, plen, n, final=True))
+    finally:
+        _tune("short_loads", 0)
+
+
+@pytest.mark.parametrize("chunk", [1, 2, 4, 8, 16, 32])
+@pytest.mark.parametrize("mode", [1, 2])
+def test_short_run_forms_ragged(oracle, mode, chunk):
+    """The short-run forms at every chunk size (column runs cap chunks at 16 packets) on
+    ragged strided and CSR batches: lengths 0..3000 with odd starts, empty packets, a batch
+    that ends mid-chunk, all-0x00 / all-0xFF packets."""
+    _tune("short_loads", mode)
+    _tune("chunk_packets", chunk)
+    try:
+        buf = torch.empty(1 << 23, dtype=torch.uint8, device=DEV)
+        synth.fill_device(buf, 51 + chunk)
+        buf[1000:5000] = 0
+        buf[9000:12000] = 255
+        hb = _np(buf)
+        rng = np.random.default_rng(60 + chunk + 100 * mode)
+        for plen in (0, 1, 15, 16, 17, 1023, 1500, 3001):
+            n = min(2999, (buf.numel() - 9) // max(plen, 1))
+            got = _np(A.chksum_batch_strided(buf, plen, plen, n, byte_offset=9))
+            assert np.array_equal(got, oracle.batch_strided(hb[9:], plen, plen, n)), plen
+        lens = rng.integers(0, 3000, 5001)
+        lens[rng.random(lens.size) < 0.1] = 0
+        off = np.concatenate([[3], 3 + np.cumsum(lens)]).astype(np.int64)
+        assert off[-1] <= buf.numel()
+        got = _np(A.chksum_batch_csr(buf, _d(off), final=True))
+        assert np.array_equal(got, oracle.batch_csr(hb, off.astype(np.uint64), final=True))
+    finally:
+        _tune("short_loads", 0)
+        _tune("chunk_packets", 0)
 
 
 def test_overlapping_and_zero_stride(oracle):

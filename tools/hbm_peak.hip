@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstdint>
 #include <cstring>
+#include <cstdlib>
 #include <vector>
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -170,8 +171,46 @@ int ceiling() {
     return 0;
 }
 
+// Per-launch times of the first 120 launches of one read shape from a cold start (3 rotated
+// 1.57 GB buffers, no warm-up): does a pure read at the checksum kernels' rate show their
+// clock dip ~3 ms into a run? Shape: 12 KiB per wave, 8 windows then 4 (u8).
+int trace_reads(int global) {
+    const uint64_t bytes = 1572864000ull;
+    const uint64_t n16 = bytes / 16;
+    constexpr int R = 3;
+    u32x4 *d[R]; uint32_t *out;
+    for (int r = 0; r < R; ++r) {
+        CK(hipMalloc(&d[r], bytes));
+        CK(hipMemset(d[r], 1 + r, bytes));
+    }
+    CK(hipMalloc(&out, 1 << 24));
+    CK(hipDeviceSynchronize());
+    const uint64_t per_wave = 768, waves = (n16 + per_wave - 1) / per_wave;
+    dim3 grid((unsigned)((waves + 3) / 4));
+    std::vector<hipEvent_t> ev(2 * 120);
+    for (auto &evk : ev) CK(hipEventCreate(&evk));
+    for (int k = 0; k < 120; ++k) {
+        CK(hipEventRecord(ev[2 * k]));
+        if (global)
+            hipLaunchKernelGGL((read_kernel_global<8>), grid, dim3(256), 0, 0, d[k % R], n16, per_wave, out);
+        else
+            hipLaunchKernelGGL((read_kernel<8, true>), grid, dim3(256), 0, 0, d[k % R], n16, per_wave, out);
+        CK(hipEventRecord(ev[2 * k + 1]));
+    }
+    CK(hipDeviceSynchronize());
+    printf("{\"trace\": \"%s\", \"us\": [", global ? "run12K_u8_global" : "run12K_u8");
+    for (int k = 0; k < 120; ++k) {
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, ev[2 * k], ev[2 * k + 1]));
+        printf("%s%.2f", k ? ", " : "", ms * 1e3);
+    }
+    printf("]}\n");
+    return 0;
+}
+
 int main(int argc, char **argv) {
     if (argc > 1 && std::strcmp(argv[1], "ceiling") == 0) return ceiling();
+    if (argc > 1 && std::strcmp(argv[1], "trace") == 0) return trace_reads(argc > 2 ? std::atoi(argv[2]) : 1);
     const uint64_t bytes = 2359296000ull;  // config B's payload (2.36 GB, > 256 MiB MALL)
     const uint64_t n16 = bytes / 16;
     u32x4 *d; uint32_t *out;

@@ -91,6 +91,61 @@ occ)  # A at fewer waves per CU (lds_pad), short runs' chunk sizes and load form
       > "$out/ab_A.jsonl" 2> "$out/ab_A.err"
   timeout -k 10 120 tools/build/hbm_peak ceiling > "$out/ceiling.jsonl"
   ;;
+driver2)  # short runs at 3 waves per SIMD (the default) under the driver's protocol, against
+          # the gathered stream; B and C shapes at steady state
+  bench n1_def --gpus 1 --steps 20 --warmup 5 --per-launch
+  AIPSTACK_CHKSUM_GATHER=0 bench n1_gath --gpus 1 --steps 20 --warmup 5 --per-launch --no-cpu-baseline
+  bench n1_def --gpus 1 --steps 20 --warmup 5 --per-launch --no-cpu-baseline
+  AIPSTACK_CHKSUM_GATHER=0 AIPSTACK_CHKSUM_LDS_PAD=33000 bench n1_gath3 --gpus 1 --steps 20 --warmup 5 --per-launch --no-cpu-baseline
+  trace tr_def --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-ceiling
+  trace long_def --steps 400 --warmup 0 --no-cpu-baseline --no-ceiling
+  AIPSTACK_CHKSUM_GATHER=0 AIPSTACK_CHKSUM_LDS_PAD=33000 trace long_gath3 --steps 400 --warmup 0 --no-cpu-baseline --no-ceiling
+  bench B_def --config B --steps 20 --warmup 5 --per-launch --no-cpu-baseline
+  bench C_def --config C --steps 20 --warmup 5 --per-launch --no-cpu-baseline
+  timeout -k 10 600 python3 tools/ab.py --config B --rounds 12 --variants \
+      "gather=1;gather=1,lds_pad=-1;gather=1,chunk_packets=2;gather=1,chunk_packets=2,lds_pad=-1;gather=0;gather=0,lds_pad=33000" \
+      > "$out/ab_B.jsonl" 2> "$out/ab_B.err"
+  timeout -k 10 600 python3 tools/ab.py --config C --rounds 12 --variants \
+      "gather=1;gather=1,lds_pad=33000;gather=2;gather=2,lds_pad=-1;gather=2,chunk_packets=32;gather=2,chunk_packets=8" \
+      > "$out/ab_C.jsonl" 2> "$out/ab_C.err"
+  ;;
+clock)  # the new defaults under the driver's protocol; per-dispatch clocks (GRBM_GUI_ACTIVE)
+        # through the first 60 launches, short runs against the gathered stream
+  bench n1_def --gpus 1 --steps 20 --warmup 5 --per-launch
+  bench C_def --config C --steps 20 --warmup 5 --per-launch --no-cpu-baseline
+  bench B_def --config B --steps 20 --warmup 5 --per-launch --no-cpu-baseline
+  bench n1_def --gpus 1 --steps 20 --warmup 5 --per-launch --no-cpu-baseline
+  for g in 1 0; do
+    AIPSTACK_CHKSUM_GATHER=$g timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv \
+        -d "$out/clk_g$g" -o run --pmc GRBM_GUI_ACTIVE GRBM_COUNT -- python3 bench.py \
+        --config A --no-cpu-baseline --no-parity --no-ceiling --steps 60 --warmup 0 \
+        > "$out/clk_g$g.log" 2>&1
+  done
+  trace long_def --steps 400 --warmup 0 --no-cpu-baseline --no-ceiling
+  ;;
+col)  # column runs (tunable short_loads 2): parity, steady state against the defaults, the
+      # driver's protocol at 4 and 3 waves per SIMD, instruction mix
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+      -k "short_run or every_read_form or full_size" > "$out/pytest.log" 2>&1
+  AIPSTACK_CHKSUM_SHORT_LOADS=2 bench n1_col --gpus 1 --steps 20 --warmup 5 --per-launch --no-cpu-baseline
+  AIPSTACK_CHKSUM_SHORT_LOADS=2 AIPSTACK_CHKSUM_LDS_PAD=26000 bench n1_col3 --gpus 1 --steps 20 --warmup 5 --per-launch --no-cpu-baseline
+  bench n1_def --gpus 1 --steps 20 --warmup 5 --per-launch --no-cpu-baseline
+  timeout -k 10 600 python3 tools/ab.py --config A --rounds 12 --variants \
+      "short_loads=0;short_loads=2;short_loads=2,lds_pad=26000;short_loads=2,lds_pad=38000;gather=0;short_loads=2,chunk_packets=16" \
+      > "$out/ab_A.jsonl" 2> "$out/ab_A.err"
+  timeout -k 10 600 python3 tools/ab.py --config C --rounds 8 --variants \
+      "short_loads=0;short_loads=2;short_loads=2,lds_pad=26000;short_loads=2,chunk_packets=8" \
+      > "$out/ab_C.jsonl" 2> "$out/ab_C.err"
+  timeout -k 10 600 python3 tools/ab.py --config B --rounds 8 --variants \
+      "short_loads=0;short_loads=2;short_loads=2,lds_pad=26000;short_loads=2,chunk_packets=2" \
+      > "$out/ab_B.jsonl" 2> "$out/ab_B.err"
+  AIPSTACK_CHKSUM_SHORT_LOADS=2 AIPSTACK_CHKSUM_LDS_PAD=26000 trace long_col3 --steps 300 --warmup 0 --no-cpu-baseline --no-ceiling
+  AIPSTACK_CHKSUM_SHORT_LOADS=2 timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv \
+      -d "$out/pmc_A_col" -o run --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD \
+      SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES -- python3 bench.py --config A \
+      --no-cpu-baseline --no-parity --no-ceiling --steps 5 --warmup 2 > "$out/pmc_A_col.log" 2>&1
+  timeout -k 10 120 tools/build/hbm_peak trace 1 > "$out/read_trace.jsonl"
+  ;;
 *)
   echo "unknown mode $mode"; exit 2 ;;
 esac
