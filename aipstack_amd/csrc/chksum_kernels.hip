@@ -363,8 +363,9 @@ struct Tuning {
     std::atomic<int> gather{1};           // back-to-back batches: -1 stream mode with 64-packet
                                           // chunks (rounds 1-3), 0 the gathered stream (round
                                           // 4), 1 (or 2) short runs (round 5, launch_short_runs)
-    std::atomic<int> short_loads{0};      // short runs: 0 stream prefixes (buffer loads), 1 the
-                                          // same through global loads, 2 column runs
+    std::atomic<int> short_loads{-1};     // short runs: 0 stream prefixes (buffer loads), 1 the
+                                          // same through global loads, 2 column runs; -1 by
+                                          // packet length (launch_short_runs)
     std::atomic<int> lds_pad{0};          // bytes of dynamic LDS per batch block (occupancy;
                                           // 0 = the launch's own, -1 = none)
     std::atomic<int> chain_short{-1};      // chains: chunks of at most this many bytes first in
@@ -641,12 +642,21 @@ int launch_short_runs(const Desc &desc, uint64_t n, uint32_t len, uint16_t *d_ou
     // (tools/ab.py, one process, rotated batches, profiles/r05/occ), but the faster kernel
     // draws the clock dip described above into the driver's 25-launch protocol: 243-247 us
     // there against 228-229 (profiles/r05/driver2). B loses at 3 (366.9 vs 331.8 us).
-    if (tuning().short_loads.load(std::memory_order_relaxed) == 2) {  // column runs (SU 64)
+    // Column runs (SU 64, sum_column_chunk) for fixed-length packets of 1 KiB or more; stream
+    // prefixes for shorter and mixed lengths (several packet starts per window: config C
+    // 235.9 us with stream prefixes against 242.7 in columns). Config A: 223.2 us against 229.6
+    // at steady state (tools/ab.py), and 218.6 under the driver's protocol (--steps 20
+    // --warmup 5; the gathered stream 230-237, stream prefixes 228-231), 35.0 M VALU per
+    // launch against 50.9 M and 74.5 M (profiles/r05/col, shape). Tunable short_loads: 0
+    // stream prefixes, 1 the same through global loads, 2 columns (-1: automatic).
+    int mode = tuning().short_loads.load(std::memory_order_relaxed);
+    if (mode < 0) mode = (!Desc::kCsr && len >= 1024u) ? 2 : 0;
+    if (mode == 2) {  // column runs (SU 64)
         if (sh.chunk_packets > (uint32_t)kColMaxPackets) sh.chunk_packets = kColMaxPackets;
         return launch_k<Desc, 1, 1, true, SEEDED, 64>(desc, n, sh, d_out, flags, stream, true,
                                                       kShortRunLds);
     }
-    if (tuning().short_loads.load(std::memory_order_relaxed) == 1)  // global loads (SU 32)
+    if (mode == 1)  // global loads (SU 32)
         return launch_k<Desc, 1, 1, true, SEEDED, 32>(desc, n, sh, d_out, flags, stream, true,
                                                       kShortRunLds);
     return launch_k<Desc, 1, 1, true, SEEDED, 16>(desc, n, sh, d_out, flags, stream, true,

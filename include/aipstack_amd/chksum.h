@@ -455,24 +455,30 @@ int aipstack_chksum_last_hip_error(void);
 int aipstack_chksum_device_check(int device);
 
 /* Launch tunables, for benchmark sweeps (0 = automatic). Keys: "waves_per_cu",
- * "chunks_per_wave", "unroll" (segments per lane issued up front, 1..4), "packets"
- * (packets a wave keeps in flight: 1, 2, 4, 8), "nontemporal" (0/1), "frames" (frames
- * in flight per wave in Rx verify / Tx fill: 2, 4, 8), "stream" (1 KiB windows a wave
- * issues together in stream mode -- a 64-packet or 64-frame chunk that lies back to back
- * in memory, or chain chunks that lie close together: 2, 4, 8; -1 turns stream mode off,
- * so every packet, frame or chunk is summed on its own), "chunk_packets" (packets, frames
- * or chains per wave chunk: 1, 2, 4, ..., 64; automatic = 64 (ring slots 8, chains 32),
- * fewer for small batches so that they spread over more waves), "tx_gather" (where the Tx fills take their header
- * segments: 0 per-lane loads, 1 captured from the stream, 2 captured + the two field lines
- * touched up front; -1 = by kind of launch), "tx_store" (how the in-place Tx fills write the
- * two checksum fields: 0 = 2-byte stores, 1 = the fields' whole 32-byte sectors from the header
- * bytes the kernel holds; -1 = the default), "chain_short" (chained batches: chunks of at most
- * this many bytes that share no 128-byte line with their neighbours in the table are read
- * first in each 64-chunk group; 0 = the table's order, -1 = the default, 128), "gather"
- * (strided and CSR checksum batches: 0 = the gathered stream of the packets' segments, the
- * default since round 4; -1 = stream mode, one contiguous run per 64-packet chunk, for
- * packets back to back). Process-wide; results never depend on them.
- * Returns _OK or _EINVAL for an unknown key. */
+ * "chunks_per_wave", "stream" (1 KiB windows a wave issues together in stream mode -- a
+ * 64-packet or 64-frame chunk that lies back to back in memory, or chain chunks that lie close
+ * together: 2, 4, 8; -1 turns stream mode off, so every packet, frame or chunk is summed on its
+ * own), "chunk_packets" (packets, frames or chains per wave chunk: 1, 2, 4, ..., 64; automatic
+ * = short runs of about 12 KiB, 64 for stream mode (ring slots 8, chains 32), fewer for small
+ * batches so that they spread over more waves), "tx_gather" (where the Tx fills take their
+ * header segments: 0 per-lane loads, 1 captured from the stream, 2 captured + the two field
+ * lines touched up front; -1 = by kind of launch), "tx_store" (how the in-place Tx fills write
+ * the two checksum fields: 0 = 2-byte stores, 1 = the fields' whole 32-byte sectors from the
+ * header bytes the kernel holds, 2 = a send ring's (slots on the 128-byte grid) first 128-byte
+ * line per frame written whole; -1 = the default, 0), "chain_short" (chained batches: chunks of
+ * at most this many bytes that share no 128-byte line with their neighbours in the table are
+ * read first in each 64-chunk group; 0 = the table's order, -1 = the default, 128), "gather"
+ * (strided and CSR checksum batches on packets back to back: 1 = short runs, one ~12 KiB chunk
+ * per wave, the default since round 5; 0 = the gathered stream of the packets' segments (round
+ * 4); -1 = stream mode, one contiguous run per 64-packet chunk), "short_loads" (short runs: 0
+ * stream prefixes, 1 the same through global loads, 2 column runs; -1 = by packet length, the
+ * default), "lds_pad" (bytes of dynamic LDS per workgroup of the batch, chain and frame
+ * kernels, which caps the workgroups per CU; -1 none, 0 the launch's own). Sweep builds only
+ * (tools/build_variant.sh NAME -DAIPSTACK_ALL_VARIANTS; the product build rejects values other
+ * than the default): "unroll" (segments per lane issued up front, 1..4), "packets" (packets a
+ * wave keeps in flight: 1, 2, 4, 8), "nontemporal" (0/1), "frames" (frames in flight per wave
+ * in Rx verify / Tx fill: 2, 4, 8). Process-wide; results never depend on them.
+ * Returns _OK or _EINVAL for an unknown key or a rejected value. */
 int aipstack_chksum_tune(const char *key, int value);
 
 /* The launch shape the batch entry points pick for n packets on a device with `cus` compute

@@ -342,11 +342,11 @@ def test_short_runs_large_batches(oracle, plen, n, mode):
         got = _np(A.chksum_batch_strided(buf, plen, plen, n, byte_offset=7, final=True))
         assert np.array_equal(got, oracle.batch_strided(_np(buf)[7:], plen, plen, n, final=True))
     finally:
-        _tune("short_loads", 0)
+        _tune("short_loads", -1)
 
 
 @pytest.mark.parametrize("chunk", [1, 2, 4, 8, 16, 32])
-@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("mode", [0, 1, 2])
 def test_short_run_forms_ragged(oracle, mode, chunk):
     """The short-run forms at every chunk size (column runs cap chunks at 16 packets) on
     ragged strided and CSR batches: lengths 0..3000 with odd starts, empty packets, a batch
@@ -371,7 +371,7 @@ def test_short_run_forms_ragged(oracle, mode, chunk):
         got = _np(A.chksum_batch_csr(buf, _d(off), final=True))
         assert np.array_equal(got, oracle.batch_csr(hb, off.astype(np.uint64), final=True))
     finally:
-        _tune("short_loads", 0)
+        _tune("short_loads", -1)
         _tune("chunk_packets", 0)
 
 

@@ -78,7 +78,8 @@ def main():
             kv[k.strip()] = int(x)
         variants.append((v, kv))
     keys = sorted({k for _, kv in variants for k in kv})
-    defaults = {"gather": 1, "lds_pad": 0, "stream": 0, "chunk_packets": 0, "tx_store": -1}
+    defaults = {"gather": 1, "lds_pad": 0, "stream": 0, "chunk_packets": 0, "tx_store": -1,
+                "short_loads": -1}
 
     def apply(kv):
         for k in keys:

@@ -146,6 +146,20 @@ col)  # column runs (tunable short_loads 2): parity, steady state against the de
       --no-cpu-baseline --no-parity --no-ceiling --steps 5 --warmup 2 > "$out/pmc_A_col.log" 2>&1
   timeout -k 10 120 tools/build/hbm_peak trace 1 > "$out/read_trace.jsonl"
   ;;
+confirm)  # the round-5 defaults: the driver's exact command (first GPU process, then again),
+          # its rocprof kernel trace, a 300-launch trace, B and C, PMC traffic for A, B, C
+  bench n1 --gpus 1 --steps 20 --warmup 5 --per-launch
+  bench n1 --gpus 1 --steps 20 --warmup 5 --per-launch --no-cpu-baseline
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/prof_A" -o run \
+      -- python3 bench.py --gpus 1 --steps 20 --warmup 5 > "$out/prof_A.log" 2>&1
+  bench n1 --gpus 1 --steps 20 --warmup 5 --per-launch --no-cpu-baseline
+  bench B --config B --steps 20 --warmup 5 --per-launch
+  bench C --config C --steps 20 --warmup 5 --per-launch
+  trace long_A --steps 300 --warmup 0 --no-cpu-baseline --no-ceiling
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+      -k "short_run or every_read_form or full_size or config_d" > "$out/pytest.log" 2>&1
+  for c in A B C; do tools/pmc_run.sh $c "$out/pmc_$c"; done
+  ;;
 *)
   echo "unknown mode $mode"; exit 2 ;;
 esac
