@@ -160,6 +160,20 @@ confirm)  # the round-5 defaults: the driver's exact command (first GPU process,
       -k "short_run or every_read_form or full_size or config_d" > "$out/pytest.log" 2>&1
   for c in A B C; do tools/pmc_run.sh $c "$out/pmc_$c"; done
   ;;
+gate)  # the whole GPU suite and smoke() on this tree; the ceiling probe's new shapes; RX and
+       # TXREC at 3 workgroups per CU (lds_pad) against their 4
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+      > "$out/pytest_gpu.log" 2>&1
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.log" 2>&1
+  timeout -k 10 120 tools/build/hbm_peak ceiling > "$out/ceiling.jsonl"
+  timeout -k 10 120 tools/build/hbm_peak ceiling >> "$out/ceiling.jsonl"
+  for i in 1 2; do
+    bench RX --config RX --steps 20 --warmup 5 --per-launch --no-cpu-baseline
+    AIPSTACK_CHKSUM_LDS_PAD=4000 bench RX_pad --config RX --steps 20 --warmup 5 --per-launch --no-cpu-baseline
+    bench TXREC --config TXREC --steps 20 --warmup 5 --per-launch --no-cpu-baseline
+    AIPSTACK_CHKSUM_LDS_PAD=4000 bench TXREC_pad --config TXREC --steps 20 --warmup 5 --per-launch --no-cpu-baseline
+  done
+  ;;
 *)
   echo "unknown mode $mode"; exit 2 ;;
 esac
