@@ -1153,6 +1153,85 @@ __device__ __forceinline__ uint32_t sum_gathered_chunks(uint64_t a, uint32_t l, 
     return from_next_lane(gsum, carry, lane) - gsum - foreign;
 }
 
+// Slot windows (round 5, SU = 128): packets that each lie on their own (ring slots, a fixed
+// length at another stride) summed without compacting their segments. Slot k's packet [S, E)
+// is read from A0 = S & ~15 as whole 1 KiB windows, lane L taking segment L of each window,
+// through a buffer descriptor of exactly its 16 * nseg bytes: lanes past the packet read 0 and
+// fetch nothing, so only the packet's own lines cross from HBM. Eight slots' first two windows
+// (packets of up to ~2 KiB) are issued together, 16 loads per wave up front; longer packets add
+// their further windows after. A lane adds its segments per slot with v_sad_u16 -- no mask and no
+// cross-lane work per window -- and the 8 x 64 partial sums are added through a transpose in LDS
+// (8 lanes per slot) and a 3-step butterfly. Each packet's first and last segment also hold
+// bytes that are not its own; lane k reads them itself before the windows (as the gathered
+// stream's edges, foreign_halves) and subtracts them. Per wave of 8 slots: 64 v_sad_u16 for the
+// windows, against a DPP scan, an owner lookup and a 64-bit address per window in the gathered
+// stream.
+constexpr int kSlotGroup = 8;            // slots whose first two windows go out together
+typedef uint32_t SlotRows[kSlotGroup * kWave];
+
+template <bool NT>
+__device__ __forceinline__ uint32_t sum_slot_windows(uint64_t S, uint64_t E, int lane, int cnt,
+                                                     uint32_t voff, uint32_t *rows) {
+    const uint64_t A0 = S & ~(uint64_t)15;
+    const uint32_t rs = (uint32_t)S & 15u;
+    const uint32_t len = lane < cnt ? (uint32_t)(E - S) : 0u;
+    const uint32_t nseg = len ? (rs + len + 15u) >> 4 : 0u;
+    const uint32_t te = ((rs + len - 1u) & 15u) + 1u;  // the packet's end in its last segment
+    // the edge segments' foreign bytes (none on a segment edge), read before the windows
+    typedef __attribute__((address_space(1))) const u32x4 gseg;
+    u32x4 fseg = {0u, 0u, 0u, 0u}, lseg = {0u, 0u, 0u, 0u};
+    if (nseg && rs != 0u) fseg = *(const gseg *)(A0);
+    if (nseg && te != 16u) lseg = *(const gseg *)(A0 + 16ull * (nseg - 1u));
+    uint32_t mine = 0;  // lane j < cnt: packet j's exact halves-sum (whole segments)
+    for (int k0 = 0; k0 < cnt; k0 += kSlotGroup) {
+        u32x4 v[kSlotGroup][2];
+        __amdgpu_buffer_rsrc_t rs_k[kSlotGroup];
+        uint32_t n_k[kSlotGroup];
+#pragma unroll
+        for (int k = 0; k < kSlotGroup; ++k) {
+            const int src = min(k0 + k, kWave - 1);
+            const uint64_t a = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(A0 >> 32), src) << 32) |
+                               (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)A0, src);
+            n_k[k] = k0 + k < cnt ? (uint32_t)__builtin_amdgcn_readlane((int)nseg, src) : 0u;
+            rs_k[k] = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(a), (short)0,
+                                                        (int)(n_k[k] * 16u), 0x00020000);
+        }
+#pragma unroll
+        for (int k = 0; k < kSlotGroup; ++k) {
+            v[k][0] = load_segment<NT>(rs_k[k], voff, 0u);
+            __builtin_amdgcn_sched_barrier(0);
+            v[k][1] = load_segment<NT>(rs_k[k], voff, 1024u);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int k = 0; k < kSlotGroup; ++k) {
+            uint32_t p = halves(v[k][0][0], halves(v[k][0][1], halves(v[k][0][2], halves(v[k][0][3], 0u))));
+            p = halves(v[k][1][0], halves(v[k][1][1], halves(v[k][1][2], halves(v[k][1][3], p))));
+            for (uint32_t w = 2; w * 64u < n_k[k]; ++w) {  // packets over ~2 KiB (uniform)
+                const u32x4 x = load_segment<NT>(rs_k[k], voff, w * 1024u);
+                p = halves(x[0], halves(x[1], halves(x[2], halves(x[3], p))));
+            }
+            rows[k * kWave + lane] = p;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        // lane t: slot t >> 3, the partials of lanes 8 (t & 7) .. 8 (t & 7) + 7
+        const u32x4 *r = reinterpret_cast<const u32x4 *>(rows + (lane >> 3) * kWave + (lane & 7) * 8);
+        const u32x4 a = r[0], b = r[1];
+        uint32_t acc = a[0] + a[1] + a[2] + a[3] + b[0] + b[1] + b[2] + b[3];
+        acc += (uint32_t)__builtin_amdgcn_ds_bpermute((lane ^ 1) << 2, (int)acc);
+        acc += (uint32_t)__builtin_amdgcn_ds_bpermute((lane ^ 2) << 2, (int)acc);
+        acc += (uint32_t)__builtin_amdgcn_ds_bpermute((lane ^ 4) << 2, (int)acc);
+        // slot k's total is on lanes 8k..8k+7: lane k0 + k takes it from lane 8k
+        const int j = lane - k0;
+        const uint32_t tot = (uint32_t)__builtin_amdgcn_ds_bpermute(((j & 7) * 8) << 2, (int)acc);
+        if (j >= 0 && j < kSlotGroup) mine = tot;
+        __builtin_amdgcn_wave_barrier();  // (the rows are rewritten by the next group)
+    }
+    const uint32_t foreign = nseg ? foreign_halves(fseg, lseg, (int)rs, (int)te) : 0u;
+    return lane < cnt ? mine - foreign : 0u;
+}
+
 // Stream mode for one chunk (stream_ok). Lane j < cnt holds packet j = [S, E); returns
 // lane j's exact halves-sum (0 on lanes >= cnt).
 // SU <= 8: SU windows issued together, the next group after the current one is summed (rounds

@@ -74,7 +74,10 @@ __global__ __launch_bounds__(kBlock) void chksum_batch_kernel(Desc desc, uint64_
     // Ring slots with SU > 0: the chunk's 64 packets read as ONE gathered stream of just
     // their 16-byte segments (the chain kernel's loader, chksum_device.h), 1 KiB per wave
     // instruction however short the packets are, instead of one packet per wave instruction.
-    constexpr bool kGathered = !Desc::kStream && SU > 0;
+    // SU = 128 (slot windows, sum_slot_windows): each packet read on its own, no compaction
+    constexpr bool kSlotWin = !Desc::kStream && SU == 128;
+    constexpr bool kGathered = !Desc::kStream && SU > 0 && !kSlotWin;
+    __shared__ typename std::conditional<kSlotWin, SlotRows[kWavesPerBlock], char>::type slot_rows;
     struct GatheredShared {
         GatherLds g[kWavesPerBlock];
         KeepTable keep;
@@ -105,7 +108,10 @@ __global__ __launch_bounds__(kBlock) void chksum_batch_kernel(Desc desc, uint64_
         // lane j: exact halves-sum of packet j (0 iff all its bytes are 0)
         uint32_t sums = 0;
         bool streamed = false;
-        if constexpr (kGathered) {
+        if constexpr (kSlotWin) {
+            sums = sum_slot_windows<NT>(lS, lE, lane, cnt, voff, slot_rows[wave_in_block]);
+            streamed = true;
+        } else if constexpr (kGathered) {
             // (CSR: every packet within the contract, else the wave mode below)
             if (!Desc::kCsr || __builtin_amdgcn_ballot_w64(lE - lS > (uint64_t)AIPSTACK_CHKSUM_MAX_LEN) == 0) {
                 sums = sum_gathered_chunks<SU, NT, Desc::kEdge>(lS, (uint32_t)(lE - lS), lane,
@@ -366,6 +372,7 @@ struct Tuning {
     std::atomic<int> short_loads{-1};     // short runs: 0 stream prefixes (buffer loads), 1 the
                                           // same through global loads, 2 column runs; -1 by
                                           // packet length (launch_short_runs)
+    std::atomic<int> slot_windows{0};     // ring slots / gaps: 1 = slot windows (SU 128)
     std::atomic<int> lds_pad{0};          // bytes of dynamic LDS per batch block (occupancy;
                                           // 0 = the launch's own, -1 = none)
     std::atomic<int> chain_short{-1};      // chains: chunks of at most this many bytes first in
@@ -397,6 +404,7 @@ struct Tuning {
         env("AIPSTACK_CHKSUM_GATHER", gather);
         env("AIPSTACK_CHKSUM_SHORT_LOADS", short_loads);
         env("AIPSTACK_CHKSUM_LDS_PAD", lds_pad);
+        env("AIPSTACK_CHKSUM_SLOT_WINDOWS", slot_windows);
         env("AIPSTACK_ENGINE_ZERO_COPY", engine_zero_copy);
         env("AIPSTACK_ENGINE_ZERO_COPY_SMALL", engine_zero_copy_small);
         env("AIPSTACK_ENGINE_PAGEABLE_ROWS", engine_pageable_rows);
@@ -587,6 +595,12 @@ int launch(const Desc &desc, uint64_t n, uint32_t max_len, uint16_t *d_out, uint
         // 243.4; profiles/r04/su8)
         const int su = tuning_stream_windows(
             std::is_same<Desc, GappedDesc>::value && max_len >= 1024u ? 8 : 4);
+        // slot windows (SU 128, sum_slot_windows): tunable slot_windows = 1 (device-memory
+        // slots and gaps; the host-memory form keeps the masked gathered stream)
+        if constexpr (Desc::kEdge) {
+            if (su != 0 && tuning().slot_windows.load(std::memory_order_relaxed) == 1)
+                return launch_k<Desc, 1, 1, true, SEEDED, 128>(desc, n, sh, d_out, flags, stream);
+        }
         if (su == 4) return launch_k<Desc, 1, 1, true, SEEDED, 4>(desc, n, sh, d_out, flags, stream);
         if (su == 8) return launch_k<Desc, 1, 1, true, SEEDED, 8>(desc, n, sh, d_out, flags, stream);
         if (su != 0) return launch_k<Desc, 1, 1, true, SEEDED, 2>(desc, n, sh, d_out, flags, stream);
@@ -882,6 +896,7 @@ extern "C" int aipstack_chksum_tune(const char *key, int value) {
     else if (!std::strcmp(key, "gather")) t.gather = value;
     else if (!std::strcmp(key, "lds_pad")) t.lds_pad = value;
     else if (!std::strcmp(key, "short_loads")) t.short_loads = value;
+    else if (!std::strcmp(key, "slot_windows")) t.slot_windows = value;
     else if (!std::strcmp(key, "engine_zero_copy")) t.engine_zero_copy = value;
     else if (!std::strcmp(key, "engine_zero_copy_small")) t.engine_zero_copy_small = value;
     else if (!std::strcmp(key, "engine_pageable_rows")) t.engine_pageable_rows = value;

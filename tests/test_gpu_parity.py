@@ -1176,6 +1176,65 @@ def test_slotted_checksums(oracle, stream_mode, stride, su):
     assert np.array_equal(fin, oracle.batch_slotted(ring[:n * stride], stride, lens, final=True))
 
 
+@pytest.fixture
+def slot_windows():
+    """Setter for the slot_windows tunable (1 = slot windows, 0 = the gathered stream);
+    restores the default afterwards."""
+    yield lambda v: _tune("slot_windows", v)
+    _tune("slot_windows", 0)
+
+
+@pytest.mark.parametrize("chunk", [0, 1, 8, 16, 64])
+@pytest.mark.parametrize("stride", [64, 1517, 2048, 9216, 65536])
+def test_slot_windows(oracle, slot_windows, stride, chunk):
+    """Slot windows (sum_slot_windows, tunable slot_windows = 1): each packet read on its own
+    through a descriptor of exactly its segments, two windows per slot up front, further
+    windows for longer packets; lengths 0..min(stride, 65535) at the alignments an odd stride
+    and a shifted base give, random slack; the same form on fixed lengths at a gap
+    (aipstack_chksum_batch_strided with stride != length, overlapping strides included) and on
+    CSR packets; every chunk size."""
+    slot_windows(1)
+    _tune("chunk_packets", chunk)
+    try:
+        rng = np.random.default_rng(stride + chunk)
+        n = {64: 20000, 1517: 8000, 2048: 8000, 9216: 1500, 65536: 200}[stride]
+        cap = min(stride, 65535)
+        lens = rng.integers(0, cap + 1, n).astype(np.uint32)
+        lens[:8] = [0, 1, 2, cap, cap - 1, 15, 16, 17][:8] if cap > 17 else lens[:8]
+        ring = synth.random_bytes(stride + 11, n * stride + 16)
+        ring[: 2 * stride] = 0xFF
+        dring = _d(ring)
+        for base in (0, 5):
+            view = ring[base:base + n * stride]
+            got = _np(A.chksum_batch_slotted(dring[base:base + n * stride], stride,
+                                             _d(lens.view(np.int32)), final=(base == 5)))
+            assert np.array_equal(got, oracle.batch_slotted(np.ascontiguousarray(view), stride,
+                                                            lens, final=(base == 5)))
+        plen = min(stride - 1, 1500) if stride > 1 else 1
+        for st, ln in ((stride, plen), (7, 1500), (1, 3000)):
+            m = min(n, (ring.size - 16 - ln) // max(st, 1))
+            got = _np(A.chksum_batch_strided(dring, st, ln, m, byte_offset=3))
+            assert np.array_equal(got, oracle.batch_strided(ring[3:], st, ln, m)), (st, ln)
+    finally:
+        _tune("chunk_packets", 0)
+
+
+def test_slot_windows_full_size(oracle, slot_windows):
+    """Slot windows on 1 M config-C packets in 2048-B slots and config A's packets in
+    2048-B slots (A2K), whole batches against the oracle."""
+    slot_windows(1)
+    n = 1 << 20
+    buf, off = synth.mixed_batch(n)
+    ring, lens = synth.to_slots(buf, off, 2048)
+    got = _np(A.chksum_batch_slotted(_d(ring), 2048, _d(lens.view(np.int32))))
+    assert np.array_equal(got, oracle.batch_slotted(ring, 2048, lens))
+    del ring, buf
+    b = torch.empty(n * 2048, dtype=torch.uint8, device=DEV)
+    synth.fill_device(b, 97)
+    got = _np(A.chksum_batch_strided(b, 2048, 1500, n))
+    assert np.array_equal(got, oracle.batch_strided(_np(b), 2048, 1500, n))
+
+
 def test_slotted_full_size_1m(oracle):
     """1 M config-C packets (64-1500 B, odd lengths, all-0x00/0xFF/sum-0 classes) in 2048-B
     ring slots, and 1 M raw frames in 2048-B slots through Rx verify: whole batch vs oracle."""

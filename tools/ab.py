@@ -25,7 +25,7 @@ sys.path.insert(0, ROOT)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", default="A", choices=["A", "B", "C", "A2K"])
+    ap.add_argument("--config", default="A", choices=["A", "B", "C", "A2K", "C2K"])
     ap.add_argument("--variants", required=True)
     ap.add_argument("--rounds", type=int, default=20)
     ap.add_argument("--reps", type=int, default=5)
@@ -45,7 +45,24 @@ def main():
     total = spec["total"]
     bufs, wants = [], []
     d_off = torch.from_numpy(spec["offsets"]).to(dev) if layout == "csr" else None
-    for r in range(args.rotate):
+    d_lens = None
+    if layout == "csrslot":  # config C's packets in 2048-B ring slots, one ring per rotation
+        orc = bench.ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "libchksum_oracle.so"))
+        orc.oracle_batch_slotted.argtypes = [bench.ctypes.c_void_p, bench.ctypes.c_uint64,
+                                             bench.ctypes.c_void_p, bench.ctypes.c_uint64,
+                                             bench.ctypes.c_void_p, bench.ctypes.c_uint32]
+        for r in range(args.rotate):
+            sp = dict(spec, data_seed=synth.SEED_DATA + r)
+            ring, lens = synth.to_slots(bench.host_shard(sp), spec["offsets"], 2048,
+                                        slack_seed=99 + r)
+            bufs.append(torch.from_numpy(ring).to(dev))
+            w = np.empty(n, dtype=np.uint16)
+            orc.oracle_batch_slotted(ring.ctypes.data, 2048, lens.ctypes.data, n, w.ctypes.data, 0)
+            wants.append(w)
+        d_lens = torch.from_numpy(lens.view(np.int32)).to(dev)
+        total = int(lens.sum(dtype=np.uint64))
+        spec["payload"] = total
+    for r in range(args.rotate if layout != "csrslot" else 0):
         b = torch.empty(total, dtype=torch.uint8, device=dev)
         synth.fill_device(b, synth.SEED_DATA + r, spec["byte_offset"])
         if layout == "csr":
@@ -79,7 +96,7 @@ def main():
         variants.append((v, kv))
     keys = sorted({k for _, kv in variants for k in kv})
     defaults = {"gather": 1, "lds_pad": 0, "stream": 0, "chunk_packets": 0, "tx_store": -1,
-                "short_loads": -1}
+                "short_loads": -1, "slot_windows": 0}
 
     def apply(kv):
         for k in keys:
@@ -88,7 +105,9 @@ def main():
                 raise SystemExit(f"tune {k}={val} rejected")
 
     def launch(r):
-        if layout == "csr":
+        if layout == "csrslot":
+            A.chksum_batch_slotted(bufs[r], 2048, d_lens, out=out, stream=stream)
+        elif layout == "csr":
             A.chksum_batch_csr(bufs[r], d_off, out=out, stream=stream)
         else:
             A.chksum_batch_strided(bufs[r], stride, plen, n, out=out, stream=stream)

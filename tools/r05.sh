@@ -174,6 +174,27 @@ gate)  # the whole GPU suite and smoke() on this tree; the ceiling probe's new s
     AIPSTACK_CHKSUM_LDS_PAD=4000 bench TXREC_pad --config TXREC --steps 20 --warmup 5 --per-launch --no-cpu-baseline
   done
   ;;
+slot)  # slot windows (tunable slot_windows 1) on ring slots and gaps: parity, steady state
+       # against the gathered stream, the driver's protocol, instruction mix
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+      -k "slot_windows or slotted_checksums or slotted_packets or overlapping" > "$out/pytest.log" 2>&1
+  timeout -k 10 600 python3 tools/ab.py --config C2K --rounds 10 --variants \
+      "slot_windows=0;slot_windows=1;slot_windows=1,chunk_packets=16;slot_windows=1,chunk_packets=4" \
+      > "$out/ab_C2K.jsonl" 2> "$out/ab_C2K.err"
+  timeout -k 10 600 python3 tools/ab.py --config A2K --rounds 10 --variants \
+      "slot_windows=0;slot_windows=1;slot_windows=1,chunk_packets=16" > "$out/ab_A2K.jsonl" 2> "$out/ab_A2K.err"
+  for sw in 0 1; do
+    AIPSTACK_CHKSUM_SLOT_WINDOWS=$sw bench C2K_sw$sw --config C2K --steps 20 --warmup 5 --per-launch --no-cpu-baseline
+    AIPSTACK_CHKSUM_SLOT_WINDOWS=$sw bench A2K_sw$sw --config A2K --steps 20 --warmup 5 --per-launch --no-cpu-baseline
+    AIPSTACK_CHKSUM_SLOT_WINDOWS=$sw timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv \
+        -d "$out/pmc_C2K_sw$sw" -o run --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD \
+        SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES -- python3 bench.py --config C2K \
+        --no-cpu-baseline --no-parity --steps 5 --warmup 2 > "$out/pmc_C2K_sw$sw.log" 2>&1
+    AIPSTACK_CHKSUM_SLOT_WINDOWS=$sw timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv \
+        -d "$out/pmcf_C2K_sw$sw" -o run --pmc FETCH_SIZE -- python3 bench.py --config C2K \
+        --no-cpu-baseline --no-parity --steps 5 --warmup 2 > "$out/pmcf_C2K_sw$sw.log" 2>&1
+  done
+  ;;
 *)
   echo "unknown mode $mode"; exit 2 ;;
 esac
