@@ -4,7 +4,10 @@
 A "step" is one pass of the hot path -- one batched checksum launch
 (aipstack_chksum_batch_strided / _csr of libaipstack_chksum.so) over one batch of
 synthetic packets already resident in HBM. Default workload = BASELINE.json configs[1]
-(config A): 1 M x 1500-byte packets per GPU.
+(config A): 1 M x 1500-byte packets per GPU. For A, B and C the timed loop rotates over
+R = 3 distinct resident batches (--rotate; step k reads batch k mod R, every batch checked),
+so that no launch finds its bytes in the 256 MiB Infinity Cache; the line also
+carries the same box's measured streaming-read ceiling (roofline.measured_peak).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config A|B|C]
     torchrun --nproc-per-node N ... bench.py --gpus N     (one rank per GPU)
