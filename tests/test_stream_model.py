@@ -426,3 +426,120 @@ def _exact_halves(buf, s, e):
     raw = np.zeros(hi - lo, dtype=np.uint8)
     raw[s - lo:e - lo] = buf[s:e]
     return int(raw.view("<u2").astype(np.uint64).sum())
+
+
+# ---- column runs (round 5, sum_column_chunk) -------------------------------------------
+
+def column_chunk_model(buf, S, E, cnt, cpk):
+    """sum_column_chunk, step for step: each lane's column sum C_L over the windows consumed,
+    the boundary rows X_{j,L} = C_L + (L < B_j ? s_L : 0) written when boundary j's window is
+    consumed (the rest after the last window), the per-boundary partial P_j from its own
+    segment, then packet j = sum_L (X_{j+1,L} - X_{j,L}) + P_{j+1} - P_j, all mod 2^32; the
+    reduction as the kernel does it (64 / cpk lanes per packet, cpk columns each)."""
+    X1 = int(E[cnt - 1])
+    b = [int(S[j]) if j < cnt else X1 for j in range(64)]
+    A = b[0] & ~15
+    nseg = (X1 - A + 15) >> 4
+    nwin = (nseg + 63) >> 6
+    seg, raw = _halves_of_segments(buf, A, max(nwin * 64, 1), nseg * 16)
+    g = [(x - A) >> 4 for x in b]
+    o = [(x - A) & 15 for x in b]
+    rows = np.zeros((cnt + 1, 64), dtype=np.uint64)
+    C = np.zeros(64, dtype=np.uint64)
+    jb = 0
+    for w in range(nwin):
+        s = seg[w * 64:(w + 1) * 64].astype(np.uint64)
+        while jb <= cnt and (g[jb] >> 6) == w:
+            B = g[jb] & 63
+            rows[jb] = (C + np.where(np.arange(64) < B, s, 0)) & M32
+            jb += 1
+        C = (C + s) & M32
+    while jb <= cnt:
+        rows[jb] = C
+        jb += 1
+    P = [(_below(raw[g[j] * 16:g[j] * 16 + 16], o[j]) if (j <= cnt and o[j]) else 0)
+         for j in range(64)]
+    q = 64 // cpk
+    sums = []
+    for j in range(cnt):
+        acc = 0
+        for part in range(q):  # 64 / cpk lanes, cpk columns each, then the butterfly
+            cols = range(part * cpk, (part + 1) * cpk)
+            acc += sum(int(rows[j + 1][c]) - int(rows[j][c]) for c in cols)
+        sums.append((acc + P[j + 1] - P[j]) & M32)
+    return sums + [0] * (64 - cnt)
+
+
+@pytest.mark.parametrize("cpk", [1, 2, 4, 8, 16])
+@pytest.mark.parametrize("case", ["tiny", "mixed", "mtu", "jumbo", "aligned_end"])
+def test_column_model_matches_oracle(oracle, case, cpk):
+    rng = np.random.default_rng(hash((case, cpk, "col")) % 2**32)
+    base = int(rng.integers(0, 16))
+    if case == "tiny":
+        off = _layout(rng, 100, [0, 0, 1, 2, 3, 5, 7, 16, 17, 31], base)
+    elif case == "mixed":
+        off = _layout(rng, 100, list(range(64, 1501, 97)) + [65, 1499], base)
+    elif case == "mtu":
+        off = _layout(rng, 64, [1500], base)
+    elif case == "jumbo":
+        off = _layout(rng, 20, [9000, 65535, 0, 1], base)
+    else:                       # the run ending exactly on a window edge (X1 past the loop)
+        lens = np.array([1024] * 16, dtype=np.int64)
+        off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    buf = rng.integers(0, 256, size=int(off[-1]) + 64, dtype=np.uint8)
+    for j in range(0, off.size - 1, 7):
+        buf[off[j]:off[j + 1]] = 0 if j % 2 else 0xFF
+    n = off.size - 1
+    got = np.zeros(n, dtype=np.uint16)
+    for p0 in range(0, n, cpk):
+        cnt = min(cpk, n - p0)
+        S = [int(off[p0 + j]) for j in range(cnt)]
+        E = [int(off[p0 + j + 1]) for j in range(cnt)]
+        got[p0:p0 + cnt] = finish(column_chunk_model(buf, S, E, cnt, cpk)[:cnt], S)
+    want = oracle.batch_csr(buf, off)
+    assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
+
+
+# ---- slot windows (round 5, sum_slot_windows) ------------------------------------------
+
+def slot_windows_model(buf, S, E, cnt):
+    """sum_slot_windows: each packet's whole segments from A0 = S & ~15 (a descriptor of
+    exactly nseg segments: lanes past it read 0), lane partials per slot added in groups of 8
+    slots, minus the foreign bytes of the packet's first and last segment."""
+    out = []
+    for j in range(cnt):
+        s, e = int(S[j]), int(E[j])
+        ln = e - s
+        if ln == 0:
+            out.append(0)
+            continue
+        a0 = s & ~15
+        rs = s & 15
+        nseg = (rs + ln + 15) >> 4
+        te = ((rs + ln - 1) & 15) + 1
+        seg, raw = _halves_of_segments(buf, a0, max(((nseg + 63) >> 6) * 64, 1), nseg * 16)
+        lanes = [int(seg[L::64].sum()) for L in range(64)]  # each lane's windows
+        whole = sum(lanes) & M32
+        first = raw[:16]
+        last = raw[(nseg - 1) * 16:nseg * 16]
+        foreign = _below(first, rs) + (int(last.view("<u2").astype(np.uint64).sum())
+                                       - _below(last, te))
+        out.append((whole - foreign) & M32)
+    return out
+
+
+@pytest.mark.parametrize("stride", [64, 1517, 2048, 9216])
+def test_slot_windows_model_matches_oracle(oracle, stride):
+    rng = np.random.default_rng(stride)
+    n = 300
+    cap = min(stride, 65535)
+    lens = rng.integers(0, cap + 1, n).astype(np.uint32)
+    lens[:6] = [0, 1, 15, 16, 17, cap]
+    base = 5
+    ring = rng.integers(0, 256, size=n * stride + base + 32, dtype=np.uint8)
+    ring[base:base + stride] = 0xFF
+    S = [base + i * stride for i in range(n)]
+    E = [S[i] + int(lens[i]) for i in range(n)]
+    got = finish(slot_windows_model(ring, S, E, n), S)
+    want = oracle.batch_slotted(np.ascontiguousarray(ring[base:base + n * stride]), stride, lens)
+    assert np.array_equal(np.array(got, dtype=np.uint16), want)
