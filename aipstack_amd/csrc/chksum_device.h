@@ -86,6 +86,12 @@ __device__ __forceinline__ uint32_t from_next_lane(uint32_t v, uint32_t last, in
     return (uint32_t)__builtin_amdgcn_ds_bpermute(((lane + 1) & 63) << 2, (int)src);
 }
 
+// Lane l's 64-bit v, wave-uniform.
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+}
+
 struct StridedDesc {
     static constexpr bool kCsr = false;
     static constexpr bool kStream = true;  // SU > 0: stream mode for back-to-back chunks
@@ -1153,6 +1159,90 @@ __device__ __forceinline__ uint32_t sum_gathered_chunks(uint64_t a, uint32_t l, 
     return from_next_lane(gsum, carry, lane) - gsum - foreign;
 }
 
+// Segment-table runs (round 5, SU = 96): the run read as in column runs, and each window's 64
+// segment sums written to a per-wave LDS table (one ds_write_b32 per window); no per-boundary
+// work in the stream at all. After it, packet j's whole segments [g_j, g_{j+1}) are added from
+// the table by its 64 / cp lanes (a contiguous share each), then a butterfly, and the partial
+// segments at both ends as in column runs: + P_{j+1} - P_j. Runs longer than kSegTabMax
+// segments (chunks of very long packets) take the per-packet wave mode.
+constexpr uint32_t kSegTabMax = 1536;  // 24 windows: 16 packets of up to ~1.5 KiB
+typedef uint32_t SegTab[kSegTabMax];
+
+template <bool NT>
+__device__ __forceinline__ uint32_t sum_segtab_chunk(uint64_t S, uint64_t E, int lane, int cnt,
+                                                     uint32_t voff, uint32_t cpk, uint32_t *tab) {
+    const uint64_t X1 = readlane64(E, cnt - 1);
+    if (lane >= cnt) S = X1;
+    const uint64_t A =
+        (((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(S >> 32)) << 32) |
+         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)S)) & ~(uint64_t)15;
+    const uint32_t nseg = ((uint32_t)(X1 - A) + 15u) >> 4;  // <= kSegTabMax (caller)
+    const uint32_t nwin = (nseg + (uint32_t)kWave - 1u) >> 6;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void *>(A), (short)0, (int)(nseg * 16u), 0x00020000);
+    const uint32_t rel = (uint32_t)(S - A);
+    const uint32_t g = rel >> 4, o = rel & 15u;
+    u32x4 bseg = {0u, 0u, 0u, 0u};
+    if (lane <= cnt && o != 0u) bseg = load_segment<false>(rsrc, g * 16u, 0u);
+    constexpr int U = 8;
+    u32x4 va[U], vb[U];
+    auto issue = [&](u32x4 (&v)[U], uint32_t w) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            v[u] = load_segment<NT>(rsrc, voff, (w + (uint32_t)u) * 1024u);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+    auto consume = [&](const u32x4 (&v)[U], uint32_t w) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t wu = w + (uint32_t)u;
+            if (wu >= nwin) break;
+            tab[wu * kWave + (uint32_t)lane] =
+                halves(v[u][0], halves(v[u][1], halves(v[u][2], halves(v[u][3], 0u))));
+        }
+    };
+    const uint32_t groups = (nwin + U - 1u) / U;
+    issue(va, 0);
+    uint32_t gi = 0;
+    for (; gi + 2u < groups; gi += 2u) {
+        issue(vb, (gi + 1u) * U);
+        consume(va, gi * U);
+        issue(va, (gi + 2u) * U);
+        consume(vb, (gi + 1u) * U);
+    }
+    if (gi + 2u == groups) {
+        issue(vb, (gi + 1u) * U);
+        consume(va, gi * U);
+        consume(vb, (gi + 1u) * U);
+    } else {
+        consume(va, gi * U);
+    }
+    const uint32_t P = halves_below_seg(bseg, o);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    // packet j = lane >> ql: segments [g_j, g_{j+1}) in 2^ql contiguous shares
+    const uint32_t ql = 6u - (uint32_t)__builtin_ctz(cpk);  // cpk: a power of two <= 32
+    const uint32_t j = (uint32_t)lane >> ql, part = (uint32_t)lane & ((1u << ql) - 1u);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(min(j, 63u) << 2), (int)g);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(min(j + 1u, 63u) << 2), (int)g);
+    uint32_t acc = 0;
+    if (j < (uint32_t)cnt) {
+        const uint32_t per = ((hi - lo) + (1u << ql) - 1u) >> ql;
+        const uint32_t a = lo + part * per;
+        const uint32_t b = min(a + per, hi);
+        for (uint32_t k = a; k < b; ++k) acc += tab[k];
+    }
+    for (uint32_t m = 1; m < (1u << ql); m <<= 1)
+        acc += (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((uint32_t)lane ^ m) << 2), (int)acc);
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t col = (uint32_t)__builtin_amdgcn_ds_bpermute(
+        (int)((((uint32_t)lane << ql) & 63u) << 2), (int)acc);
+    const uint32_t pn = from_next_lane(P, 0u, lane);  // P_{j+1} (lane cnt: X1's)
+    __builtin_amdgcn_wave_barrier();  // (the table is rewritten by the next chunk)
+    return lane < cnt ? col + pn - P : 0u;
+}
+
 // Slot windows (round 5, SU = 128): packets that each lie on their own (ring slots, a fixed
 // length at another stride) summed without compacting their segments. Slot k's packet [S, E)
 // is read from A0 = S & ~15 as whole 1 KiB windows, lane L taking segment L of each window,
@@ -1280,11 +1370,6 @@ __device__ __forceinline__ uint32_t sum_stream_chunk(uint64_t S, uint64_t E, int
 // (stream mode: a 6-step DPP scan per window and 5 ds_bpermute per boundary).
 constexpr int kColMaxPackets = 16;
 typedef uint32_t ColRows[(kColMaxPackets + 1) * kWave];
-
-__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
-    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32) |
-           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
-}
 
 template <bool NT>
 __device__ __forceinline__ uint32_t sum_column_chunk(uint64_t S, uint64_t E, int lane, int cnt,

@@ -85,6 +85,8 @@ __global__ __launch_bounds__(kBlock) void chksum_batch_kernel(Desc desc, uint64_
     __shared__ typename std::conditional<kGathered, GatheredShared, char>::type gsh;
     constexpr bool kColumns = Desc::kStream && SU == 64;  // column runs (sum_column_chunk)
     __shared__ typename std::conditional<kColumns, ColRows[kWavesPerBlock], char>::type col_rows;
+    constexpr bool kSegTab = Desc::kStream && SU == 96;   // segment tables (sum_segtab_chunk)
+    __shared__ typename std::conditional<kSegTab, SegTab[kWavesPerBlock], char>::type seg_tab;
     if constexpr (kGathered) {
         if constexpr (!Desc::kEdge) {  // edges masked in the stream: the mask table
             fill_keep_table(gsh.keep);
@@ -119,9 +121,17 @@ __global__ __launch_bounds__(kBlock) void chksum_batch_kernel(Desc desc, uint64_
                 streamed = true;
             }
         } else if constexpr (SU > 0) {
-            if (stream_ok(lS, lE, lane, cnt)) {
+            if (stream_ok(lS, lE, lane, cnt) &&
+                (!kSegTab ||
+                 ((uint32_t)(readlane64(lE, cnt - 1) -
+                             (((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(lS >> 32)) << 32) |
+                              ((uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)lS) & ~15u))) +
+                  15u) >> 4 <= kSegTabMax)) {
                 // back-to-back packets: the chunk read as one contiguous run
-                if constexpr (kColumns)
+                if constexpr (kSegTab)
+                    sums = sum_segtab_chunk<NT>(lS, lE, lane, cnt, voff, chunk_packets,
+                                                seg_tab[wave_in_block]);
+                else if constexpr (kColumns)
                     sums = sum_column_chunk<NT>(lS, lE, lane, cnt, voff, chunk_packets,
                                                 col_rows[wave_in_block]);
                 else
@@ -665,6 +675,11 @@ int launch_short_runs(const Desc &desc, uint64_t n, uint32_t len, uint16_t *d_ou
     // stream prefixes, 1 the same through global loads, 2 columns (-1: automatic).
     int mode = tuning().short_loads.load(std::memory_order_relaxed);
     if (mode < 0) mode = (!Desc::kCsr && len >= 1024u) ? 2 : 0;
+    if (mode == 3) {  // segment tables (SU 96): lane cnt holds the run's end, so cnt < 64
+        if (sh.chunk_packets > 32u) sh.chunk_packets = 32u;
+        return launch_k<Desc, 1, 1, true, SEEDED, 96>(desc, n, sh, d_out, flags, stream, true,
+                                                      kShortRunLds);
+    }
     if (mode == 2) {  // column runs (SU 64)
         if (sh.chunk_packets > (uint32_t)kColMaxPackets) sh.chunk_packets = kColMaxPackets;
         return launch_k<Desc, 1, 1, true, SEEDED, 64>(desc, n, sh, d_out, flags, stream, true,

@@ -329,12 +329,12 @@ def test_strided_and_csr_in_every_read_form(oracle, gather, chunk):
         _tune("chunk_packets", 0)
 
 
-@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
 @pytest.mark.parametrize("plen,n", [(64, 300000), (1500, 270000), (9000, 40000)])
 def test_short_runs_large_batches(oracle, plen, n, mode):
     """Back-to-back strided batches large enough for the default short-run shape (one chunk of
     ~12 KiB per wave), at an odd base, against the oracle: stream prefixes through buffer loads
-    (tunable short_loads 0) or global loads (1), and column runs (2)."""
+    (tunable short_loads 0) or global loads (1), column runs (2) and segment tables (3)."""
     _tune("short_loads", mode)
     try:
         buf = torch.empty(n * plen + 7, dtype=torch.uint8, device=DEV)
@@ -346,11 +346,12 @@ def test_short_runs_large_batches(oracle, plen, n, mode):
 
 
 @pytest.mark.parametrize("chunk", [1, 2, 4, 8, 16, 32])
-@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
 def test_short_run_forms_ragged(oracle, mode, chunk):
-    """The short-run forms at every chunk size (column runs cap chunks at 16 packets) on
-    ragged strided and CSR batches: lengths 0..3000 with odd starts, empty packets, a batch
-    that ends mid-chunk, all-0x00 / all-0xFF packets."""
+    """The short-run forms at every chunk size (column runs cap chunks at 16 packets; runs
+    over the segment table's 1,536 segments take the per-packet path) on ragged strided and
+    CSR batches: lengths 0..3000 with odd starts, empty packets, a batch that ends mid-chunk,
+    all-0x00 / all-0xFF packets."""
     _tune("short_loads", mode)
     _tune("chunk_packets", chunk)
     try:

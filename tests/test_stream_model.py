@@ -543,3 +543,59 @@ def test_slot_windows_model_matches_oracle(oracle, stride):
     got = finish(slot_windows_model(ring, S, E, n), S)
     want = oracle.batch_slotted(np.ascontiguousarray(ring[base:base + n * stride]), stride, lens)
     assert np.array_equal(np.array(got, dtype=np.uint16), want)
+
+
+# ---- segment-table runs (round 5, sum_segtab_chunk) ------------------------------------
+
+def segtab_chunk_model(buf, S, E, cnt, cpk):
+    """sum_segtab_chunk: the run's per-segment halves-sums in a table, packet j = its whole
+    segments [g_j, g_{j+1}) added in 64 / cpk contiguous shares, + P_{j+1} - P_j, mod 2^32."""
+    X1 = int(E[cnt - 1])
+    b = [int(S[j]) if j < cnt else X1 for j in range(64)]
+    A = b[0] & ~15
+    nseg = (X1 - A + 15) >> 4
+    nwin = (nseg + 63) >> 6
+    seg, raw = _halves_of_segments(buf, A, max(nwin * 64, 1), nseg * 16)
+    g = [(x - A) >> 4 for x in b]
+    o = [(x - A) & 15 for x in b]
+    P = [(_below(raw[g[j] * 16:g[j] * 16 + 16], o[j]) if (j <= cnt and o[j]) else 0)
+         for j in range(64)]
+    q = 64 // cpk
+    sums = []
+    for j in range(cnt):
+        lo, hi = g[j], g[j + 1]
+        per = (hi - lo + q - 1) // q
+        acc = 0
+        for part in range(q):
+            a = lo + part * per
+            acc += int(seg[a:min(a + per, hi)].sum()) if a < hi else 0
+        sums.append((acc + P[j + 1] - P[j]) & M32)
+    return sums + [0] * (64 - cnt)
+
+
+@pytest.mark.parametrize("cpk", [1, 4, 16, 32])
+@pytest.mark.parametrize("case", ["tiny", "mixed", "mtu", "aligned_end"])
+def test_segtab_model_matches_oracle(oracle, case, cpk):
+    rng = np.random.default_rng(hash((case, cpk, "segtab")) % 2**32)
+    base = int(rng.integers(0, 16))
+    if case == "tiny":
+        off = _layout(rng, 200, [0, 0, 1, 2, 3, 5, 7, 16, 17, 31], base)
+    elif case == "mixed":
+        off = _layout(rng, 100, list(range(64, 1501, 97)) + [65, 1499], base)
+    elif case == "mtu":
+        off = _layout(rng, 64, [1500], base)
+    else:
+        lens = np.array([1024] * 16, dtype=np.int64)
+        off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    buf = rng.integers(0, 256, size=int(off[-1]) + 64, dtype=np.uint8)
+    for j in range(0, off.size - 1, 7):
+        buf[off[j]:off[j + 1]] = 0 if j % 2 else 0xFF
+    n = off.size - 1
+    got = np.zeros(n, dtype=np.uint16)
+    for p0 in range(0, n, cpk):
+        cnt = min(cpk, n - p0)
+        S = [int(off[p0 + j]) for j in range(cnt)]
+        E = [int(off[p0 + j + 1]) for j in range(cnt)]
+        got[p0:p0 + cnt] = finish(segtab_chunk_model(buf, S, E, cnt, cpk)[:cnt], S)
+    want = oracle.batch_csr(buf, off)
+    assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]

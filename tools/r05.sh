@@ -195,6 +195,28 @@ slot)  # slot windows (tunable slot_windows 1) on ring slots and gaps: parity, s
         --no-cpu-baseline --no-parity --steps 5 --warmup 2 > "$out/pmcf_C2K_sw$sw.log" 2>&1
   done
   ;;
+segtab)  # segment-table runs (short_loads 3) against column runs and stream prefixes
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+      -k "short_run or every_read_form" > "$out/pytest.log" 2>&1
+  timeout -k 10 600 python3 tools/ab.py --config C --rounds 10 --variants \
+      "short_loads=0;short_loads=2;short_loads=3;short_loads=3,chunk_packets=32;short_loads=3,chunk_packets=8" \
+      > "$out/ab_C.jsonl" 2> "$out/ab_C.err"
+  timeout -k 10 600 python3 tools/ab.py --config A --rounds 10 --variants \
+      "short_loads=2;short_loads=3;short_loads=3,chunk_packets=16;short_loads=0" > "$out/ab_A.jsonl" 2> "$out/ab_A.err"
+  timeout -k 10 600 python3 tools/ab.py --config B --rounds 8 --variants \
+      "short_loads=2;short_loads=3;short_loads=3,chunk_packets=2" > "$out/ab_B.jsonl" 2> "$out/ab_B.err"
+  for m in 3 0 3 0; do
+    AIPSTACK_CHKSUM_SHORT_LOADS=$m bench C_m$m --config C --steps 20 --warmup 5 --per-launch --no-cpu-baseline
+  done
+  for m in 3 2; do
+    AIPSTACK_CHKSUM_SHORT_LOADS=$m bench A_m$m --config A --steps 20 --warmup 5 --per-launch --no-cpu-baseline
+    AIPSTACK_CHKSUM_SHORT_LOADS=$m bench B_m$m --config B --steps 20 --warmup 5 --per-launch --no-cpu-baseline
+  done
+  AIPSTACK_CHKSUM_SHORT_LOADS=3 timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv \
+      -d "$out/pmc_C_m3" -o run --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD \
+      SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES -- python3 bench.py --config C \
+      --no-cpu-baseline --no-parity --no-ceiling --steps 5 --warmup 2 > "$out/pmc_C_m3.log" 2>&1
+  ;;
 *)
   echo "unknown mode $mode"; exit 2 ;;
 esac
