@@ -265,6 +265,11 @@ struct SlottedHostDesc : SlottedDesc {
     static constexpr bool kEdge = false;
 };
 
+// The same for fixed-length packets at a gap read over the link.
+struct GappedHostDesc : GappedDesc {
+    static constexpr bool kEdge = false;
+};
+
 struct SeededCsrDesc : CsrDesc {
     const uint32_t *states;  // n accumulator states (IpChksumAccumulator::State)
 

@@ -604,7 +604,7 @@ int launch(const Desc &desc, uint64_t n, uint32_t max_len, uint16_t *d_out, uint
         // 217.1 us at 4; C and C2K, mixed lengths, lose at 8: 233.3 / 267.1 against 229.9 /
         // 243.4; profiles/r04/su8)
         const int su = tuning_stream_windows(
-            std::is_same<Desc, GappedDesc>::value && max_len >= 1024u ? 8 : 4);
+            std::is_base_of<GappedDesc, Desc>::value && max_len >= 1024u ? 8 : 4);
         // slot windows (SU 128, sum_slot_windows): tunable slot_windows = 1 (device-memory
         // slots and gaps; the host-memory form keeps the masked gathered stream)
         if constexpr (Desc::kEdge) {
@@ -797,6 +797,11 @@ int batch_strided_from(const void *d_base, uint64_t stride, uint32_t len, uint64
     // Round 5: back-to-back packets in device memory take short runs (launch_short_runs);
     // tunable "gather" 0 = the round-4 gathered stream, -1 = rounds 1-3 stream mode.
     const int gm = tuning().gather.load(std::memory_order_relaxed);
+    if (stride != len && host_bytes) {  // over the link: edges masked in the stream
+        GappedHostDesc h;
+        static_cast<GappedDesc &>(h) = GappedDesc{(uint64_t)(uintptr_t)d_base, stride, len};
+        return launch<GappedHostDesc, false>(h, n, len, d_out, flags, (hipStream_t)stream);
+    }
     if (stride != len || (!host_bytes && gm == 0)) {
         GappedDesc d{(uint64_t)(uintptr_t)d_base, stride, len};
         return launch<GappedDesc, false>(d, n, len, d_out, flags, (hipStream_t)stream);
