@@ -80,7 +80,8 @@ __global__ __launch_bounds__(kBlock) void chksum_batch_kernel(Desc desc, uint64_
     __shared__ typename std::conditional<kSlotWin, SlotRows[kWavesPerBlock], char>::type slot_rows;
     struct GatheredShared {
         GatherLds g[kWavesPerBlock];
-        KeepTable keep;
+        // the byte-mask table, for edges masked in the stream only
+        typename std::conditional<Desc::kEdge, char, KeepTable>::type keep;
     };
     __shared__ typename std::conditional<kGathered, GatheredShared, char>::type gsh;
     constexpr bool kColumns = Desc::kStream && SU == 64;  // column runs (sum_column_chunk)
@@ -116,8 +117,12 @@ __global__ __launch_bounds__(kBlock) void chksum_batch_kernel(Desc desc, uint64_
         } else if constexpr (kGathered) {
             // (CSR: every packet within the contract, else the wave mode below)
             if (!Desc::kCsr || __builtin_amdgcn_ballot_w64(lE - lS > (uint64_t)AIPSTACK_CHKSUM_MAX_LEN) == 0) {
-                sums = sum_gathered_chunks<SU, NT, Desc::kEdge>(lS, (uint32_t)(lE - lS), lane,
-                                                                &gsh.g[wave_in_block], &gsh.keep);
+                if constexpr (Desc::kEdge)
+                    sums = sum_gathered_chunks<SU, NT, true>(lS, (uint32_t)(lE - lS), lane,
+                                                             &gsh.g[wave_in_block], nullptr);
+                else
+                    sums = sum_gathered_chunks<SU, NT, false>(lS, (uint32_t)(lE - lS), lane,
+                                                              &gsh.g[wave_in_block], &gsh.keep);
                 streamed = true;
             }
         } else if constexpr (SU > 0) {
@@ -597,9 +602,14 @@ int launch(const Desc &desc, uint64_t n, uint32_t max_len, uint16_t *d_out, uint
         // summed whole segments (fewer VGPRs): 8-packet chunks 244.2 us, 16 248.8, 4 291.9
         // (A2K 224.2 / 225.8 / 221.9; profiles/r04/shape2).
         // CSR packets in the gathered stream (config C, 64-1500 B): 16-packet chunks 231.0 us,
-        // 8 242.3, 32 233.6 (profiles/r04/chunks) -- about 12 KiB per chunk, as A's 8 x 1500 B
+        // 8 242.3, 32 233.6 (profiles/r04/chunks) -- about 12 KiB per chunk, as A's 8 x 1500 B.
+        // Round 5, the driver's protocol (--steps 20 --warmup 5, profiles/r05/shape5): ring
+        // slots of mixed lengths (C2K) run 254.8-256.6 us in 16-packet chunks against
+        // 281.9-284.2 in 8 (32: 262), the per-chunk setup spread over twice the bytes; fixed
+        // 1500-B packets at a stride (A2K) 231.6-233.1 against 231.5-232.1, so they keep 8.
         if (!sh.small && tuning().chunk_packets.load(std::memory_order_relaxed) == 0)
-            sh.chunk_packets = Desc::kCsr ? 16 : 8;
+            sh.chunk_packets =
+                (Desc::kCsr || std::is_base_of<SlottedDesc, Desc>::value) ? 16 : 8;
         // 4 windows per group; 8 for fixed-length packets of 1 KiB or more (A 213.4 against
         // 217.1 us at 4; C and C2K, mixed lengths, lose at 8: 233.3 / 267.1 against 229.9 /
         // 243.4; profiles/r04/su8)

@@ -1177,6 +1177,41 @@ def test_slotted_checksums(oracle, stream_mode, stride, su):
     assert np.array_equal(fin, oracle.batch_slotted(ring[:n * stride], stride, lens, final=True))
 
 
+@pytest.mark.parametrize("chunk", [0, 8, 16, 64])
+def test_gathered_stream_chunk_edges(oracle, chunk):
+    """The gathered stream on ring slots at the edges of its chunks: 16-slot chunks whose
+    streams hold 1023, 1024 and 1025 segments, a multiple of 64 plus one, empty slots at a
+    chunk's end (the last prefix is the stream's total) and in its middle, one segment per
+    slot, and 2000-byte slots; in 8-, 16- and 64-slot chunks, slots starting at 0, 5 and 15
+    within a segment."""
+    stride = 2048
+    rows = [
+        [1024] * 16,                       # T = 1024
+        [1024] * 15 + [1040],              # T = 1025
+        [1023] * 16,                       # T = 1024 with a partial last segment per slot
+        [1024] * 15 + [1008],              # T = 1023
+        [16 * 61 + 1] + [1024] * 15,       # T = 1024, first slot ends past a block edge
+        [1500] * 10 + [0] * 6,             # empty slots at the end: cs = T
+        [0, 0, 2000] + [0] * 5 + [64] * 8,  # empty slots first and in the middle
+        [1] * 16,                          # one segment each
+        [2000] * 16,                       # T = 2000
+    ]
+    lens = np.array([x for r in rows for x in r] * 5, dtype=np.uint32)
+    n = len(lens)
+    _tune("chunk_packets", chunk)
+    try:
+        for base in (0, 5, 15):
+            ring = synth.random_bytes(stride + base, n * stride + 32)
+            view = np.ascontiguousarray(ring[base:base + n * stride])
+            dring = _d(ring)
+            got = _np(A.chksum_batch_slotted(dring[base:base + n * stride], stride,
+                                             _d(lens.view(np.int32))))
+            want = oracle.batch_slotted(view, stride, lens)
+            assert np.array_equal(got, want), (base, np.nonzero(got != want)[0][:8])
+    finally:
+        _tune("chunk_packets", 0)
+
+
 @pytest.fixture
 def slot_windows():
     """Setter for the slot_windows tunable (1 = slot windows, 0 = the gathered stream);

@@ -34,6 +34,32 @@ __global__ __launch_bounds__(256) void read_kernel(const u32x4 *__restrict__ p, 
     if (acc == 0x12345678u) out[wave] = acc;  // practically never: keeps loads live
 }
 
+// The same read with LS contiguous segments per lane: in each group of 64 * LS segments lane
+// l loads segments l * LS .. l * LS + LS - 1 (one wave instruction per segment index, lanes
+// LS * 16 bytes apart), so a wave-wide prefix scan covers LS KiB instead of one.
+template <int UNROLL, int LS>
+__global__ __launch_bounds__(256) void read_kernel_ls(const u32x4 *__restrict__ p, uint64_t n16,
+                                                      uint64_t per_wave, uint32_t *out) {
+    static_assert(UNROLL % LS == 0, "whole groups");
+    const int lane = threadIdx.x & 63;
+    const uint64_t wave = (uint64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint64_t i = wave * per_wave;
+    const uint64_t end = min(i + per_wave, n16);
+    uint32_t acc = 0;
+    __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)(p + i), (short)0,
+                                                                 (int)((end - i) * 16), 0x00020000);
+    for (uint32_t off = 0; i + off < end; off += 64 * UNROLL) {
+        u32x4 v[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u)
+            v[u] = __builtin_amdgcn_raw_buffer_load_b128(
+                r, ((u / LS) * 64 * LS + lane * LS + u % LS) * 16, off * 16, 2);
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) acc ^= v[u][0] + v[u][1] + v[u][2] + v[u][3];
+    }
+    if (acc == 0x12345678u) out[wave] = acc;
+}
+
 // The same read through global_load_dwordx4 with a 64-bit address per lane (the gathered
 // checksum loader's form) instead of a buffer descriptor.
 template <int UNROLL>
@@ -114,7 +140,7 @@ float run(const u32x4 *d, uint64_t n16, uint64_t per_wave, uint32_t *out, int re
 // Shapes: long runs per wave (32 KiB, 2 or 4 windows in flight: the rounds 1-3 probe) and the
 // gathered checksum loader's shape (one short run per wave, ~12 KiB, every window issued up
 // front). Prints one JSON line; "GBps" is the best shape.
-template <int U, bool NT, bool GLOBAL = false>
+template <int U, bool NT, bool GLOBAL = false, int LS = 1>
 float run_rot(u32x4 *const *d, int nbuf, uint64_t n16, uint64_t per_wave, uint32_t *out,
               unsigned lds_pad = 0) {
     uint64_t waves = (n16 + per_wave - 1) / per_wave;
@@ -126,6 +152,8 @@ float run_rot(u32x4 *const *d, int nbuf, uint64_t n16, uint64_t per_wave, uint32
         (void)hipEventRecord(a);
         if (GLOBAL)
             hipLaunchKernelGGL((read_kernel_global<U>), grid, dim3(256), lds_pad, 0, d[r % nbuf], n16, per_wave, out);
+        else if (LS > 1)
+            hipLaunchKernelGGL((read_kernel_ls<U, LS>), grid, dim3(256), lds_pad, 0, d[r % nbuf], n16, per_wave, out);
         else
             hipLaunchKernelGGL((read_kernel<U, NT>), grid, dim3(256), lds_pad, 0, d[r % nbuf], n16, per_wave, out);
         (void)hipEventRecord(b);
@@ -179,6 +207,40 @@ int ceiling() {
     return 0;
 }
 
+// Lane-contiguous load shapes (read_kernel_ls) against the contiguous one, 12 KiB per wave,
+// 8 windows then 4, at the bare kernel's 8 waves per SIMD and at 4 and 5 (lds_pad).
+int lanes() {
+    const uint64_t bytes = 1572864000ull;
+    const uint64_t n16 = bytes / 16;
+    constexpr int R = 3;
+    u32x4 *d[R]; uint32_t *out;
+    for (int r = 0; r < R; ++r) {
+        CK(hipMalloc(&d[r], bytes));
+        CK(hipMemset(d[r], 1 + r, bytes));
+    }
+    CK(hipMalloc(&out, 1 << 24));
+    CK(hipDeviceSynchronize());
+    auto gbps = [&](float ms) { return bytes / ms / 1e6; };
+    for (int pass = 0; pass < 2; ++pass) {
+        const float a1 = run_rot<8, true>(d, R, n16, 768, out);
+        const float a2 = run_rot<8, true, false, 2>(d, R, n16, 768, out);
+        const float a4 = run_rot<8, true, false, 4>(d, R, n16, 768, out);
+        const float b1 = run_rot<8, true>(d, R, n16, 768, out, 33792);
+        const float b2 = run_rot<8, true, false, 2>(d, R, n16, 768, out, 33792);
+        const float b4 = run_rot<8, true, false, 4>(d, R, n16, 768, out, 33792);
+        const float c1 = run_rot<8, true>(d, R, n16, 768, out, 27648);
+        const float c4 = run_rot<8, true, false, 4>(d, R, n16, 768, out, 27648);
+        const float e4 = run_rot<16, true, false, 4>(d, R, n16, 1024, out, 33792);
+        printf("{\"lanes_GBps\": {\"ls1\": %.1f, \"ls2\": %.1f, \"ls4\": %.1f, \"ls1_4waves\": %.1f, "
+               "\"ls2_4waves\": %.1f, \"ls4_4waves\": %.1f, \"ls1_5waves\": %.1f, \"ls4_5waves\": %.1f, "
+               "\"ls4_16K_4waves\": %.1f}}\n",
+               gbps(a1), gbps(a2), gbps(a4), gbps(b1), gbps(b2), gbps(b4), gbps(c1), gbps(c4), gbps(e4));
+    }
+    for (int r = 0; r < R; ++r) CK(hipFree(d[r]));
+    CK(hipFree(out));
+    return 0;
+}
+
 // Per-launch times of the first 120 launches of one read shape from a cold start (3 rotated
 // 1.57 GB buffers, no warm-up): does a pure read at the checksum kernels' rate show their
 // clock dip ~3 ms into a run? Shape: 12 KiB per wave, 8 windows then 4 (u8).
@@ -218,6 +280,7 @@ int trace_reads(int global) {
 
 int main(int argc, char **argv) {
     if (argc > 1 && std::strcmp(argv[1], "ceiling") == 0) return ceiling();
+    if (argc > 1 && std::strcmp(argv[1], "lanes") == 0) return lanes();
     if (argc > 1 && std::strcmp(argv[1], "trace") == 0) return trace_reads(argc > 2 ? std::atoi(argv[2]) : 1);
     const uint64_t bytes = 2359296000ull;  // config B's payload (2.36 GB, > 256 MiB MALL)
     const uint64_t n16 = bytes / 16;

@@ -217,6 +217,41 @@ segtab)  # segment-table runs (short_loads 3) against column runs and stream pre
       SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES -- python3 bench.py --config C \
       --no-cpu-baseline --no-parity --no-ceiling --steps 5 --warmup 2 > "$out/pmc_C_m3.log" 2>&1
   ;;
+shape5)  # chunk sizes of the gathered stream, the chain groups and the frame chunks under the
+         # driver's protocol (the round-4 choices were steady-state ones), two passes
+  for pass in 1 2; do
+    for cp in 0 16 32; do
+      AIPSTACK_CHKSUM_CHUNK_PACKETS=$cp bench C2K_cp$cp --config C2K --steps 20 --warmup 5 --per-launch --no-cpu-baseline
+    done
+    AIPSTACK_CHKSUM_STREAM=8 bench C2K_su8 --config C2K --steps 20 --warmup 5 --per-launch --no-cpu-baseline
+    for cp in 0 16; do
+      AIPSTACK_CHKSUM_CHUNK_PACKETS=$cp bench A2K_cp$cp --config A2K --steps 20 --warmup 5 --per-launch --no-cpu-baseline
+    done
+    AIPSTACK_CHKSUM_SLOT_WINDOWS=1 bench A2K_slotwin --config A2K --steps 20 --warmup 5 --per-launch --no-cpu-baseline
+    for cp in 0 64; do
+      AIPSTACK_CHKSUM_CHUNK_PACKETS=$cp bench CHAIN_cp$cp --config CHAIN --steps 20 --warmup 5 --per-launch --no-cpu-baseline
+    done
+    for cp in 0 64; do
+      AIPSTACK_CHKSUM_CHUNK_PACKETS=$cp bench RX_cp$cp --config RX --steps 20 --warmup 5 --per-launch --no-cpu-baseline
+      AIPSTACK_CHKSUM_CHUNK_PACKETS=$cp bench RX2K_cp$cp --config RX2K --steps 20 --warmup 5 --per-launch --no-cpu-baseline
+    done
+  done
+  ;;
+tab)  # the gathered stream's segment tables (default build) against the scan (lib_notab,
+      # -DAIPSTACK_GATHER_TAB=0), driver protocol, two passes; the GPU suite first
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+      > "$out/pytest_gpu.log" 2>&1
+  for pass in 1 2; do
+    for c in C2K A2K; do
+      bench ${c}_tab --config $c --steps 20 --warmup 5 --per-launch --no-cpu-baseline
+      AIPSTACK_AMD_LIB=tools/build/lib_notab.so bench ${c}_notab --config $c --steps 20 --warmup 5 --per-launch --no-cpu-baseline
+    done
+  done
+  ;;
+lanes)  # the read probe's lane-contiguous shapes (LS segments per lane, hbm_peak lanes)
+  timeout -k 10 200 tools/build/hbm_peak lanes > "$out/lanes.jsonl"
+  timeout -k 10 120 tools/build/hbm_peak ceiling > "$out/ceiling.jsonl"
+  ;;
 final_bench)  # every config under the driver's protocol (A first, as the box's first GPU
               # process), the ceiling probe, the slot-read probes (RX2K / C2K lines)
   for c in A B C A2K C2K CHAIN RX RX2K TXREC TX TX2K; do
