@@ -610,11 +610,11 @@ int launch(const Desc &desc, uint64_t n, uint32_t max_len, uint16_t *d_out, uint
         if (!sh.small && tuning().chunk_packets.load(std::memory_order_relaxed) == 0)
             sh.chunk_packets =
                 (Desc::kCsr || std::is_base_of<SlottedDesc, Desc>::value) ? 16 : 8;
-        // 4 windows per group; 8 for fixed-length packets of 1 KiB or more (A 213.4 against
-        // 217.1 us at 4; C and C2K, mixed lengths, lose at 8: 233.3 / 267.1 against 229.9 /
-        // 243.4; profiles/r04/su8)
-        const int su = tuning_stream_windows(
-            std::is_base_of<GappedDesc, Desc>::value && max_len >= 1024u ? 8 : 4);
+        // 4 windows per group. Round 4 took 8 for fixed-length packets of 1 KiB or more (A
+        // 213.4 against 217.1 us at 4, steady state; C and C2K lost at 8: 233.3 / 267.1 against
+        // 229.9 / 243.4; profiles/r04/su8); under the driver's protocol A2K runs 230.4-230.8
+        // at 4 against 232.1-232.9 at 8 (profiles/r05/shape6), so 4 everywhere.
+        const int su = tuning_stream_windows(4);
         // slot windows (SU 128, sum_slot_windows): tunable slot_windows = 1 (device-memory
         // slots and gaps; the host-memory form keeps the masked gathered stream)
         if constexpr (Desc::kEdge) {

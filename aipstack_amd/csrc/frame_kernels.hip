@@ -400,13 +400,16 @@ __device__ __forceinline__ uint32_t hdr_below(const u32x4 (&seg)[kHdrSegs],
 // windows into a compact LDS array as they pass (a segment's slot = the union segments
 // before it), instead of being loaded per lane before the stream: a header line loaded up
 // front has left L2 by the time the stream reaches it, so it was fetched twice (RX 1.11x).
-// Which lanes of window w hold header segments is bit (w & 31) of word (w >> 5) of an LDS
-// bit table per lane slot, so runs of at most kGatherWindows windows take this path.
-constexpr uint32_t kGatherWindows = 128;
+// Which lanes of window w hold header segments is word w of an LDS mask table, so runs of at
+// most kGatherWindows windows take this path; chunks of at most kCaptureFrames frames (the
+// launch's 32, round 4), so that the compact slots take 4 KiB per wave (round 5: 64 frames'
+// 8 KiB held the kernel at 4 waves per SIMD by LDS alone).
+constexpr uint32_t kGatherWindows = 64;
+constexpr uint32_t kCaptureFrames = 32;
 #ifndef AIPSTACK_FRAME_NT  // experiments: 0 = the frame stream loads with the default policy
 #define AIPSTACK_FRAME_NT 1
 #endif
-constexpr uint32_t kHdrSlots = kWave * kHdrSegs;  // at most 8 segments per frame
+constexpr uint32_t kHdrSlots = kCaptureFrames * kHdrSegs;  // at most 8 segments per frame
 
 struct FrameLds {
     uint64_t wmask[kGatherWindows + 8];  // per window: the lanes holding header segments
@@ -605,7 +608,8 @@ __device__ __forceinline__ FrameOut process_chunk(const Desc &desc, uint64_t p0,
              << 32) |
             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)E, lastl);
         const uint32_t nseg = ((uint32_t)(X1 - base) + 15u) >> 4;
-        if (GATHER != kHdrLoads && ((nseg + 63u) >> 6) <= kGatherWindows) {
+        if (GATHER != kHdrLoads && cnt <= (int)kCaptureFrames &&
+            ((nseg + 63u) >> 6) <= kGatherWindows) {
             // (B'+C') one pass: the stream gives H at every frame's aligned start A0_j and
             // hands the header segments to LDS; the parse runs on them after the stream.
             const uint64_t A0 = S & ~(uint64_t)15;
@@ -616,8 +620,10 @@ __device__ __forceinline__ FrameOut process_chunk(const Desc &desc, uint64_t p0,
             {
                 uint32_t z;  // made here (a zero quad kept live across the loop was spilled)
                 asm volatile("v_mov_b32 %0, 0" : "=v"(z));
-                reinterpret_cast<u32x4 *>(lds->wmask)[lane] = u32x4{z, z, z, z};
-                if (lane < 4) reinterpret_cast<u32x4 *>(lds->wmask)[kWave + lane] = u32x4{z, z, z, z};
+                static_assert((kGatherWindows + 8) % 2 == 0 && (kGatherWindows + 8) / 2 <= kWave,
+                              "one 16-byte store per lane clears the masks");
+                if (lane < (int)(kGatherWindows + 8) / 2)
+                    reinterpret_cast<u32x4 *>(lds->wmask)[lane] = u32x4{z, z, z, z};
             }
             __builtin_amdgcn_wave_barrier();
             if (r1 > r0) {
@@ -797,12 +803,6 @@ __device__ __forceinline__ FrameOut process_chunk(const Desc &desc, uint64_t p0,
     return o;
 }
 
-// The classic kernel: a wave walks its chunks and stores each chunk's results right after
-// it. SPLIT (Tx only): lane j writes frame j's record (w0 | w1 << 32) to a workspace
-// instead, and tx_scatter_kernel stores the fields after the whole read pass.
-#ifndef AIPSTACK_FRAME_WAVES_PER_SIMD  // occupancy the register budget is fitted to
-#define AIPSTACK_FRAME_WAVES_PER_SIMD 4
-#endif
 // Line stores (round 5, the send ring's in-place fill, tx_store = 2): a 2-byte field store
 // leaves a partly written line that the memory side merges with the bytes around it (TX2K:
 // ~49 us of its 170 for 2 M field stores, WRITE_SIZE ~52 B per frame). On a ring of slots
@@ -854,8 +854,12 @@ __device__ __forceinline__ void store_frame_lines(const FrameOut &o, uint32_t fl
 #ifndef AIPSTACK_FRAME_WAVES_PER_SIMD  // occupancy the register budget is fitted to
 #define AIPSTACK_FRAME_WAVES_PER_SIMD 4
 #endif
+#ifndef AIPSTACK_FRAME_RX_WAVES_PER_SIMD  // the same for Rx verify (no field stores)
+#define AIPSTACK_FRAME_RX_WAVES_PER_SIMD AIPSTACK_FRAME_WAVES_PER_SIMD
+#endif
 template <class Desc, bool TX, int U, int P, bool NT, int SU, bool SPLIT, int GATHER, int STORE>
-__global__ __launch_bounds__(kBlock, AIPSTACK_FRAME_WAVES_PER_SIMD) void frame_kernel(Desc desc, uint64_t n,
+__global__ __launch_bounds__(kBlock, TX ? AIPSTACK_FRAME_WAVES_PER_SIMD
+                                        : AIPSTACK_FRAME_RX_WAVES_PER_SIMD) void frame_kernel(Desc desc, uint64_t n,
                                                        uint32_t chunks_per_wave,
                                                        uint32_t chunk_packets,
                                                        uint8_t *__restrict__ status,
@@ -920,7 +924,11 @@ int launch_frames_g(const Desc &desc, uint64_t n, uint8_t *d_status, uint64_t *d
     const bool slots = !Desc::kStream && big;
     if (big) cpk = 32;
     const uint64_t nchunks = (n + cpk - 1) / cpk;
-    const int su = tuning_stream_windows(8);  // measured: 8 > 4 > off > 2 (RX and TX)
+    // stream windows per group: round 4 measured 8 > 4 > off > 2 for RX and TX at steady
+    // state; under the driver's protocol 4 runs RX 122.9-124.7 us against 124.5-127.3, the
+    // records pass 130.5-132.3 against 132.3-132.9 and the split fill 161.1 against
+    // 163.3-165.0 (profiles/r05/shape6)
+    const int su = tuning_stream_windows(4);
     const uint64_t target_waves =
         (slots && wpc <= 0) ? nchunks : (uint64_t)cus * (wpc > 0 ? wpc : 128);
     uint64_t cpw = (nchunks + target_waves - 1) / target_waves;

@@ -252,6 +252,37 @@ lanes)  # the read probe's lane-contiguous shapes (LS segments per lane, hbm_pea
   timeout -k 10 200 tools/build/hbm_peak lanes > "$out/lanes.jsonl"
   timeout -k 10 120 tools/build/hbm_peak ceiling > "$out/ceiling.jsonl"
   ;;
+shape6)  # launch shapes of the remaining configs under the driver's protocol (their round-4
+         # choices were steady-state ones), two passes
+  b() { n=$1; shift; env "$@" timeout -k 10 300 python3 bench.py --config ${n%%_*} --steps 20 \
+        --warmup 5 --per-launch --no-cpu-baseline --no-ceiling >> "$out/$n.json" 2>> "$out/$n.err"; }
+  for pass in 1 2; do
+    b RX_def X=0;            b RX_su4 AIPSTACK_CHKSUM_STREAM=4;  b RX_cp16 AIPSTACK_CHKSUM_CHUNK_PACKETS=16
+    b RX_cp24 AIPSTACK_CHKSUM_CHUNK_PACKETS=24;  b RX_wpc64 AIPSTACK_CHKSUM_WAVES_PER_CU=64
+    b TXREC_def X=0;         b TXREC_su4 AIPSTACK_CHKSUM_STREAM=4
+    b TXREC_cp24 AIPSTACK_CHKSUM_CHUNK_PACKETS=24
+    b TX_def X=0;            b TX_su4 AIPSTACK_CHKSUM_STREAM=4;  b TX_g0 AIPSTACK_CHKSUM_TX_GATHER=0
+    b RX2K_def X=0;          b RX2K_cp16 AIPSTACK_CHKSUM_CHUNK_PACKETS=16
+    b TX2K_def X=0;          b TX2K_cp16 AIPSTACK_CHKSUM_CHUNK_PACKETS=16
+    b CHAIN_def X=0;         b CHAIN_cp16 AIPSTACK_CHKSUM_CHUNK_PACKETS=16;  b CHAIN_su2 AIPSTACK_CHKSUM_STREAM=2
+    b A2K_def X=0;           b A2K_su4 AIPSTACK_CHKSUM_STREAM=4;  b A2K_cp4 AIPSTACK_CHKSUM_CHUNK_PACKETS=4
+    b C2K_def X=0;           b C2K_su2 AIPSTACK_CHKSUM_STREAM=2
+    b C_def X=0;             b C_cp8 AIPSTACK_CHKSUM_CHUNK_PACKETS=8;  b C_cp32 AIPSTACK_CHKSUM_CHUNK_PACKETS=32
+    b B_def X=0;             b B_cp2 AIPSTACK_CHKSUM_CHUNK_PACKETS=2
+  done
+  ;;
+rx5)  # frame shapes after the round-5 changes (4 stream windows, 32-frame capture); Rx verify
+      # at 5 waves per SIMD (lib_rx5) against 4; the frame tests first
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+      -k "frame or rx or tx or slotted or gathered" > "$out/pytest.log" 2>&1
+  b() { n=$1; shift; env "$@" timeout -k 10 300 python3 bench.py --config ${n%%_*} --steps 20 \
+        --warmup 5 --per-launch --no-cpu-baseline --no-ceiling >> "$out/$n.json" 2>> "$out/$n.err"; }
+  for pass in 1 2 3; do
+    b RX_def X=0;  b RX_rx5 AIPSTACK_AMD_LIB=tools/build/lib_rx5.so
+    b RX2K_def X=0;  b RX2K_rx5 AIPSTACK_AMD_LIB=tools/build/lib_rx5.so
+    b TXREC_def X=0;  b TX_def X=0;  b A2K_def X=0
+  done
+  ;;
 final_bench)  # every config under the driver's protocol (A first, as the box's first GPU
               # process), the ceiling probe, the slot-read probes (RX2K / C2K lines)
   for c in A B C A2K C2K CHAIN RX RX2K TXREC TX TX2K; do
