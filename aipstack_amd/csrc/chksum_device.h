@@ -1334,6 +1334,13 @@ __device__ __forceinline__ uint32_t sum_slot_windows(uint64_t S, uint64_t E, int
 // next group goes out before the current one is summed, so a wave of one short chunk issues
 // all of its ~12 KiB before it sums the first window (the gathered stream's issue pattern,
 // without its per-window owner lookup and address arithmetic).
+// Short runs' stream prefixes: packet starts' partial segments loaded per lane up front (1) or
+// taken from the stream (0). Driver protocol (profiles/r05/edge): config C 247.9-250.1 us with
+// the loads against 240.5-243.5 without (2 M extra loads); A in stream prefixes 223.4-224.2
+// against 230.3-230.5 (A's default, column runs, does this already). A/B build switch.
+#ifndef AIPSTACK_STREAM_EDGE_LOADS
+#define AIPSTACK_STREAM_EDGE_LOADS 0
+#endif
 template <int SU, bool NT>
 __device__ __forceinline__ uint32_t sum_stream_chunk(uint64_t S, uint64_t E, int lane, int cnt,
                                                      uint32_t voff) {
@@ -1351,10 +1358,29 @@ __device__ __forceinline__ uint32_t sum_stream_chunk(uint64_t S, uint64_t E, int
         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)S);
     // the run spans <= 64 * 2^17 + 15 bytes (stream_ok)
     StreamRun<U, NT, U, kDb, kGl> run;
-    run.begin(S0 & ~(uint64_t)15, X1, voff);
     const uint64_t bs[1] = {S};
     uint32_t hb[1], hx;
-    run.prefixes(bs, hb, hx, voff);
+    if constexpr (AIPSTACK_STREAM_EDGE_LOADS && SU > 8) {
+        // Short runs (device memory only): H at each packet start's segment (one ds_bpermute
+        // per window with starts, no partial segment from the stream) plus the bytes of that
+        // segment below the start, from one segment load per lane before the stream (as column
+        // runs; the stream reads that line again later). A start at X1 (lanes past the batch,
+        // empty tail packets) is exact. Stream mode (SU <= 8) also reads host memory over the
+        // link, where the edge segment would cross it twice.
+        const uint64_t A = S0 & ~(uint64_t)15;
+        const uint32_t o = (uint32_t)S & 15u;
+        u32x4 bseg = {0u, 0u, 0u, 0u};
+        if (S != X1 && o != 0u) {
+            typedef __attribute__((address_space(1))) const u32x4 gseg;
+            bseg = *(const gseg *)(S & ~(uint64_t)15);
+        }
+        run.begin(A, X1, voff);
+        run.template prefixes<1, true>(bs, hb, hx, voff);
+        hb[0] += S != X1 ? halves_below_seg(bseg, o) : 0u;
+    } else {
+        run.begin(S0 & ~(uint64_t)15, X1, voff);
+        run.prefixes(bs, hb, hx, voff);
+    }
     const uint32_t hn = from_next_lane(hb[0], hx, lane);  // H(S_{j+1}); lane 63: H(X1)
     return lane < cnt ? hn - hb[0] : 0u;
 }

@@ -283,6 +283,19 @@ rx5)  # frame shapes after the round-5 changes (4 stream windows, 32-frame captu
     b TXREC_def X=0;  b TX_def X=0;  b A2K_def X=0
   done
   ;;
+edge)  # short runs' stream prefixes with packet starts' edge segments loaded up front (default
+       # build) against partial segments from the stream (lib_noedge), driver protocol
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+      -k "read_form or short_runs or csr or lengths or random_packet or full_size or golden or config" \
+      > "$out/pytest.log" 2>&1
+  b() { n=$1; shift; env "$@" timeout -k 10 300 python3 bench.py --config ${n%%_*} --steps 20 \
+        --warmup 5 --per-launch --no-cpu-baseline --no-ceiling >> "$out/$n.json" 2>> "$out/$n.err"; }
+  for pass in 1 2 3; do
+    b C_edge X=0;  b C_noedge AIPSTACK_AMD_LIB=tools/build/lib_noedge.so
+    b A_m0edge AIPSTACK_CHKSUM_SHORT_LOADS=0
+    b A_m0noedge AIPSTACK_CHKSUM_SHORT_LOADS=0 AIPSTACK_AMD_LIB=tools/build/lib_noedge.so
+  done
+  ;;
 final_bench)  # every config under the driver's protocol (A first, as the box's first GPU
               # process), the ceiling probe, the slot-read probes (RX2K / C2K lines)
   for c in A B C A2K C2K CHAIN RX RX2K TXREC TX TX2K; do
