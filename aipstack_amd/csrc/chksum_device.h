@@ -158,6 +158,18 @@ struct GappedDesc {
     }
 };
 
+// Gapped packets whose segments can be counted without a table (round 5): the stride a
+// multiple of 16, so every packet starts at the same offset rs within its segment and spans
+// the same ns segments. Compact segment c of a chunk (its packets' segments in order) is
+// segment c - k ns of packet k = c / ns (magic = ceil(2^32 / ns), exact for c < 2^16 and
+// ns <= 2048), at byte k (stride - 16 ns) + 16 c from the chunk's first aligned start: the
+// column runs' loop over a gathered stream whose owners are arithmetic (no LDS lookups).
+struct GappedColDesc : GappedDesc {
+    uint32_t ns;     // segments per packet
+    uint32_t magic;  // ceil(2^32 / ns)
+    int32_t gap;     // stride - 16 * ns (negative when packets share their edge segments)
+};
+
 struct CsrDesc {
     static constexpr bool kCsr = true;
     static constexpr bool kStream = true;
@@ -1492,6 +1504,108 @@ __device__ __forceinline__ uint32_t sum_column_chunk(uint64_t S, uint64_t E, int
     const uint32_t pn = from_next_lane(P, 0u, lane);  // P_{j+1} (lane cnt: X1's)
     __builtin_amdgcn_wave_barrier();  // (the table is rewritten by the next chunk)
     return lane < cnt ? col + pn - P : 0u;
+}
+
+// Gapped column runs (round 5, GappedColDesc, SU = 64): the column runs' loop (each lane adds
+// its own column of segments; per-boundary snapshots in LDS) over a chunk's packets read as one
+// compact stream of just their segments, lane L of window w loading compact segment 64w + L
+// through one buffer descriptor over the chunk's span at k gap + 16 c (five VALU per window,
+// against the gathered stream's owner lookup, 64-bit address and DPP scan). Packet j's whole
+// segments are [j ns, (j + 1) ns): no boundary falls inside a segment; the bytes of its first
+// and last segments that are not its own (below rs, from its end on) come from the two edge
+// segments lane j reads up front and are subtracted (foreign_halves).
+template <bool NT>
+__device__ __forceinline__ uint32_t sum_gapped_column_chunk(uint64_t s0, int lane, int cnt,
+                                                            uint32_t cpk, uint32_t *rows,
+                                                            const GappedColDesc &d) {
+    const uint32_t ns = d.ns;
+    const uint32_t rs = (uint32_t)s0 & 15u;
+    const uint64_t B0 = s0 & ~(uint64_t)15;
+    const uint32_t T = (uint32_t)cnt * ns;  // < 2^16 (launch)
+    const uint32_t nwin = (T + (uint32_t)kWave - 1u) >> 6;
+    const uint32_t span = (uint32_t)((uint64_t)(cnt - 1) * d.stride) + 16u * ns;  // < 2^31
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void *>(B0), (short)0, (int)span, 0x00020000);
+    // edge segments (default cache policy; the stream reads them again later)
+    const uint32_t te = ((rs + d.len - 1u) & 15u) + 1u;
+    const uint32_t pkoff = (uint32_t)lane * (uint32_t)d.stride;  // lanes < cnt: < span
+    u32x4 fseg = {0u, 0u, 0u, 0u}, lseg = {0u, 0u, 0u, 0u};
+    if (lane < cnt && rs != 0u) fseg = load_segment<false>(rsrc, pkoff, 0u);
+    if (lane < cnt && te != 16u) lseg = load_segment<false>(rsrc, pkoff + 16u * (ns - 1u), 0u);
+    constexpr int U = 8;
+    u32x4 va[U], vb[U];
+    auto issue = [&](u32x4 (&v)[U], uint32_t w) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t c = min((w + (uint32_t)u) * (uint32_t)kWave + (uint32_t)lane, T - 1u);
+            const uint32_t k = __umulhi(c, d.magic);
+            const uint32_t off = (uint32_t)(__mul24((int)k, d.gap) + (int)(c << 4));
+            v[u] = load_segment<NT>(rsrc, off, 0u);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+    uint32_t C = 0;   // this lane's column sum
+    uint32_t jb = 0;  // next boundary (uniform): compact segment jb * ns
+    auto consume = [&](const u32x4 (&v)[U], uint32_t w) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t wu = w + (uint32_t)u;
+            if (wu >= nwin) break;
+            uint32_t s = halves(v[u][0], halves(v[u][1], halves(v[u][2], halves(v[u][3], 0u))));
+            if (wu + 1u == nwin)  // lanes past the stream re-read its last segment
+                s = wu * (uint32_t)kWave + (uint32_t)lane < T ? s : 0u;
+            while (jb <= (uint32_t)cnt && ((jb * ns) >> 6) == wu) {
+                rows[jb * kWave + (uint32_t)lane] =
+                    C + ((uint32_t)lane < ((jb * ns) & 63u) ? s : 0u);
+                ++jb;
+            }
+            C += s;
+        }
+    };
+    const uint32_t groups = (nwin + U - 1u) / U;
+    issue(va, 0);
+    uint32_t gi = 0;
+    for (; gi + 2u < groups; gi += 2u) {
+        issue(vb, (gi + 1u) * U);
+        consume(va, gi * U);
+        issue(va, (gi + 2u) * U);
+        consume(vb, (gi + 1u) * U);
+    }
+    if (gi + 2u == groups) {
+        issue(vb, (gi + 1u) * U);
+        consume(va, gi * U);
+        consume(vb, (gi + 1u) * U);
+    } else {
+        consume(va, gi * U);
+    }
+    for (; jb <= (uint32_t)cnt; ++jb) rows[jb * kWave + (uint32_t)lane] = C;  // at T
+    const uint32_t foreign = lane < cnt ? foreign_halves(fseg, lseg, (int)rs, (int)te) : 0u;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    // packet j = lane >> ql: its 2^ql lanes add cpk column differences each
+    const uint32_t ql = 6u - (uint32_t)__builtin_ctz(cpk);  // cpk: a power of two <= 16
+    const uint32_t j = (uint32_t)lane >> ql, part = (uint32_t)lane & ((1u << ql) - 1u);
+    uint32_t acc = 0;
+    if (j < (uint32_t)cnt) {
+        const uint32_t *r0 = rows + j * kWave + part * cpk;
+        const uint32_t *r1 = r0 + kWave;
+        if (cpk >= 4u) {
+            for (uint32_t i = 0; i < cpk; i += 4u) {
+                const u32x4 a = *reinterpret_cast<const u32x4 *>(r0 + i);
+                const u32x4 b = *reinterpret_cast<const u32x4 *>(r1 + i);
+                acc += (b[0] - a[0]) + (b[1] - a[1]) + (b[2] - a[2]) + (b[3] - a[3]);
+            }
+        } else {
+            for (uint32_t i = 0; i < cpk; ++i) acc += r1[i] - r0[i];
+        }
+    }
+    for (uint32_t m = 1; m < (1u << ql); m <<= 1)
+        acc += (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((uint32_t)lane ^ m) << 2), (int)acc);
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t col = (uint32_t)__builtin_amdgcn_ds_bpermute(
+        (int)((((uint32_t)lane << ql) & 63u) << 2), (int)acc);
+    __builtin_amdgcn_wave_barrier();  // (the table is rewritten by the next chunk)
+    return lane < cnt ? col - foreign : 0u;
 }
 
 // Sum over the 64 lanes (DPP row scan + row broadcasts); result valid in lane 63,

@@ -76,7 +76,9 @@ __global__ __launch_bounds__(kBlock) void chksum_batch_kernel(Desc desc, uint64_
     // instruction however short the packets are, instead of one packet per wave instruction.
     // SU = 128 (slot windows, sum_slot_windows): each packet read on its own, no compaction
     constexpr bool kSlotWin = !Desc::kStream && SU == 128;
-    constexpr bool kGathered = !Desc::kStream && SU > 0 && !kSlotWin;
+    // gapped column runs (sum_gapped_column_chunk): owners by arithmetic, no gathered stream
+    constexpr bool kGapCols = std::is_same<Desc, GappedColDesc>::value;
+    constexpr bool kGathered = !Desc::kStream && SU > 0 && !kSlotWin && !kGapCols;
     __shared__ typename std::conditional<kSlotWin, SlotRows[kWavesPerBlock], char>::type slot_rows;
     struct GatheredShared {
         GatherLds g[kWavesPerBlock];
@@ -85,7 +87,8 @@ __global__ __launch_bounds__(kBlock) void chksum_batch_kernel(Desc desc, uint64_
     };
     __shared__ typename std::conditional<kGathered, GatheredShared, char>::type gsh;
     constexpr bool kColumns = Desc::kStream && SU == 64;  // column runs (sum_column_chunk)
-    __shared__ typename std::conditional<kColumns, ColRows[kWavesPerBlock], char>::type col_rows;
+    __shared__ typename std::conditional<kColumns || kGapCols, ColRows[kWavesPerBlock], char>::type
+        col_rows;
     constexpr bool kSegTab = Desc::kStream && SU == 96;   // segment tables (sum_segtab_chunk)
     __shared__ typename std::conditional<kSegTab, SegTab[kWavesPerBlock], char>::type seg_tab;
     if constexpr (kGathered) {
@@ -113,6 +116,10 @@ __global__ __launch_bounds__(kBlock) void chksum_batch_kernel(Desc desc, uint64_
         bool streamed = false;
         if constexpr (kSlotWin) {
             sums = sum_slot_windows<NT>(lS, lE, lane, cnt, voff, slot_rows[wave_in_block]);
+            streamed = true;
+        } else if constexpr (kGapCols) {
+            sums = sum_gapped_column_chunk<NT>(chunk.s0, lane, cnt, chunk_packets,
+                                               col_rows[wave_in_block], desc);
             streamed = true;
         } else if constexpr (kGathered) {
             // (CSR: every packet within the contract, else the wave mode below)
@@ -702,6 +709,41 @@ int launch_short_runs(const Desc &desc, uint64_t n, uint32_t len, uint16_t *d_ou
                                                   kShortRunLds);
 }
 
+// Gapped column runs (round 5, the default for fixed-length packets at a stride that is a
+// multiple of 16, in device memory): chunks of the largest power of two of packets with
+// <= 12 KiB (at most 16), one per wave, through sum_gapped_column_chunk. Strides from 8 MiB,
+// packets over 32 KiB, small batches and tunable gather = 0 keep the gathered stream.
+int launch_gapped(const GappedDesc &g, uint64_t n, uint16_t *d_out, uint32_t flags,
+                  hipStream_t stream) {
+    if (n == 0) return AIPSTACK_CHKSUM_OK;
+    const int cus = device_cu_count(stream);
+    if (cus <= 0) return AIPSTACK_CHKSUM_EHIP;
+    const uint32_t rs = (uint32_t)g.base & 15u;
+    const uint32_t ns = (rs + g.len + 15u) >> 4;
+    Shape sh = pick_shape(n, cus);
+    const int gm = tuning().gather.load(std::memory_order_relaxed);
+    const bool cols = gm != 0 && g.len > 0 && (g.stride & 15u) == 0 && g.stride < (1u << 23) &&
+                      ns <= 2048u && tuning_stream_windows(4) != 0 &&
+                      (!sh.small || tuning().chunk_packets.load(std::memory_order_relaxed) != 0);
+    if (!cols) return launch<GappedDesc, false>(g, n, g.len, d_out, flags, stream);
+    if (tuning().chunk_packets.load(std::memory_order_relaxed) == 0) {
+        uint32_t cp = 1;
+        while (cp < (uint32_t)kColMaxPackets && (uint64_t)(2 * cp) * g.len <= 12288u) cp <<= 1;
+        sh.chunk_packets = cp;
+    }
+    if (sh.chunk_packets > (uint32_t)kColMaxPackets) sh.chunk_packets = kColMaxPackets;
+    uint32_t cp2 = 1;  // a power of two (the column sums' lane split)
+    while (cp2 * 2u <= sh.chunk_packets) cp2 <<= 1;
+    sh.chunk_packets = cp2;
+    GappedColDesc d;
+    static_cast<GappedDesc &>(d) = g;
+    d.ns = ns;
+    d.magic = (uint32_t)(((1ull << 32) + ns - 1u) / ns);
+    d.gap = (int32_t)((int64_t)g.stride - 16 * (int64_t)ns);
+    return launch_k<GappedColDesc, 1, 1, true, false, 64>(d, n, sh, d_out, flags, stream, true,
+                                                          kShortRunLds);
+}
+
 template <bool NT, int SU>
 int launch_chain(const uint64_t *d_addr, const uint32_t *d_len, const uint64_t *d_index,
                  const uint32_t *d_states, const uint64_t *d_fields, uint64_t n,
@@ -812,7 +854,11 @@ int batch_strided_from(const void *d_base, uint64_t stride, uint32_t len, uint64
         static_cast<GappedDesc &>(h) = GappedDesc{(uint64_t)(uintptr_t)d_base, stride, len};
         return launch<GappedHostDesc, false>(h, n, len, d_out, flags, (hipStream_t)stream);
     }
-    if (stride != len || (!host_bytes && gm == 0)) {
+    if (stride != len) {  // gaps between the packets (device memory)
+        GappedDesc d{(uint64_t)(uintptr_t)d_base, stride, len};
+        return launch_gapped(d, n, d_out, flags, (hipStream_t)stream);
+    }
+    if (!host_bytes && gm == 0) {
         GappedDesc d{(uint64_t)(uintptr_t)d_base, stride, len};
         return launch<GappedDesc, false>(d, n, len, d_out, flags, (hipStream_t)stream);
     }

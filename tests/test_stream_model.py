@@ -545,6 +545,83 @@ def test_slot_windows_model_matches_oracle(oracle, stride):
     assert np.array_equal(np.array(got, dtype=np.uint16), want)
 
 
+# ---- gapped column runs (round 5, sum_gapped_column_chunk) ------------------------------
+
+def gapped_column_chunk_model(buf, s0, stride, ln, cnt, cpk):
+    """sum_gapped_column_chunk, step for step: compact segment c of the chunk is loaded from
+    B0 + k * gap + 16 c with k = mulhi(c, ceil(2^32 / ns)) (checked against c // ns), the
+    columns and boundary rows as in column runs with boundaries at j * ns (no partial
+    segment), then each packet's foreign edge bytes subtracted."""
+    rs = s0 & 15
+    B0 = s0 & ~15
+    ns = (rs + ln + 15) >> 4
+    magic = ((1 << 32) + ns - 1) // ns
+    gap = stride - 16 * ns
+    T = cnt * ns
+    nwin = (T + 63) >> 6
+    span = (cnt - 1) * stride + 16 * ns
+    C = np.zeros(64, dtype=np.uint64)
+    rows = np.zeros((cnt + 1, 64), dtype=np.uint64)
+    jb = 0
+    for w in range(nwin):
+        s = np.zeros(64, dtype=np.uint64)
+        for lane in range(64):
+            c = min(w * 64 + lane, T - 1)
+            k = (c * magic) >> 32
+            assert k == c // ns
+            off = k * gap + 16 * c
+            assert 0 <= off and off + 16 <= span
+            if w * 64 + lane < T:
+                raw = np.array(buf[B0 + off:B0 + off + 16], dtype=np.uint8)
+                s[lane] = int(raw.view("<u2").astype(np.uint64).sum())
+        while jb <= cnt and ((jb * ns) >> 6) == w:
+            B = (jb * ns) & 63
+            rows[jb] = (C + np.where(np.arange(64) < B, s, 0)) & M32
+            jb += 1
+        C = (C + s) & M32
+    while jb <= cnt:
+        rows[jb] = C
+        jb += 1
+    te = ((rs + ln - 1) & 15) + 1
+    out = []
+    q = 64 // cpk
+    for j in range(cnt):
+        acc = 0
+        for part in range(q):
+            cols = range(part * cpk, (part + 1) * cpk)
+            acc += sum(int(rows[j + 1][c]) - int(rows[j][c]) for c in cols)
+        a0 = B0 + j * stride
+        first = np.array(buf[a0:a0 + 16], dtype=np.uint8)
+        last = np.array(buf[a0 + 16 * (ns - 1):a0 + 16 * ns], dtype=np.uint8)
+        foreign = _below(first, rs) + (int(last.view("<u2").astype(np.uint64).sum())
+                                       - _below(last, te))
+        out.append((acc - foreign) & M32)
+    return out
+
+
+@pytest.mark.parametrize("stride,ln", [(2048, 1500), (1504, 1500), (16, 40), (0, 100),
+                                       (48, 1), (2048, 2048 - 16), (9216, 9000), (64, 16)])
+def test_gapped_column_model_matches_oracle(oracle, stride, ln):
+    """Strides a multiple of 16, packets at any start offset within a segment: gaps, packets
+    sharing their edge segments (1504 / 1500 at an odd offset), overlapping and zero strides."""
+    rng = np.random.default_rng(stride * 7 + ln)
+    n = 40
+    for base in (0, 3, 12, 15):
+        cp = 1
+        while cp < 16 and 2 * cp * ln <= 12288:
+            cp *= 2
+        ring = rng.integers(0, 256, size=n * max(stride, 16) + ln + base + 64, dtype=np.uint8)
+        ring[base:base + ln] = 0xFF
+        got = np.zeros(n, dtype=np.uint16)
+        for p0 in range(0, n, cp):
+            cnt = min(cp, n - p0)
+            s0 = base + p0 * stride
+            S = [s0 + j * stride for j in range(cnt)]
+            got[p0:p0 + cnt] = finish(gapped_column_chunk_model(ring, s0, stride, ln, cnt, cp), S)
+        want = oracle.batch_strided(ring, stride, ln, n, base_off=base)
+        assert np.array_equal(got, want), (base, np.nonzero(got != want)[0][:8])
+
+
 # ---- segment-table runs (round 5, sum_segtab_chunk) ------------------------------------
 
 def segtab_chunk_model(buf, S, E, cnt, cpk):

@@ -296,6 +296,17 @@ edge)  # short runs' stream prefixes with packet starts' edge segments loaded up
     b A_m0noedge AIPSTACK_CHKSUM_SHORT_LOADS=0 AIPSTACK_AMD_LIB=tools/build/lib_noedge.so
   done
   ;;
+gapcol)  # gapped column runs (the new default for strides that are multiples of 16) against the
+         # gathered stream (gather 0), driver protocol; the strided/gapped tests first
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+      -k "strided or slotted or lengths or overlapping or read_form or random_packet or golden or engine_host" \
+      > "$out/pytest.log" 2>&1
+  b() { n=$1; shift; env "$@" timeout -k 10 300 python3 bench.py --config ${n%%_*} --steps 20 \
+        --warmup 5 --per-launch --no-cpu-baseline --no-ceiling >> "$out/$n.json" 2>> "$out/$n.err"; }
+  for pass in 1 2 3; do
+    b A2K_cols X=0;  b A2K_gath AIPSTACK_CHKSUM_GATHER=0
+  done
+  ;;
 final_bench)  # every config under the driver's protocol (A first, as the box's first GPU
               # process), the ceiling probe, the slot-read probes (RX2K / C2K lines)
   for c in A B C A2K C2K CHAIN RX RX2K TXREC TX TX2K; do
