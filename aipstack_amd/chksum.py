@@ -1068,12 +1068,6 @@ def rx_verify(frames, offsets, *, out=None, stream=None):
     return out
 
 
-# Frames per batch from which the two-pass split fill beats the one-pass fill (measured,
-# profiles/r02/small_batches/tx_small.jsonl: one pass 57 vs 61 us at 256 K frames, split
-# 182 vs 188 us at 1 M).
-TX_SPLIT_MIN_FRAMES = 1 << 19
-
-
 def tx_fill(frames, offsets, *, out=None, stream=None, split=None, workspace=None):
     """Tx fill on the GPU, IN PLACE: writes the IPv4 header checksum and the TCP / UDP /
     ICMP checksum of every frame; returns one status per frame (AIPSTACK_RX_* codes).
@@ -1081,8 +1075,9 @@ def tx_fill(frames, offsets, *, out=None, stream=None, split=None, workspace=Non
     ``split=True`` runs the two-pass ``aipstack_chksum_tx_fill_split`` with a workspace of
     8 bytes per frame (``workspace``: a device tensor of at least that many bytes, else one
     is taken from torch's allocator); ``split=False`` the one-pass
-    ``aipstack_chksum_tx_fill``; ``None`` (default) picks the faster for the batch size
-    (split from TX_SPLIT_MIN_FRAMES frames on). Both write the same bytes."""
+    ``aipstack_chksum_tx_fill``; ``None`` (default) the one pass, the faster at every batch
+    size measured (round 5, driver protocol: 159.8 against 161.6 us at 1 M frames,
+    profiles/r05/txsplit; round 2: 57 against 61 us at 256 K). Both write the same bytes."""
     _require_device(frames, "frames")
     _require_offsets(offsets)
     _same_device(frames, offsets, "frames and offsets")
@@ -1090,7 +1085,7 @@ def tx_fill(frames, offsets, *, out=None, stream=None, split=None, workspace=Non
     out = _u8_out(out, max(n, 0), frames)
     lib = _lib.load()
     if split is None:
-        split = n >= TX_SPLIT_MIN_FRAMES
+        split = False
     if not split:
         _check(lib.aipstack_chksum_tx_fill(frames.data_ptr(), offsets.data_ptr(), n,
                                            out.data_ptr(), _stream_handle(stream, frames)),

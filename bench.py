@@ -125,8 +125,13 @@ def parse():
     p.add_argument("--chain-fill", action="store_true",
                    help="CHAIN: the Tx form (aipstack_chksum_batch_chain_fill): each chain's "
                         "checksum is also stored big-endian into its 20-B header node")
+    p.add_argument("--tx-split", action="store_true",
+                   help="TX, TX2K: the two-pass split fill (read pass + scatter pass through a "
+                        "workspace; default: the one-pass in-place fill, which measured faster "
+                        "under the driver's protocol in round 5: TX 159.8 vs 161.6 us, TX2K "
+                        "175.2 vs 178.9, profiles/r05/txsplit)")
     p.add_argument("--tx-inplace", action="store_true",
-                   help="TX: the one-pass in-place fill (default: the two-pass split fill)")
+                   help="TX: the one-pass in-place fill (the default; kept for older scripts)")
     p.add_argument("--small", type=int, default=0, metavar="N",
                    help="small-batch mode (A or RX): batches of N packets/frames from a ring of "
                         "64 slots, eager launches vs the same launches replayed from a HIP "
@@ -604,6 +609,7 @@ def main():
         buf = torch.from_numpy(ring_host).to(dev)
         d_lens = torch.from_numpy(lens_host.view(np.int32)).to(dev)
         status = torch.empty(n, dtype=torch.uint8, device=dev)
+        tx_ws = torch.empty(8 * n, dtype=torch.uint8, device=dev)  # slotted split's records
         spec["total"] = int(lens_host.sum(dtype=np.uint64))
         spec["payload"] = spec["total"]
     if layout == "chain":
@@ -650,7 +656,8 @@ def main():
         elif layout == "csrslot":
             A.chksum_batch_slotted(buf, 2048, d_lens, out=out, stream=stream)
         elif layout == "txslot":  # idempotent, as the CSR fill
-            A.tx_fill_slotted(buf, 2048, d_lens, out=status, stream=stream)
+            A.tx_fill_slotted(buf, 2048, d_lens, out=status, stream=stream,
+                              split=args.tx_split, workspace=tx_ws if args.tx_split else None)
         elif layout == "chain" and args.chain_fill:
             A.chksum_chain_fill(chain["addr"], chain["len"], chain["index"], chain["states"],
                                 chain["fields"], out=out, stream=stream)
@@ -658,7 +665,7 @@ def main():
             A.chksum_batch_chain(chain["addr"], chain["len"], chain["index"], chain["states"],
                                  out=out, final=True, stream=stream)
         else:  # tx: idempotent (the filled fields are excluded from their own sums)
-            A.tx_fill(buf, d_off, out=status, stream=stream, split=not args.tx_inplace,
+            A.tx_fill(buf, d_off, out=status, stream=stream, split=args.tx_split,
                       workspace=tx_ws)
 
     for _ in range(args.warmup):
@@ -849,8 +856,8 @@ def main():
                          "note": ("step k reads batch k mod R (data seeds 42..42+R-1), every "
                                   "batch checked" if rot > 1 else
                                   "one batch, read by every step")},
-            **({"tx_fill": "in-place, one pass" if args.tx_inplace else
-                "split: read pass + scatter pass (both timed)"} if layout == "tx" else {}),
+            **({"tx_fill": "split: read pass + scatter pass (both timed)" if args.tx_split else
+                "in-place, one pass"} if layout in ("tx", "txslot") else {}),
             **({"chain_fill": "checksum also stored big-endian into each header node"}
                if layout == "chain" and args.chain_fill else {}),
         },
@@ -938,7 +945,7 @@ def small_batches(args, layout, plen, dev):
             if layout == "rx":
                 A.rx_verify(buf, offs[r], out=outs[r])
             else:
-                A.tx_fill(buf, offs[r], out=outs[r], workspace=ws[r], split=not args.tx_inplace)
+                A.tx_fill(buf, offs[r], out=outs[r], workspace=ws[r], split=args.tx_split)
         payload = int(off[-1]) // R
 
         def check(r):
@@ -991,8 +998,8 @@ def small_batches(args, layout, plen, dev):
         "value": round(wall_g * 1e6, 3), "unit": "us per batch (graph, wall)",
         "n_gpus": 1, "steps": K, "warmup": K, "higher_is_better": False,
         "config": {"workload": f"config {args.config} in batches of {N}"
-                               + (" (one-pass in-place fill)" if layout == "tx" and args.tx_inplace
-                                  else " (split fill)" if layout == "tx" else ""),
+                               + (" (split fill)" if layout == "tx" and args.tx_split
+                                  else " (one-pass in-place fill)" if layout == "tx" else ""),
                    "ring_slots": R,
                    "tuning": {k: v for k, v in os.environ.items()
                               if k.startswith("AIPSTACK_CHKSUM_")},

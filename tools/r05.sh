@@ -307,6 +307,14 @@ gapcol)  # gapped column runs (the new default for strides that are multiples of
     b A2K_cols X=0;  b A2K_gath AIPSTACK_CHKSUM_GATHER=0
   done
   ;;
+txsplit)  # the send ring's split fill (records pass + scatter) against its one-pass fill, and
+          # the CSR fill's one pass against its split, driver protocol
+  b() { n=$1; shift; env X=0 timeout -k 10 300 python3 bench.py --config ${n%%_*} --steps 20 \
+        --warmup 5 --per-launch --no-cpu-baseline --no-ceiling "$@" >> "$out/$n.json" 2>> "$out/$n.err"; }
+  for pass in 1 2 3; do
+    b TX2K_one;  b TX2K_split --tx-split;  b TX_split;  b TX_one --tx-inplace
+  done
+  ;;
 final_bench)  # every config under the driver's protocol (A first, as the box's first GPU
               # process), the ceiling probe, the slot-read probes (RX2K / C2K lines)
   for c in A B C A2K C2K CHAIN RX RX2K TXREC TX TX2K; do
