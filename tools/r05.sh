@@ -315,6 +315,17 @@ txsplit)  # the send ring's split fill (records pass + scatter) against its one-
     b TX2K_one;  b TX2K_split --tx-split;  b TX_split;  b TX_one --tx-inplace
   done
   ;;
+txmodes)  # the one-pass fills' header and store forms, the gapped column chunk size, under
+          # the driver's protocol
+  b() { n=$1; shift; env "$@" timeout -k 10 300 python3 bench.py --config ${n%%_*} --steps 20 \
+        --warmup 5 --per-launch --no-cpu-baseline --no-ceiling >> "$out/$n.json" 2>> "$out/$n.err"; }
+  for pass in 1 2; do
+    b TX_def X=0;  b TX_g1 AIPSTACK_CHKSUM_TX_GATHER=1;  b TX_st1 AIPSTACK_CHKSUM_TX_STORE=1
+    b TX_st1g2 AIPSTACK_CHKSUM_TX_STORE=1 AIPSTACK_CHKSUM_TX_GATHER=2
+    b TX2K_def X=0;  b TX2K_st1 AIPSTACK_CHKSUM_TX_STORE=1
+    b A2K_def X=0;  b A2K_cp4 AIPSTACK_CHKSUM_CHUNK_PACKETS=4;  b A2K_cp16 AIPSTACK_CHKSUM_CHUNK_PACKETS=16
+  done
+  ;;
 final_bench)  # every config under the driver's protocol (A first, as the box's first GPU
               # process), the ceiling probe, the slot-read probes (RX2K / C2K lines)
   for c in A B C A2K C2K CHAIN RX RX2K TXREC TX TX2K; do
