@@ -1146,7 +1146,9 @@ __device__ __forceinline__ uint32_t sum_gathered_chunks(uint64_t a, uint32_t l, 
     const uint32_t groups = (nwin + U - 1u) / U;
     // EDGE: the lane reads its chunk's two edge segments itself (they lie inside the chunk's
     // segments, so they are mapped) before the stream's first group, at the default cache
-    // policy (the stream reads the same lines later).
+    // policy (the stream reads the same lines later). Read after the stream's last group was
+    // issued instead, they miss L2 more often (the stream's nontemporal lines do not stay):
+    // C2K 282 against 268 us, FETCH_SIZE +12 %, CHAIN 271 against 261 (profiles/r05/edgeafter).
     // (none where the chunk starts or ends on a segment boundary: nothing foreign there)
     u32x4 fseg = {0u, 0u, 0u, 0u}, lseg = {0u, 0u, 0u, 0u};
     const uint32_t te = ((rs + l - 1u) & 15u) + 1u;  // the chunk's end in its last segment

@@ -326,6 +326,26 @@ txmodes)  # the one-pass fills' header and store forms, the gapped column chunk 
     b A2K_def X=0;  b A2K_cp4 AIPSTACK_CHKSUM_CHUNK_PACKETS=4;  b A2K_cp16 AIPSTACK_CHKSUM_CHUNK_PACKETS=16
   done
   ;;
+edgeafter)  # the gathered stream's / gapped columns' edge segments read after the last group is
+            # issued (default) against before the stream (lib_edgebefore); FETCH_SIZE of each
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+      -k "slotted or gathered or chain or strided or random or frame" > "$out/pytest.log" 2>&1
+  b() { n=$1; shift; env "$@" timeout -k 10 300 python3 bench.py --config ${n%%_*} --steps 20 \
+        --warmup 5 --per-launch --no-cpu-baseline --no-ceiling >> "$out/$n.json" 2>> "$out/$n.err"; }
+  for pass in 1 2; do
+    for c in C2K A2K CHAIN RX2K; do
+      b ${c}_after X=0;  b ${c}_before AIPSTACK_AMD_LIB=tools/build/lib_edgebefore.so
+    done
+  done
+  for c in C2K CHAIN; do
+    for v in after before; do
+      lib=""; [ $v = before ] && lib=tools/build/lib_edgebefore.so
+      AIPSTACK_AMD_LIB=$lib timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv \
+          -d "$out/pmc_${c}_$v" -o run --pmc FETCH_SIZE -- python3 bench.py --config $c \
+          --no-cpu-baseline --no-parity --no-ceiling --steps 5 --warmup 2 > "$out/pmc_${c}_$v.log" 2>&1
+    done
+  done
+  ;;
 final_bench)  # every config under the driver's protocol (A first, as the box's first GPU
               # process), the ceiling probe, the slot-read probes (RX2K / C2K lines)
   for c in A B C A2K C2K CHAIN RX RX2K TXREC TX TX2K; do
