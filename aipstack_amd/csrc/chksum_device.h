@@ -1416,7 +1416,8 @@ __device__ __forceinline__ uint32_t sum_stream_chunk(uint64_t S, uint64_t E, int
 constexpr int kColMaxPackets = 16;
 typedef uint32_t ColRows[(kColMaxPackets + 1) * kWave];
 
-template <bool NT>
+// U: windows per group (8; 6 for chunks of one long packet, launch_short_runs).
+template <bool NT, int U = 8>
 __device__ __forceinline__ uint32_t sum_column_chunk(uint64_t S, uint64_t E, int lane, int cnt,
                                                      uint32_t voff, uint32_t cpk, uint32_t *rows) {
     const uint64_t X1 = readlane64(E, cnt - 1);  // end of the chunk's last packet
@@ -1433,7 +1434,6 @@ __device__ __forceinline__ uint32_t sum_column_chunk(uint64_t S, uint64_t E, int
     // P_j: boundary j's segment below it (lanes 0..cnt; none on a segment edge)
     u32x4 bseg = {0u, 0u, 0u, 0u};
     if (lane <= cnt && o != 0u) bseg = load_segment<false>(rsrc, g * 16u, 0u);
-    constexpr int U = 8;
     u32x4 va[U], vb[U];
     auto issue = [&](u32x4 (&v)[U], uint32_t w) {
 #pragma unroll

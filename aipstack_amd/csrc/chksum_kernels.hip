@@ -86,7 +86,8 @@ __global__ __launch_bounds__(kBlock) void chksum_batch_kernel(Desc desc, uint64_
         typename std::conditional<Desc::kEdge, char, KeepTable>::type keep;
     };
     __shared__ typename std::conditional<kGathered, GatheredShared, char>::type gsh;
-    constexpr bool kColumns = Desc::kStream && SU == 64;  // column runs (sum_column_chunk)
+    // column runs (sum_column_chunk): SU 64 = groups of 8 windows, 48 = groups of 6
+    constexpr bool kColumns = Desc::kStream && (SU == 64 || SU == 48);
     __shared__ typename std::conditional<kColumns || kGapCols, ColRows[kWavesPerBlock], char>::type
         col_rows;
     constexpr bool kSegTab = Desc::kStream && SU == 96;   // segment tables (sum_segtab_chunk)
@@ -144,8 +145,9 @@ __global__ __launch_bounds__(kBlock) void chksum_batch_kernel(Desc desc, uint64_
                     sums = sum_segtab_chunk<NT>(lS, lE, lane, cnt, voff, chunk_packets,
                                                 seg_tab[wave_in_block]);
                 else if constexpr (kColumns)
-                    sums = sum_column_chunk<NT>(lS, lE, lane, cnt, voff, chunk_packets,
-                                                col_rows[wave_in_block]);
+                    sums = sum_column_chunk<NT, SU == 48 ? 6 : 8>(lS, lE, lane, cnt, voff,
+                                                                   chunk_packets,
+                                                                   col_rows[wave_in_block]);
                 else
                     sums = sum_stream_chunk<SU, NT>(lS, lE, lane, cnt, voff);
                 streamed = true;
@@ -699,6 +701,15 @@ int launch_short_runs(const Desc &desc, uint64_t n, uint32_t len, uint16_t *d_ou
     }
     if (mode == 2) {  // column runs (SU 64)
         if (sh.chunk_packets > (uint32_t)kColMaxPackets) sh.chunk_packets = kColMaxPackets;
+        // chunks of one packet over 8 KiB (B: 9000 B, 8.8 windows) in groups of 6 windows: 12
+        // loaded against 16 in groups of 8; under the driver's protocol B 336.8-337.7 us
+        // against 338.3-344.0 (A, 12 KiB chunks, keeps 8: 220.9-221.9 against 222.7-223.1;
+        // profiles/r05/colu)
+        if constexpr (!Desc::kCsr) {
+            if (sh.chunk_packets == 1u && len > 8192u)
+                return launch_k<Desc, 1, 1, true, SEEDED, 48>(desc, n, sh, d_out, flags, stream,
+                                                              true, kShortRunLds);
+        }
         return launch_k<Desc, 1, 1, true, SEEDED, 64>(desc, n, sh, d_out, flags, stream, true,
                                                       kShortRunLds);
     }

@@ -346,6 +346,25 @@ edgeafter)  # the gathered stream's / gapped columns' edge segments read after t
     done
   done
   ;;
+colu)  # column runs' windows per group: 8 (default) against 6 and 4 (lib_col6 / lib_col4)
+  b() { n=$1; shift; env "$@" timeout -k 10 300 python3 bench.py --config ${n%%_*} --steps 20 \
+        --warmup 5 --per-launch --no-cpu-baseline --no-ceiling >> "$out/$n.json" 2>> "$out/$n.err"; }
+  for pass in 1 2 3; do
+    for c in A B; do
+      b ${c}_u8 X=0;  b ${c}_u6 AIPSTACK_AMD_LIB=tools/build/lib_col6.so
+      b ${c}_u4 AIPSTACK_AMD_LIB=tools/build/lib_col4.so
+    done
+  done
+  ;;
+colb)  # B's 6-window column runs in the product build: the strided tests, then B and A
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+      -k "strided or lengths or read_form or short_runs or full_size or golden or random_packet" \
+      > "$out/pytest.log" 2>&1
+  for pass in 1 2; do
+    bench B --config B --steps 20 --warmup 5 --per-launch --no-cpu-baseline --no-ceiling
+    bench A --config A --steps 20 --warmup 5 --per-launch --no-cpu-baseline --no-ceiling
+  done
+  ;;
 final_bench)  # every config under the driver's protocol (A first, as the box's first GPU
               # process), the ceiling probe, the slot-read probes (RX2K / C2K lines)
   for c in A B C A2K C2K CHAIN RX RX2K TXREC TX TX2K; do
