@@ -1344,10 +1344,10 @@ __device__ __forceinline__ uint32_t sum_slot_windows(uint64_t S, uint64_t E, int
 // Stream mode for one chunk (stream_ok). Lane j < cnt holds packet j = [S, E); returns
 // lane j's exact halves-sum (0 on lanes >= cnt).
 // SU <= 8: SU windows issued together, the next group after the current one is summed (rounds
-// 1-4). SU > 8 (round 5, the strided default): groups of SU / 2 windows, double-buffered -- the
-// next group goes out before the current one is summed, so a wave of one short chunk issues
-// all of its ~12 KiB before it sums the first window (the gathered stream's issue pattern,
-// without its per-window owner lookup and address arithmetic).
+// 1-4). SU > 8 (round 5, short runs): groups of AIPSTACK_SHORT_RUN_WINDOWS windows,
+// double-buffered -- the next group goes out before the current one is summed, so a wave of
+// one short chunk issues all of its ~12 KiB before it sums the first window (the gathered
+// stream's issue pattern, without its per-window owner lookup and address arithmetic).
 // Short runs' stream prefixes: packet starts' partial segments loaded per lane up front (1) or
 // taken from the stream (0). Driver protocol (profiles/r05/edge): config C 247.9-250.1 us with
 // the loads against 240.5-243.5 without (2 M extra loads); A in stream prefixes 223.4-224.2
@@ -1359,7 +1359,13 @@ template <int SU, bool NT>
 __device__ __forceinline__ uint32_t sum_stream_chunk(uint64_t S, uint64_t E, int lane, int cnt,
                                                      uint32_t voff) {
     constexpr bool kDb = SU > 8 || AIPSTACK_STREAM_DB != 0;
-    constexpr int U = SU > 8 ? 8 : SU;
+// Short runs' windows per group, double-buffered (A/B build switch): config C under the
+// driver's protocol 241.7-242.5 us at 6 against 242.1-249.3 at 8 and 247.3-248.4 at 4
+// (profiles/r05/sru): ~12 KiB chunks load 12 windows instead of 16.
+#ifndef AIPSTACK_SHORT_RUN_WINDOWS
+#define AIPSTACK_SHORT_RUN_WINDOWS 6
+#endif
+    constexpr int U = SU > 8 ? AIPSTACK_SHORT_RUN_WINDOWS : SU;
     constexpr bool kGl = SU == 32;  // (SU 32: SU 16 through global loads, StreamRun GL)
     // X1 = end of the chunk's last packet; lanes past the batch sit at X1 (empty)
     const int lastl = cnt - 1;

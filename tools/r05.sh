@@ -365,6 +365,13 @@ colb)  # B's 6-window column runs in the product build: the strided tests, then 
     bench A --config A --steps 20 --warmup 5 --per-launch --no-cpu-baseline --no-ceiling
   done
   ;;
+sru)  # short runs' (stream prefixes, config C) windows per group: 8 against 6 and 4
+  b() { n=$1; shift; env "$@" timeout -k 10 300 python3 bench.py --config ${n%%_*} --steps 20 \
+        --warmup 5 --per-launch --no-cpu-baseline --no-ceiling >> "$out/$n.json" 2>> "$out/$n.err"; }
+  for pass in 1 2 3; do
+    b C_u8 X=0;  b C_u6 AIPSTACK_AMD_LIB=tools/build/lib_sr6.so;  b C_u4 AIPSTACK_AMD_LIB=tools/build/lib_sr4.so
+  done
+  ;;
 final_bench)  # every config under the driver's protocol (A first, as the box's first GPU
               # process), the ceiling probe, the slot-read probes (RX2K / C2K lines)
   for c in A B C A2K C2K CHAIN RX RX2K TXREC TX TX2K; do
