@@ -1540,7 +1540,12 @@ __device__ __forceinline__ uint32_t sum_gapped_column_chunk(uint64_t s0, int lan
     u32x4 fseg = {0u, 0u, 0u, 0u}, lseg = {0u, 0u, 0u, 0u};
     if (lane < cnt && rs != 0u) fseg = load_segment<false>(rsrc, pkoff, 0u);
     if (lane < cnt && te != 16u) lseg = load_segment<false>(rsrc, pkoff + 16u * (ns - 1u), 0u);
-    constexpr int U = 8;
+// windows per group (A/B build switch; A2K 228.9-229.7 us at 6 and 228.9-229.6 at 8,
+// profiles/r05/gcu)
+#ifndef AIPSTACK_GAPCOL_WINDOWS
+#define AIPSTACK_GAPCOL_WINDOWS 8
+#endif
+    constexpr int U = AIPSTACK_GAPCOL_WINDOWS;
     u32x4 va[U], vb[U];
     auto issue = [&](u32x4 (&v)[U], uint32_t w) {
 #pragma unroll

@@ -372,6 +372,16 @@ sru)  # short runs' (stream prefixes, config C) windows per group: 8 against 6 a
     b C_u8 X=0;  b C_u6 AIPSTACK_AMD_LIB=tools/build/lib_sr6.so;  b C_u4 AIPSTACK_AMD_LIB=tools/build/lib_sr4.so
   done
   ;;
+gcu)  # gapped column runs' windows per group (8 against 6, lib_gc6); C with the 6-window
+      # short runs (product) and its tests
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+      -k "csr or read_form or short_runs or random_packet or config" > "$out/pytest.log" 2>&1
+  b() { n=$1; shift; env "$@" timeout -k 10 300 python3 bench.py --config ${n%%_*} --steps 20 \
+        --warmup 5 --per-launch --no-cpu-baseline --no-ceiling >> "$out/$n.json" 2>> "$out/$n.err"; }
+  for pass in 1 2 3; do
+    b A2K_u8 X=0;  b A2K_u6 AIPSTACK_AMD_LIB=tools/build/lib_gc6.so;  b C_def X=0
+  done
+  ;;
 final_bench)  # every config under the driver's protocol (A first, as the box's first GPU
               # process), the ceiling probe, the slot-read probes (RX2K / C2K lines)
   for c in A B C A2K C2K CHAIN RX RX2K TXREC TX TX2K; do
