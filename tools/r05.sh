@@ -382,6 +382,20 @@ gcu)  # gapped column runs' windows per group (8 against 6, lib_gc6); C with the
     b A2K_u8 X=0;  b A2K_u6 AIPSTACK_AMD_LIB=tools/build/lib_gc6.so;  b C_def X=0
   done
   ;;
+slotmask)  # ring slots' edges masked in the stream (lib_slotmask) against edge loads (default);
+           # C2K time and FETCH_SIZE
+  b() { n=$1; shift; env "$@" timeout -k 10 300 python3 bench.py --config ${n%%_*} --steps 20 \
+        --warmup 5 --per-launch --no-cpu-baseline --no-ceiling >> "$out/$n.json" 2>> "$out/$n.err"; }
+  for pass in 1 2 3; do
+    b C2K_edge X=0;  b C2K_mask AIPSTACK_AMD_LIB=tools/build/lib_slotmask.so
+  done
+  for v in edge mask; do
+    lib=""; [ $v = mask ] && lib=tools/build/lib_slotmask.so
+    AIPSTACK_AMD_LIB=$lib timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv \
+        -d "$out/pmc_C2K_$v" -o run --pmc FETCH_SIZE -- python3 bench.py --config C2K \
+        --no-cpu-baseline --no-parity --no-ceiling --steps 5 --warmup 2 > "$out/pmc_C2K_$v.log" 2>&1
+  done
+  ;;
 final_bench)  # every config under the driver's protocol (A first, as the box's first GPU
               # process), the ceiling probe, the slot-read probes (RX2K / C2K lines)
   for c in A B C A2K C2K CHAIN RX RX2K TXREC TX TX2K; do
