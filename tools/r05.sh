@@ -396,6 +396,11 @@ slotmask)  # ring slots' edges masked in the stream (lib_slotmask) against edge 
         --no-cpu-baseline --no-parity --no-ceiling --steps 5 --warmup 2 > "$out/pmc_C2K_$v.log" 2>&1
   done
   ;;
+confirm2)  # the driver's exact command, three processes in a row, on the final device code
+  for i in 1 2 3; do
+    timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 >> "$out/n1.json" 2>> "$out/n1.err"
+  done
+  ;;
 final_bench)  # every config under the driver's protocol (A first, as the box's first GPU
               # process), the ceiling probe, the slot-read probes (RX2K / C2K lines)
   for c in A B C A2K C2K CHAIN RX RX2K TXREC TX TX2K; do
