@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 #include "aipstack_amd/chksum.h"
 #include "chksum_internal.h"
@@ -762,8 +763,9 @@ __device__ __forceinline__ bool stream_ok(uint64_t S, uint64_t E, int lane, int 
 // h[k] = H(b[k]) for every b[k] in [A, X1], and hx = H(X1). Windows past the run read
 // zeros (range check) and change nothing.
 struct NoStreamHook {
+    static constexpr bool kWantH = false;  // window() gets H at each segment start (else 0)
     __device__ __forceinline__ void group(uint32_t) {}
-    __device__ __forceinline__ void window(const u32x4 &, uint32_t) {}
+    __device__ __forceinline__ void window(const u32x4 &, uint32_t, uint32_t) {}
 };
 
 // DB (round 4): the next group of U windows is issued before the current one is summed (two
@@ -894,8 +896,10 @@ struct StreamRun {
                     for (int d = 0; d < 4; ++d) hh = halves(vv[u][d] & xabove[d], hh);
                     x_hi = (uint32_t)__builtin_amdgcn_readlane((int)hh, xlane);
                 }
+                // H at this lane's segment start, for hooks that keep it (frames' capture)
+                const uint32_t hseg = std::remove_reference_t<Hook>::kWantH ? carry + excl : 0u;
                 carry += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-                hook.window(vv[u], wu);
+                hook.window(vv[u], wu, hseg);
             }
         };
         if constexpr (DB) {

@@ -411,18 +411,27 @@ constexpr uint32_t kCaptureFrames = 32;
 #endif
 constexpr uint32_t kHdrSlots = kCaptureFrames * kHdrSegs;  // at most 8 segments per frame
 
+// Round 5 (AIPSTACK_FRAME_HCAP): the capture also stores H at each captured segment's start,
+// so a frame's H(A0) is read from LDS after the stream instead of fetched per window with a
+// ds_bpermute (and its wait) as a stream boundary.
+#ifndef AIPSTACK_FRAME_HCAP
+#define AIPSTACK_FRAME_HCAP 1
+#endif
 struct FrameLds {
     uint64_t wmask[kGatherWindows + 8];  // per window: the lanes holding header segments
                                          // (+8: whole groups past the last window read 0)
     u32x4 slots[kHdrSlots];          // the compact header segments
+    uint32_t hslot[AIPSTACK_FRAME_HCAP ? kHdrSlots : 1];  // H at each slot's segment start
 };
 
 // Capture hook: group(w) fetches the group's U window masks into SGPRs (broadcast LDS
 // reads); window(v, w) writes the lanes of the mask to consecutive compact slots.
 template <int U>
 struct HeaderCapture {
+    static constexpr bool kWantH = AIPSTACK_FRAME_HCAP != 0;
     const uint64_t *wmask;
     u32x4 *slots;
+    uint32_t *hslot;
     uint32_t count;  // header segments before the current window (wave-uniform)
     uint64_t mk[U];
     __device__ __forceinline__ void group(uint32_t w) {
@@ -436,7 +445,7 @@ struct HeaderCapture {
     }
     // The store runs under exec = the window's mask, set and restored inside one asm
     // statement (the compiler would test each lane's bit with VALU instead).
-    __device__ __forceinline__ void window(const u32x4 &v, uint32_t w) {
+    __device__ __forceinline__ void window(const u32x4 &v, uint32_t w, uint32_t hv) {
         static_assert(U <= 8, "wmask holds 8 zero words past the last window");
         const uint64_t m = mk[w & (uint32_t)(U - 1)];
         const uint32_t below =
@@ -444,13 +453,26 @@ struct HeaderCapture {
         typedef __attribute__((address_space(3))) u32x4 lds_seg;
         const uint32_t addr = (uint32_t)(uintptr_t)(lds_seg *)(slots + count) + 16u * below;
         uint64_t save;
-        asm volatile(
-            "s_and_saveexec_b64 %0, %2\n\t"
-            "ds_write_b128 %1, %3\n\t"
-            "s_mov_b64 exec, %0"
-            : "=&s"(save)
-            : "v"(addr), "s"(m), "v"(v)
-            : "memory");
+        if constexpr (kWantH) {
+            typedef __attribute__((address_space(3))) uint32_t lds_h;
+            const uint32_t haddr = (uint32_t)(uintptr_t)(lds_h *)(hslot + count) + 4u * below;
+            asm volatile(
+                "s_and_saveexec_b64 %0, %2\n\t"
+                "ds_write_b128 %1, %3\n\t"
+                "ds_write_b32 %4, %5\n\t"
+                "s_mov_b64 exec, %0"
+                : "=&s"(save)
+                : "v"(addr), "s"(m), "v"(v), "v"(haddr), "v"(hv)
+                : "memory");
+        } else {
+            asm volatile(
+                "s_and_saveexec_b64 %0, %2\n\t"
+                "ds_write_b128 %1, %3\n\t"
+                "s_mov_b64 exec, %0"
+                : "=&s"(save)
+                : "v"(addr), "s"(m), "v"(v)
+                : "memory");
+        }
         count += (uint32_t)__builtin_popcountll(m);
     }
 };
@@ -659,11 +681,15 @@ __device__ __forceinline__ FrameOut process_chunk(const Desc &desc, uint64_t p0,
             HeaderCapture<SU> cap;
             cap.wmask = lds->wmask;
             cap.slots = lds->slots;
+            cap.hslot = lds->hslot;
             cap.count = 0;
-            const uint64_t bs[1] = {act ? A0 : X1};
+            // (HCAP: no stream boundary but X1; H(A0) comes from the capture after the stream)
+            const uint64_t bs[1] = {act && !AIPSTACK_FRAME_HCAP ? A0 : X1};
             uint32_t hA[1], hx;
             run.template prefixes<1, true>(bs, hA, hx, voff, cap);
             __builtin_amdgcn_wave_barrier();
+            if constexpr (AIPSTACK_FRAME_HCAP)  // r0 < nseg: its segment was captured at cslot
+                hA[0] = act && nmine ? lds->hslot[min(cslot, kHdrSlots - 1u)] : hx;
             // this lane's header blocks, and the next frame's first block (its start)
 #pragma unroll
             for (int i = 0; i < kHdrSegs; ++i) {

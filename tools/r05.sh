@@ -401,6 +401,17 @@ confirm2)  # the driver's exact command, three processes in a row, on the final 
     timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 >> "$out/n1.json" 2>> "$out/n1.err"
   done
   ;;
+hcap)  # frames' H(A0) from the header capture (default) against a stream boundary (lib_nohcap)
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+      -k "frame or rx or tx" > "$out/pytest.log" 2>&1
+  b() { n=$1; shift; env "$@" timeout -k 10 300 python3 bench.py --config ${n%%_*} --steps 20 \
+        --warmup 5 --per-launch --no-cpu-baseline --no-ceiling >> "$out/$n.json" 2>> "$out/$n.err"; }
+  for pass in 1 2 3; do
+    for c in RX TXREC TX; do
+      b ${c}_hcap X=0;  b ${c}_nohcap AIPSTACK_AMD_LIB=tools/build/lib_nohcap.so
+    done
+  done
+  ;;
 final_bench)  # every config under the driver's protocol (A first, as the box's first GPU
               # process), the ceiling probe, the slot-read probes (RX2K / C2K lines)
   for c in A B C A2K C2K CHAIN RX RX2K TXREC TX TX2K; do
