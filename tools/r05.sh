@@ -412,6 +412,18 @@ hcap)  # frames' H(A0) from the header capture (default) against a stream bounda
     done
   done
   ;;
+gtab)  # the gathered stream's chunk starts stored in LDS (default) against a ds_bpermute per
+       # window (lib_nogtab); the GPU suite first
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+      > "$out/pytest_gpu.log" 2>&1
+  b() { n=$1; shift; env "$@" timeout -k 10 300 python3 bench.py --config ${n%%_*} --steps 20 \
+        --warmup 5 --per-launch --no-cpu-baseline --no-ceiling >> "$out/$n.json" 2>> "$out/$n.err"; }
+  for pass in 1 2 3; do
+    for c in C2K CHAIN RX2K TX2K; do
+      b ${c}_gtab X=0;  b ${c}_nogtab AIPSTACK_AMD_LIB=tools/build/lib_nogtab.so
+    done
+  done
+  ;;
 final_bench)  # every config under the driver's protocol (A first, as the box's first GPU
               # process), the ceiling probe, the slot-read probes (RX2K / C2K lines)
   for c in A B C A2K C2K CHAIN RX RX2K TXREC TX TX2K; do
