@@ -432,6 +432,11 @@ final_bench)  # every config under the driver's protocol (A first, as the box's 
   timeout -k 10 120 tools/build/hbm_peak ceiling > "$out/ceiling.jsonl"
   timeout -k 10 120 tools/build/hbm_peak > "$out/hbm_peak.jsonl"
   ;;
+final_bench2)  # the same set again on another box (the spread between boxes)
+  for c in A B C A2K C2K CHAIN RX RX2K TXREC TX TX2K; do
+    bench bench_$c --config $c --steps 20 --warmup 5 --per-launch --no-ceiling
+  done
+  ;;
 final_prof)  # rocprofv3 --kernel-trace --stats of each config's driver-protocol command
   for c in A B C A2K C2K CHAIN RX RX2K TXREC TX TX2K; do
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/prof_$c" -o run \
