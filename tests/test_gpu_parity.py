@@ -1859,17 +1859,22 @@ def test_bench_e2e_ring_slots_line(config, pageable, engines):
         config, "GiB/s checksummed"))
 
 
-def test_bench_tx2k_line():
-    """bench.py --config TX2K (a send ring filled in place on the device): one JSON line,
-    every slot filled as the oracle fills it, the slot-read ceiling beside it."""
+@pytest.mark.parametrize("config,split", [("TX2K", False), ("TX2K", True), ("TX", True)])
+def test_bench_tx_fill_lines(config, split):
+    """bench.py --config TX2K (a send ring filled in place on the device) and TX, in the
+    default one-pass form and with --tx-split (read pass + scatter pass): one JSON line,
+    every frame filled as the oracle fills it, the form named in the config."""
     import json
-    r = subprocess.run([sys.executable, "bench.py", "--config", "TX2K", "--steps", "5",
-                        "--warmup", "5", "--no-cpu-baseline"], cwd=ROOT, capture_output=True,
+    r = subprocess.run([sys.executable, "bench.py", "--config", config, "--steps", "5",
+                        "--warmup", "5", "--no-cpu-baseline", "--no-ceiling"]
+                       + (["--tx-split"] if split else []), cwd=ROOT, capture_output=True,
                        text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([l for l in r.stdout.splitlines() if l.strip()][-1])
-    assert d["parity"].startswith("bit-exact") and d["config"]["slot_stride"] == 2048
-    assert d["roofline"]["frac"] > 0
+    assert d["parity"].startswith("bit-exact") and d["roofline"]["frac"] > 0
+    if config == "TX2K":
+        assert d["config"]["slot_stride"] == 2048
+    assert d["config"]["tx_fill"].startswith("split" if split else "in-place")
 
 
 # ---- frame decisions pinned by the reference's own call sites (tests/golden/frame_ref.py) ---
