@@ -424,6 +424,17 @@ gtab)  # the gathered stream's chunk starts stored in LDS (default) against a ds
     done
   done
   ;;
+fr6)  # frames' stream in groups of 6 windows (lib_fr6) against 4 (default); frame tests on fr6
+  AIPSTACK_AMD_LIB=tools/build/lib_fr6.so timeout -k 10 600 python -u -m pytest tests -m gpu -x -v \
+      --timeout 120 --timeout-method thread -k "frame or rx or tx" > "$out/pytest.log" 2>&1
+  b() { n=$1; shift; env "$@" timeout -k 10 300 python3 bench.py --config ${n%%_*} --steps 20 \
+        --warmup 5 --per-launch --no-cpu-baseline --no-ceiling >> "$out/$n.json" 2>> "$out/$n.err"; }
+  for pass in 1 2 3; do
+    for c in RX TXREC TX; do
+      b ${c}_su4 X=0;  b ${c}_su6 AIPSTACK_AMD_LIB=tools/build/lib_fr6.so
+    done
+  done
+  ;;
 final_bench)  # every config under the driver's protocol (A first, as the box's first GPU
               # process), the ceiling probe, the slot-read probes (RX2K / C2K lines)
   for c in A B C A2K C2K CHAIN RX RX2K TXREC TX TX2K; do
