@@ -435,6 +435,15 @@ fr6)  # frames' stream in groups of 6 windows (lib_fr6) against 4 (default); fra
     done
   done
   ;;
+fnt0)  # frames' stream loads at the default cache policy (lib_fnt0) against nontemporal
+  b() { n=$1; shift; env "$@" timeout -k 10 300 python3 bench.py --config ${n%%_*} --steps 20 \
+        --warmup 5 --per-launch --no-cpu-baseline --no-ceiling >> "$out/$n.json" 2>> "$out/$n.err"; }
+  for pass in 1 2; do
+    for c in TX TX2K RX; do
+      b ${c}_nt X=0;  b ${c}_def AIPSTACK_AMD_LIB=tools/build/lib_fnt0.so
+    done
+  done
+  ;;
 final_bench)  # every config under the driver's protocol (A first, as the box's first GPU
               # process), the ceiling probe, the slot-read probes (RX2K / C2K lines)
   for c in A B C A2K C2K CHAIN RX RX2K TXREC TX TX2K; do
