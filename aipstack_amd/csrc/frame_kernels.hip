@@ -102,10 +102,20 @@ __device__ __forceinline__ uint32_t frame_w1(int fld, bool ip, bool l4, int stat
 }
 
 // The stores of one frame: its status byte, and for Tx the two checksum fields in place.
+#ifndef AIPSTACK_TX_RETOUCH  // experiment: load the field dwords again right before the stores
+#define AIPSTACK_TX_RETOUCH 0
+#endif
 template <bool TX>
 __device__ __forceinline__ void store_frame(uint64_t S, uint32_t w0, uint32_t w1,
                                             uint8_t *__restrict__ status, uint64_t i) {
     status[i] = (uint8_t)(w1 >> 16);
+    if constexpr (TX && AIPSTACK_TX_RETOUCH) {
+        typedef __attribute__((address_space(1))) const uint32_t gdw;
+        uint32_t t0 = 0, t1 = 0;
+        if (w1 & 0x100u) t0 = *(const gdw *)((S + 24) & ~(uint64_t)3);
+        if (w1 & 0x200u) t1 = *(const gdw *)((S + (w1 & 0xFFu)) & ~(uint64_t)3);
+        asm volatile("" ::"v"(t0), "v"(t1));
+    }
     if constexpr (TX) {
         if (w1 & 0x100u) store_be16(S + 24, w0);
         if (w1 & 0x200u) store_be16(S + (w1 & 0xFFu), w0 >> 16);

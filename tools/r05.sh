@@ -444,6 +444,15 @@ fnt0)  # frames' stream loads at the default cache policy (lib_fnt0) against non
     done
   done
   ;;
+retouch)  # in-place Tx fills loading the field dwords again right before the stores (lib_retouch)
+  b() { n=$1; shift; env "$@" timeout -k 10 300 python3 bench.py --config ${n%%_*} --steps 20 \
+        --warmup 5 --per-launch --no-cpu-baseline --no-ceiling >> "$out/$n.json" 2>> "$out/$n.err"; }
+  for pass in 1 2; do
+    for c in TX TX2K; do
+      b ${c}_def X=0;  b ${c}_retouch AIPSTACK_AMD_LIB=tools/build/lib_retouch.so
+    done
+  done
+  ;;
 final_bench)  # every config under the driver's protocol (A first, as the box's first GPU
               # process), the ceiling probe, the slot-read probes (RX2K / C2K lines)
   for c in A B C A2K C2K CHAIN RX RX2K TXREC TX TX2K; do
