@@ -453,6 +453,16 @@ retouch)  # in-place Tx fills loading the field dwords again right before the st
     done
   done
   ;;
+splitg)  # the split Tx fill's read pass without the field-line touches (tx_gather 1)
+  b() { n=$1; shift; env "$@" timeout -k 10 300 python3 bench.py --config TX --steps 20 \
+        --warmup 5 --per-launch --no-cpu-baseline --no-ceiling --tx-split >> "$out/$n.json" 2>> "$out/$n.err"; }
+  for pass in 1 2 3; do
+    b TXs_touch X=0;  b TXs_g1 AIPSTACK_CHKSUM_TX_GATHER=1
+  done
+  AIPSTACK_CHKSUM_TX_GATHER=1 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/prof_g1" -o run \
+      -- python3 bench.py --config TX --tx-split --steps 20 --warmup 5 --no-cpu-baseline --no-ceiling \
+      > "$out/prof_g1.log" 2>&1
+  ;;
 final_bench)  # every config under the driver's protocol (A first, as the box's first GPU
               # process), the ceiling probe, the slot-read probes (RX2K / C2K lines)
   for c in A B C A2K C2K CHAIN RX RX2K TXREC TX TX2K; do
