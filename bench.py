@@ -147,13 +147,21 @@ def parse():
     p.add_argument("--rotate", type=int, default=3, metavar="R",
                    help="A, B, C, A2K: R distinct resident batches, step k reads batch k mod R "
                         "(3 x 1.5 GB for A: no launch can find its bytes in the 256 MiB "
-                        "Infinity Cache); 1 = one batch read by every step")
+                        "Infinity Cache); frames and ring slots (RX, TX, TXREC, RX2K, TX2K, "
+                        "C2K): R copies of the batch at distinct addresses; 1 = one batch "
+                        "read by every step")
     return p.parse_args()
 
 
+# Layouts whose batch is synthesised on the host: rotated over copies at other addresses.
+FRAME_LAYOUTS = ("rx", "tx", "txrec", "rxslot", "csrslot", "txslot")
+
+
 def rotation_count(args, layout):
-    """Batches the timed loop rotates over: the checksum batches only."""
-    return max(1, args.rotate) if layout in ("strided", "csr") else 1
+    """Batches the timed loop rotates over: the checksum batches (distinct data
+    per batch) and the frame and ring-slot batches (copies of the batch at other addresses;
+    round 5); chains keep one batch."""
+    return max(1, args.rotate) if layout in ("strided", "csr") + FRAME_LAYOUTS else 1
 
 
 def shard_spec(config, rank, world, n=None):
@@ -635,6 +643,9 @@ def main():
             bufs.append(b)
             outs.append(torch.empty(n, dtype=torch.uint16, device=dev))
         buf = bufs[0]
+    fbufs = [buf] if layout in FRAME_LAYOUTS else []  # frame / ring-slot batches: R copies
+    if layout in FRAME_LAYOUTS and rot > 1:               # at distinct addresses
+        fbufs += [buf.clone() for _ in range(rot - 1)]
     out = outs[0] if outs else torch.empty(n, dtype=torch.uint16, device=dev)
     torch.cuda.synchronize()
     step_no = [0]
@@ -648,15 +659,15 @@ def main():
         elif layout == "csr":
             A.chksum_batch_csr(bufs[k % rot], d_off, out=outs[k % rot], stream=stream)
         elif layout == "rx":
-            A.rx_verify(buf, d_off, out=status, stream=stream)
+            A.rx_verify(fbufs[k % len(fbufs)], d_off, out=status, stream=stream)
         elif layout == "txrec":
-            A.tx_fill_records(buf, d_off, out=records, stream=stream)
+            A.tx_fill_records(fbufs[k % len(fbufs)], d_off, out=records, stream=stream)
         elif layout == "rxslot":
-            A.rx_verify_slotted(buf, 2048, d_lens, out=status, stream=stream)
+            A.rx_verify_slotted(fbufs[k % len(fbufs)], 2048, d_lens, out=status, stream=stream)
         elif layout == "csrslot":
-            A.chksum_batch_slotted(buf, 2048, d_lens, out=out, stream=stream)
+            A.chksum_batch_slotted(fbufs[k % len(fbufs)], 2048, d_lens, out=out, stream=stream)
         elif layout == "txslot":  # idempotent, as the CSR fill
-            A.tx_fill_slotted(buf, 2048, d_lens, out=status, stream=stream,
+            A.tx_fill_slotted(fbufs[k % len(fbufs)], 2048, d_lens, out=status, stream=stream,
                               split=args.tx_split, workspace=tx_ws if args.tx_split else None)
         elif layout == "chain" and args.chain_fill:
             A.chksum_chain_fill(chain["addr"], chain["len"], chain["index"], chain["states"],
@@ -665,8 +676,8 @@ def main():
             A.chksum_batch_chain(chain["addr"], chain["len"], chain["index"], chain["states"],
                                  out=out, final=True, stream=stream)
         else:  # tx: idempotent (the filled fields are excluded from their own sums)
-            A.tx_fill(buf, d_off, out=status, stream=stream, split=args.tx_split,
-                      workspace=tx_ws)
+            A.tx_fill(fbufs[k % len(fbufs)], d_off, out=status, stream=stream,
+                      split=args.tx_split, workspace=tx_ws)
 
     for _ in range(args.warmup):
         step()
@@ -728,6 +739,16 @@ def main():
     rot_parity = None
     cpu = None
     baseline = None  # rank 0's CPU baseline, run after every rank's check
+    if layout in FRAME_LAYOUTS and len(fbufs) > 1:
+        # every copy processed at least once (the Tx fills write each in place); the last
+        # step's outputs are checked below, and the copies must equal copy 0 afterwards
+        while step_no[0] < len(fbufs) or (step_no[0] - 1) % len(fbufs) != 0:
+            step()
+        torch.cuda.synchronize()
+        if not args.no_parity:
+            same = all(torch.equal(fbufs[0], b) for b in fbufs[1:])
+            rot_parity = (f"rotation copies 1..{len(fbufs) - 1} identical to copy 0 after the run"
+                          if same else "MISMATCH")
     if layout in ("rx", "tx", "txrec"):
         if not args.no_parity and layout == "txrec":
             parity = records_check(spec, frames_host, buf.cpu().numpy(), records.cpu().numpy())
@@ -852,10 +873,14 @@ def main():
             "payload_bytes_per_gpu": payload,
             "layout": layout,
             "parallelism": f"disjoint packet shards x{world}, no collective",
-            "rotation": {"batches": rot, "resident_bytes_per_gpu": int(rot * total),
-                         "note": ("step k reads batch k mod R (data seeds 42..42+R-1), every "
-                                  "batch checked" if rot > 1 else
-                                  "one batch, read by every step")},
+            "rotation": {"batches": rot,
+                         "resident_bytes_per_gpu": int(rot * (buf.numel() if layout in
+                                                              FRAME_LAYOUTS else total)),
+                         "note": ("one batch, read by every step" if rot == 1 else
+                                  "step k reads copy k mod R of the batch (the same frames at "
+                                  "R addresses), every copy checked" if layout in FRAME_LAYOUTS
+                                  else "step k reads batch k mod R (data seeds 42..42+R-1), "
+                                  "every batch checked")},
             **({"tx_fill": "split: read pass + scatter pass (both timed)" if args.tx_split else
                 "in-place, one pass"} if layout in ("tx", "txslot") else {}),
             **({"chain_fill": "checksum also stored big-endian into each header node"}

@@ -463,6 +463,17 @@ splitg)  # the split Tx fill's read pass without the field-line touches (tx_gath
       -- python3 bench.py --config TX --tx-split --steps 20 --warmup 5 --no-cpu-baseline --no-ceiling \
       > "$out/prof_g1.log" 2>&1
   ;;
+frot)  # frame and ring-slot batches rotated over 3 copies (the new default) against one buffer
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread \
+      -k "bench" > "$out/pytest.log" 2>&1
+  b() { n=$1; shift; timeout -k 10 300 python3 bench.py --config ${n%%_*} --steps 20 \
+        --warmup 5 --per-launch --no-cpu-baseline --no-ceiling "$@" >> "$out/$n.json" 2>> "$out/$n.err"; }
+  for pass in 1 2; do
+    for c in RX TXREC TX RX2K TX2K C2K; do
+      b ${c}_rot3;  b ${c}_rot1 --rotate 1
+    done
+  done
+  ;;
 final_bench)  # every config under the driver's protocol (A first, as the box's first GPU
               # process), the ceiling probe, the slot-read probes (RX2K / C2K lines)
   for c in A B C A2K C2K CHAIN RX RX2K TXREC TX TX2K; do
