@@ -474,6 +474,23 @@ frot)  # frame and ring-slot batches rotated over 3 copies (the new default) aga
     done
   done
   ;;
+txrot)  # the Tx fill forms under rotation (3 copies): one pass against split, touches
+  b() { n=$1; shift; env X=0 timeout -k 10 300 python3 bench.py --config ${n%%_*} --steps 20 \
+        --warmup 5 --per-launch --no-cpu-baseline --no-ceiling "$@" >> "$out/$n.json" 2>> "$out/$n.err"; }
+  for pass in 1 2; do
+    b TX_one;  b TX_split --tx-split;  b TX2K_one;  b TX2K_split --tx-split
+  done
+  for pass in 1 2; do
+    AIPSTACK_CHKSUM_TX_GATHER=1 timeout -k 10 300 python3 bench.py --config TX --steps 20 --warmup 5 \
+        --per-launch --no-cpu-baseline --no-ceiling >> "$out/TX_g1.json" 2>> "$out/TX_g1.err"
+    AIPSTACK_CHKSUM_TX_STORE=1 timeout -k 10 300 python3 bench.py --config TX --steps 20 --warmup 5 \
+        --per-launch --no-cpu-baseline --no-ceiling >> "$out/TX_st1.json" 2>> "$out/TX_st1.err"
+    AIPSTACK_CHKSUM_TX_STORE=2 timeout -k 10 300 python3 bench.py --config TX2K --steps 20 --warmup 5 \
+        --per-launch --no-cpu-baseline --no-ceiling >> "$out/TX2K_st2.json" 2>> "$out/TX2K_st2.err"
+    AIPSTACK_CHKSUM_TX_STORE=1 timeout -k 10 300 python3 bench.py --config TX2K --steps 20 --warmup 5 \
+        --per-launch --no-cpu-baseline --no-ceiling >> "$out/TX2K_st1.json" 2>> "$out/TX2K_st1.err"
+  done
+  ;;
 final_bench)  # every config under the driver's protocol (A first, as the box's first GPU
               # process), the ceiling probe, the slot-read probes (RX2K / C2K lines)
   for c in A B C A2K C2K CHAIN RX RX2K TXREC TX TX2K; do
