@@ -514,6 +514,9 @@ final_prof)  # rocprofv3 --kernel-trace --stats of each config's driver-protocol
 final_pmc)  # PMC passes for every config on this device code (tools/pmc_summary.py after)
   for c in A B C A2K C2K CHAIN RX RX2K TXREC TX TX2K; do tools/pmc_run.sh $c "$out/pmc_$c"; done
   ;;
+final_pmc_frames)  # PMC of the frame and ring-slot configs, rotated as bench.py now runs them
+  for c in C2K RX RX2K TXREC TX TX2K; do tools/pmc_run.sh $c "$out/pmc_$c"; done
+  ;;
 final_misc)  # small batches, end to end, the 8-rank launch rehearsed on one GPU
   for n in 64 4096; do
     for c in A RX TX; do
