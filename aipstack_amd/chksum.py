@@ -1076,8 +1076,9 @@ def tx_fill(frames, offsets, *, out=None, stream=None, split=None, workspace=Non
     8 bytes per frame (``workspace``: a device tensor of at least that many bytes, else one
     is taken from torch's allocator); ``split=False`` the one-pass
     ``aipstack_chksum_tx_fill``; ``None`` (default) the one pass, the faster at every batch
-    size measured (round 5, driver protocol: 159.8 against 161.6 us at 1 M frames,
-    profiles/r05/txsplit; round 2: 57 against 61 us at 256 K). Both write the same bytes."""
+    size measured (round 5, driver protocol, 1 M frames: 193.4 against 194.5 us on rotated
+    batches, 159.8 against 161.6 on one buffer, profiles/r05/txrot, txsplit; round 2: 57
+    against 61 us at 256 K). Both write the same bytes."""
     _require_device(frames, "frames")
     _require_offsets(offsets)
     _same_device(frames, offsets, "frames and offsets")

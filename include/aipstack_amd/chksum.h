@@ -167,8 +167,8 @@ int aipstack_chksum_tx_fill(void *d_base, const uint64_t *d_offsets, uint64_t n,
  * computes every frame's fields into d_workspace (8 bytes per frame, 8-byte aligned, at
  * least aipstack_chksum_tx_fill_workspace_bytes(n) bytes, owned by the caller and free
  * again once the stream passes the call), then a scatter pass stores them into the frames.
- * Round 5: no faster than the one pass at any batch size measured (1 M frames: 161.6 vs
- * 159.8 us); for callers that want the stores as a pass of their own. */
+ * Round 5: no faster than the one pass at any batch size measured (1 M frames: 194.5 vs
+ * 193.4 us); for callers that want the stores as a pass of their own. */
 uint64_t aipstack_chksum_tx_fill_workspace_bytes(uint64_t n);
 int aipstack_chksum_tx_fill_split(void *d_base, const uint64_t *d_offsets, uint64_t n,
                                   uint8_t *d_status, void *d_workspace,
