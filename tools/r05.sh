@@ -491,6 +491,13 @@ txrot)  # the Tx fill forms under rotation (3 copies): one pass against split, t
         --per-launch --no-cpu-baseline --no-ceiling >> "$out/TX2K_st1.json" 2>> "$out/TX2K_st1.err"
   done
   ;;
+acp)  # A's column-run chunk size under the driver's protocol: 8 packets (default) against 16 and 4
+  b() { n=$1; shift; env "$@" timeout -k 10 300 python3 bench.py --config A --steps 20 \
+        --warmup 5 --per-launch --no-cpu-baseline --no-ceiling >> "$out/$n.json" 2>> "$out/$n.err"; }
+  for pass in 1 2 3; do
+    b A_cp8 X=0;  b A_cp16 AIPSTACK_CHKSUM_CHUNK_PACKETS=16;  b A_cp4 AIPSTACK_CHKSUM_CHUNK_PACKETS=4
+  done
+  ;;
 final_bench)  # every config under the driver's protocol (A first, as the box's first GPU
               # process), the ceiling probe, the slot-read probes (RX2K / C2K lines)
   for c in A B C A2K C2K CHAIN RX RX2K TXREC TX TX2K; do
