@@ -498,6 +498,14 @@ acp)  # A's column-run chunk size under the driver's protocol: 8 packets (defaul
     b A_cp8 X=0;  b A_cp16 AIPSTACK_CHKSUM_CHUNK_PACKETS=16;  b A_cp4 AIPSTACK_CHKSUM_CHUNK_PACKETS=4
   done
   ;;
+ccp)  # C and C2K chunk sizes between the powers of two under the driver's protocol
+  b() { n=$1; shift; env "$@" timeout -k 10 300 python3 bench.py --config ${n%%_*} --steps 20 \
+        --warmup 5 --per-launch --no-cpu-baseline --no-ceiling >> "$out/$n.json" 2>> "$out/$n.err"; }
+  for pass in 1 2; do
+    b C_cp16 X=0;  b C_cp12 AIPSTACK_CHKSUM_CHUNK_PACKETS=12;  b C_cp24 AIPSTACK_CHKSUM_CHUNK_PACKETS=24
+    b C2K_cp16 X=0;  b C2K_cp12 AIPSTACK_CHKSUM_CHUNK_PACKETS=12;  b C2K_cp24 AIPSTACK_CHKSUM_CHUNK_PACKETS=24
+  done
+  ;;
 final_bench)  # every config under the driver's protocol (A first, as the box's first GPU
               # process), the ceiling probe, the slot-read probes (RX2K / C2K lines)
   for c in A B C A2K C2K CHAIN RX RX2K TXREC TX TX2K; do
