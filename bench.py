@@ -159,9 +159,9 @@ FRAME_LAYOUTS = ("rx", "tx", "txrec", "rxslot", "csrslot", "txslot")
 
 def rotation_count(args, layout):
     """Batches the timed loop rotates over: the checksum batches (distinct data
-    per batch) and the frame and ring-slot batches (copies of the batch at other addresses;
-    round 5); chains keep one batch."""
-    return max(1, args.rotate) if layout in ("strided", "csr") + FRAME_LAYOUTS else 1
+    per batch), the frame and ring-slot batches and the chains (copies of the batch at other
+    addresses, the chunk table rebased onto each; round 5)."""
+    return max(1, args.rotate) if layout in ("strided", "csr", "chain") + FRAME_LAYOUTS else 1
 
 
 def shard_spec(config, rank, world, n=None):
@@ -643,6 +643,13 @@ def main():
             bufs.append(b)
             outs.append(torch.empty(n, dtype=torch.uint16, device=dev))
         buf = bufs[0]
+    chain_rot = []  # chains: copies of the buffer, each with its chunk table rebased onto it
+    if layout == "chain" and rot > 1:
+        for _ in range(rot - 1):
+            bc = chain["buf"].clone()
+            delta = bc.data_ptr() - chain["base"]
+            chain_rot.append({"buf": bc, "addr": chain["addr"] + delta,
+                              "fields": chain["fields"] + delta})
     fbufs = [buf] if layout in FRAME_LAYOUTS else []  # frame / ring-slot batches: R copies
     if layout in FRAME_LAYOUTS and rot > 1:               # at distinct addresses
         fbufs += [buf.clone() for _ in range(rot - 1)]
@@ -669,12 +676,14 @@ def main():
         elif layout == "txslot":  # idempotent, as the CSR fill
             A.tx_fill_slotted(fbufs[k % len(fbufs)], 2048, d_lens, out=status, stream=stream,
                               split=args.tx_split, workspace=tx_ws if args.tx_split else None)
-        elif layout == "chain" and args.chain_fill:
-            A.chksum_chain_fill(chain["addr"], chain["len"], chain["index"], chain["states"],
-                                chain["fields"], out=out, stream=stream)
         elif layout == "chain":
-            A.chksum_batch_chain(chain["addr"], chain["len"], chain["index"], chain["states"],
-                                 out=out, final=True, stream=stream)
+            cc = chain if k % rot == 0 else chain_rot[k % rot - 1]
+            if args.chain_fill:
+                A.chksum_chain_fill(cc["addr"], chain["len"], chain["index"], chain["states"],
+                                    cc["fields"], out=out, stream=stream)
+            else:
+                A.chksum_batch_chain(cc["addr"], chain["len"], chain["index"], chain["states"],
+                                     out=out, final=True, stream=stream)
         else:  # tx: idempotent (the filled fields are excluded from their own sums)
             A.tx_fill(fbufs[k % len(fbufs)], d_off, out=status, stream=stream,
                       split=args.tx_split, workspace=tx_ws)
@@ -773,6 +782,23 @@ def main():
             c["sample"] += " (the same packets in their compact CSR form)"
             return c
     elif layout == "chain":
+        if chain_rot and not args.no_parity:
+            # each copy once more into its own output: the same sums as copy 0 (and, for the
+            # fill, the same headers afterwards)
+            while step_no[0] < rot:
+                step()
+            ref = A.chksum_batch_chain(chain["addr"], chain["len"], chain["index"],
+                                       chain["states"], final=True, stream=stream)
+            same = True
+            for cc in chain_rot:
+                o = A.chksum_batch_chain(cc["addr"], chain["len"], chain["index"],
+                                         chain["states"], final=True, stream=stream)
+                torch.cuda.synchronize()
+                same = same and torch.equal(o, ref)
+                if args.chain_fill:
+                    same = same and torch.equal(cc["buf"], chain["buf"])
+            rot_parity = (f"rotation copies 1..{rot - 1} give copy 0's sums" if same
+                          else "MISMATCH")
         if not args.no_parity:
             parity = (chain_fill_check(chain) if args.chain_fill
                       else chain_check(chain, out.cpu().numpy()))
@@ -874,11 +900,15 @@ def main():
             "layout": layout,
             "parallelism": f"disjoint packet shards x{world}, no collective",
             "rotation": {"batches": rot,
-                         "resident_bytes_per_gpu": int(rot * (buf.numel() if layout in
-                                                              FRAME_LAYOUTS else total)),
+                         "resident_bytes_per_gpu": int(rot * (
+                             buf.numel() if layout in FRAME_LAYOUTS else
+                             chain["buf"].numel() if layout == "chain" else total)),
                          "note": ("one batch, read by every step" if rot == 1 else
                                   "step k reads copy k mod R of the batch (the same frames at "
                                   "R addresses), every copy checked" if layout in FRAME_LAYOUTS
+                                  else "step k reads copy k mod R of the chains (the buffer "
+                                  "cloned, the chunk table rebased), every copy checked"
+                                  if layout == "chain"
                                   else "step k reads batch k mod R (data seeds 42..42+R-1), "
                                   "every batch checked")},
             **({"tx_fill": "split: read pass + scatter pass (both timed)" if args.tx_split else

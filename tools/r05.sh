@@ -506,6 +506,15 @@ ccp)  # C and C2K chunk sizes between the powers of two under the driver's proto
     b C2K_cp16 X=0;  b C2K_cp12 AIPSTACK_CHKSUM_CHUNK_PACKETS=12;  b C2K_cp24 AIPSTACK_CHKSUM_CHUNK_PACKETS=24
   done
   ;;
+chrot)  # chains rotated over 3 rebased copies (the new default) against one buffer; the fill too
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread \
+      -k "bench or chain" > "$out/pytest.log" 2>&1
+  b() { n=$1; shift; timeout -k 10 300 python3 bench.py --config CHAIN --steps 20 \
+        --warmup 5 --per-launch --no-cpu-baseline --no-ceiling "$@" >> "$out/$n.json" 2>> "$out/$n.err"; }
+  for pass in 1 2; do
+    b CHAIN_rot3;  b CHAIN_rot1 --rotate 1;  b CHAINF_rot3 --chain-fill
+  done
+  ;;
 final_bench)  # every config under the driver's protocol (A first, as the box's first GPU
               # process), the ceiling probe, the slot-read probes (RX2K / C2K lines)
   for c in A B C A2K C2K CHAIN RX RX2K TXREC TX TX2K; do
