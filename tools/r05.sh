@@ -541,6 +541,12 @@ final_pmc)  # PMC passes for every config on this device code (tools/pmc_summary
 final_pmc_frames)  # PMC of the frame and ring-slot configs, rotated as bench.py now runs them
   for c in C2K RX RX2K TXREC TX TX2K; do tools/pmc_run.sh $c "$out/pmc_$c"; done
   ;;
+final_chain)  # CHAIN's final line and rocprof with its batch rotated
+  bench bench_CHAIN --config CHAIN --steps 20 --warmup 5 --per-launch
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/prof_CHAIN" -o run \
+      -- python3 bench.py --config CHAIN --steps 20 --warmup 5 --no-cpu-baseline --no-ceiling \
+      > "$out/prof_CHAIN.log" 2>&1
+  ;;
 final_misc)  # small batches, end to end, the 8-rank launch rehearsed on one GPU
   for n in 64 4096; do
     for c in A RX TX; do
