@@ -515,6 +515,17 @@ chrot)  # chains rotated over 3 rebased copies (the new default) against one buf
     b CHAIN_rot3;  b CHAIN_rot1 --rotate 1;  b CHAINF_rot3 --chain-fill
   done
   ;;
+hdrt)  # ring slots' header blocks read 8 lanes per frame (lib_hdrt) against per-lane loads
+  AIPSTACK_AMD_LIB=tools/build/lib_hdrt.so timeout -k 10 600 python -u -m pytest tests -m gpu -x -v \
+      --timeout 120 --timeout-method thread -k "slotted or frame" > "$out/pytest.log" 2>&1
+  b() { n=$1; shift; env "$@" timeout -k 10 300 python3 bench.py --config ${n%%_*} --steps 20 \
+        --warmup 5 --per-launch --no-cpu-baseline --no-ceiling >> "$out/$n.json" 2>> "$out/$n.err"; }
+  for pass in 1 2 3; do
+    for c in RX2K TX2K; do
+      b ${c}_def X=0;  b ${c}_hdrt AIPSTACK_AMD_LIB=tools/build/lib_hdrt.so
+    done
+  done
+  ;;
 final_bench)  # every config under the driver's protocol (A first, as the box's first GPU
               # process), the ceiling probe, the slot-read probes (RX2K / C2K lines)
   for c in A B C A2K C2K CHAIN RX RX2K TXREC TX TX2K; do
