@@ -14,6 +14,7 @@ from .chksum import (  # noqa: E402
     AIPSTACK_CHKSUM_EINVAL,
     AIPSTACK_CHKSUM_ENODEV,
     AIPSTACK_CHKSUM_FINAL,
+    AIPSTACK_CHKSUM_JUST_WRITTEN,
     AIPSTACK_CHKSUM_MAX_LEN,
     AIPSTACK_CHKSUM_OK,
     ChksumEngine,
@@ -52,7 +53,7 @@ LIB_PATH = _lib.LIB_PATH
 
 __all__ = [
     "AIPSTACK_CHKSUM_EHIP", "AIPSTACK_CHKSUM_EINVAL", "AIPSTACK_CHKSUM_ENODEV",
-    "AIPSTACK_CHKSUM_FINAL", "AIPSTACK_CHKSUM_MAX_LEN", "AIPSTACK_CHKSUM_OK", "ChksumEngine",
+    "AIPSTACK_CHKSUM_FINAL", "AIPSTACK_CHKSUM_JUST_WRITTEN", "AIPSTACK_CHKSUM_MAX_LEN", "AIPSTACK_CHKSUM_OK", "ChksumEngine",
     "ChksumError",
     "IpBufNode", "IpBufRef", "IpChksum", "IpChksumAccumulator", "IpChksumInverted",
     "chksum_batch_chain", "chksum_chain_fill", "chksum_batch_csr", "chksum_batch_seeded_csr", "flatten_chains", "chksum_batch_strided", "device_check",

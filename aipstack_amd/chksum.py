@@ -35,6 +35,7 @@ AIPSTACK_CHKSUM_EHIP = -2
 AIPSTACK_CHKSUM_ENODEV = -3
 AIPSTACK_CHKSUM_FINAL = 1
 AIPSTACK_CHKSUM_ZERO_AS_FFFF = 2
+AIPSTACK_CHKSUM_JUST_WRITTEN = 4  # hint: written by device stores since last read (chksum.h)
 AIPSTACK_CHKSUM_MAX_LEN = 65535
 
 
@@ -300,16 +301,21 @@ def _out_tensor(out, n: int, like):
 
 
 def chksum_batch_strided(buf, stride: int, length: int, n: int, *, out=None,
-                         final: bool = False, byte_offset: int = 0, stream=None):
+                         final: bool = False, byte_offset: int = 0, stream=None,
+                         just_written: bool = False):
     """``out[i] = IpChksumInverted(buf[byte_offset + i*stride :][:length])`` for i < n
-    (``IpChksum`` with ``final=True``), on the GPU. ``buf`` is a device uint8 tensor."""
+    (``IpChksum`` with ``final=True``), on the GPU. ``buf`` is a device uint8 tensor.
+    ``just_written``: the AIPSTACK_CHKSUM_JUST_WRITTEN hint (the bytes were written by device
+    kernels with ordinary stores since they were last read); the results do not change."""
     _require_device(buf, "buf")
     if n and byte_offset + (n - 1) * stride + length > buf.numel() * buf.element_size():
         raise ValueError("batch exceeds buf")
     out = _out_tensor(out, n, buf)
+    flags = (AIPSTACK_CHKSUM_FINAL if final else 0) | (
+        AIPSTACK_CHKSUM_JUST_WRITTEN if just_written else 0)
     st = _lib.load().aipstack_chksum_batch_strided(
-        buf.data_ptr() + byte_offset, stride, length, n, out.data_ptr(),
-        AIPSTACK_CHKSUM_FINAL if final else 0, _stream_handle(stream, buf))
+        buf.data_ptr() + byte_offset, stride, length, n, out.data_ptr(), flags,
+        _stream_handle(stream, buf))
     _check(st, "aipstack_chksum_batch_strided")
     return out
 

@@ -565,6 +565,22 @@ __device__ __forceinline__ uint32_t dword_keep(int a, int b) {
     return b > a ? ((0xFFFFFFFFu >> (32 - 8 * (b - a))) << (8 * a)) : 0u;
 }
 
+// Edge / boundary segments (the few per chunk read outside the stream): their cache policy.
+// 0 = default (the stream reads the same line again and finds it in L2), 1 = nontemporal.
+#ifndef AIPSTACK_EDGE_NT
+#define AIPSTACK_EDGE_NT 0
+#endif
+constexpr bool kEdgeNT = AIPSTACK_EDGE_NT != 0;
+
+__device__ __forceinline__ u32x4 load_edge_segment(uint64_t addr) {
+    typedef __attribute__((address_space(1))) const u32x4 gseg;
+    const gseg *p = (const gseg *)addr;
+    if constexpr (kEdgeNT)
+        return __builtin_nontemporal_load(p);
+    else
+        return *p;
+}
+
 template <bool NT>
 __device__ __forceinline__ u32x4 load_lane_segment(uint64_t addr) {
     const u32x4 *p = reinterpret_cast<const u32x4 *>(addr);
@@ -788,6 +804,9 @@ struct StreamRun {
 
     __device__ __forceinline__ u32x4 load_win(uint32_t voff, uint32_t w) const {
         if constexpr (GL) {
+            // an empty run (a chunk of empty packets on a segment boundary, possibly at the
+            // very end of an allocation) has no segment to clamp to: no load at all
+            if (nseg == 0u) return u32x4{0u, 0u, 0u, 0u};
             const uint32_t k = min(w * 64u + (voff >> 4), nseg - 1u);
             typedef __attribute__((address_space(1))) const u32x4 gseg;
             const gseg *p = (const gseg *)(A + 16ull * k);
@@ -1157,9 +1176,8 @@ __device__ __forceinline__ uint32_t sum_gathered_chunks(uint64_t a, uint32_t l, 
     u32x4 fseg = {0u, 0u, 0u, 0u}, lseg = {0u, 0u, 0u, 0u};
     const uint32_t te = ((rs + l - 1u) & 15u) + 1u;  // the chunk's end in its last segment
     if constexpr (EDGE) {
-        typedef __attribute__((address_space(1))) const u32x4 gseg;
-        if (ns && rs != 0u) fseg = *(const gseg *)(a & ~(uint64_t)15);
-        if (ns && te != 16u) lseg = *(const gseg *)((a + l - 1u) & ~(uint64_t)15);
+        if (ns && rs != 0u) fseg = load_edge_segment(a & ~(uint64_t)15);
+        if (ns && te != 16u) lseg = load_edge_segment((a + l - 1u) & ~(uint64_t)15);
     }
     ld.issue(0, va, ka);
     const uint32_t foreign = EDGE && ns ? foreign_halves(fseg, lseg, (int)rs, (int)te) : 0u;
@@ -1206,7 +1224,7 @@ __device__ __forceinline__ uint32_t sum_segtab_chunk(uint64_t S, uint64_t E, int
     const uint32_t rel = (uint32_t)(S - A);
     const uint32_t g = rel >> 4, o = rel & 15u;
     u32x4 bseg = {0u, 0u, 0u, 0u};
-    if (lane <= cnt && o != 0u) bseg = load_segment<false>(rsrc, g * 16u, 0u);
+    if (lane <= cnt && o != 0u) bseg = load_segment<kEdgeNT>(rsrc, g * 16u, 0u);
     constexpr int U = 8;
     u32x4 va[U], vb[U];
     auto issue = [&](u32x4 (&v)[U], uint32_t w) {
@@ -1291,10 +1309,9 @@ __device__ __forceinline__ uint32_t sum_slot_windows(uint64_t S, uint64_t E, int
     const uint32_t nseg = len ? (rs + len + 15u) >> 4 : 0u;
     const uint32_t te = ((rs + len - 1u) & 15u) + 1u;  // the packet's end in its last segment
     // the edge segments' foreign bytes (none on a segment edge), read before the windows
-    typedef __attribute__((address_space(1))) const u32x4 gseg;
     u32x4 fseg = {0u, 0u, 0u, 0u}, lseg = {0u, 0u, 0u, 0u};
-    if (nseg && rs != 0u) fseg = *(const gseg *)(A0);
-    if (nseg && te != 16u) lseg = *(const gseg *)(A0 + 16ull * (nseg - 1u));
+    if (nseg && rs != 0u) fseg = load_edge_segment(A0);
+    if (nseg && te != 16u) lseg = load_edge_segment(A0 + 16ull * (nseg - 1u));
     uint32_t mine = 0;  // lane j < cnt: packet j's exact halves-sum (whole segments)
     for (int k0 = 0; k0 < cnt; k0 += kSlotGroup) {
         u32x4 v[kSlotGroup][2];
@@ -1394,10 +1411,7 @@ __device__ __forceinline__ uint32_t sum_stream_chunk(uint64_t S, uint64_t E, int
         const uint64_t A = S0 & ~(uint64_t)15;
         const uint32_t o = (uint32_t)S & 15u;
         u32x4 bseg = {0u, 0u, 0u, 0u};
-        if (S != X1 && o != 0u) {
-            typedef __attribute__((address_space(1))) const u32x4 gseg;
-            bseg = *(const gseg *)(S & ~(uint64_t)15);
-        }
+        if (S != X1 && o != 0u) bseg = load_edge_segment(S & ~(uint64_t)15);
         run.begin(A, X1, voff);
         run.template prefixes<1, true>(bs, hb, hx, voff);
         hb[0] += S != X1 ? halves_below_seg(bseg, o) : 0u;
@@ -1414,20 +1428,33 @@ __device__ __forceinline__ uint32_t sum_stream_chunk(uint64_t S, uint64_t E, int
 // window w loads segment 64w + L), groups of 8 windows double-buffered -- and no cross-lane
 // work per window. Each lane keeps the sum of its own column (its segments of the windows
 // consumed so far, C). Boundary j of the chunk (packet starts S_0..S_{cnt-1} and the run's end
-// X1, lane j holding b_j) lies in segment g_j = 64 W + B; when window W is consumed, every lane
-// writes X_{j,L} = C_L + (L < B ? s_L : 0) to row j of an LDS table, so that the sum over L of
-// X_{j,L} is the halves-sum of the whole segments before b_j. The bytes of segment g_j below
-// b_j (P_j) come from one segment load per lane at the start (default cache policy; the stream
-// reads that line again later). Packet j's exact halves-sum is then
-//     sum over L of (X_{j+1,L} - X_{j,L}) + P_{j+1} - P_j   (mod 2^32, exact: < 2^17 bytes),
+// X1, lane j holding b_j) lies at byte o_j of segment g_j = 64 W + B; when window W is
+// consumed, every lane writes X_{j,L} = C_L + (L < B ? s_L : 0) to row j of an LDS table, so
+// that the sum over L of X_{j,L} is the halves-sum of the whole segments before b_j. P_j, the
+// halves of segment g_j's bytes below o_j, is added per packet at the end:
+//     packet j = sum over L of (X_{j+1,L} - X_{j,L}) + P_{j+1} - P_j   (mod 2^32, exact),
 // the column differences added by 64 / cp lanes per packet from the table, then a butterfly.
 // Per window: 4 v_sad_u16 and one add per lane; per boundary a select, an add and an LDS write
 // (stream mode: a 6-step DPP scan per window and 5 ds_bpermute per boundary).
+//
+// Where P_j's bytes come from:
+//   CAPTURE = false (the default): one default-policy segment load per lane ahead of the
+//     stream (the stream finds those lines in L2 later). Steady state 219-223 us on A.
+//   CAPTURE = true (AIPSTACK_CHKSUM_JUST_WRITTEN, round 6): captured from the stream -- lane B
+//     writes the boundary's segment to a 17-entry LDS table as window W passes (one
+//     ds_write_b128 under a one-lane exec mask), lane j reads entry j after the stream; no
+//     line of the batch is read through the L2-allocating path. Steady state 228-235 us.
+// A default-policy read of a line that plain (write-back) stores wrote since it was last read
+// costs the memory side far more than a nontemporal one, and slows the whole stream, not just
+// that load: A's first read after a plain-store writer 285-312 us with the loads against
+// 242-258 captured; after DMA or nontemporal stores 221-231 against 231-240 (DESIGN 6.1,
+// tools/fresh.py, profiles/r06/).
 constexpr int kColMaxPackets = 16;
-typedef uint32_t ColRows[(kColMaxPackets + 1) * kWave];
+constexpr uint32_t kColSegTab = (kColMaxPackets + 1) * kWave;  // dword offset of the segments
+typedef uint32_t ColRows[(kColMaxPackets + 1) * kWave + (kColMaxPackets + 1) * 4];
 
 // U: windows per group (8; 6 for chunks of one long packet, launch_short_runs).
-template <bool NT, int U = 8>
+template <bool NT, int U = 8, bool CAPTURE = false>
 __device__ __forceinline__ uint32_t sum_column_chunk(uint64_t S, uint64_t E, int lane, int cnt,
                                                      uint32_t voff, uint32_t cpk, uint32_t *rows) {
     const uint64_t X1 = readlane64(E, cnt - 1);  // end of the chunk's last packet
@@ -1439,11 +1466,12 @@ __device__ __forceinline__ uint32_t sum_column_chunk(uint64_t S, uint64_t E, int
     const uint32_t nwin = (nseg + (uint32_t)kWave - 1u) >> 6;
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         reinterpret_cast<void *>(A), (short)0, (int)(nseg * 16u), 0x00020000);
-    const uint32_t rel = (uint32_t)(S - A);
-    const uint32_t g = rel >> 4, o = rel & 15u;
-    // P_j: boundary j's segment below it (lanes 0..cnt; none on a segment edge)
-    u32x4 bseg = {0u, 0u, 0u, 0u};
-    if (lane <= cnt && o != 0u) bseg = load_segment<false>(rsrc, g * 16u, 0u);
+    const uint32_t rel = (uint32_t)(S - A);  // lane j: boundary j's byte in the run
+    const uint32_t o = rel & 15u;
+    uint32_t *const segs = rows + kColSegTab;  // (CAPTURE) boundary j's segment: entry j
+    u32x4 bseg = {0u, 0u, 0u, 0u};            // boundary j's segment (lanes 0..cnt, o != 0)
+    if (!CAPTURE && lane <= cnt && o != 0u)
+        bseg = load_segment<kEdgeNT>(rsrc, (rel >> 4) * 16u, 0u);
     u32x4 va[U], vb[U];
     auto issue = [&](u32x4 (&v)[U], uint32_t w) {
 #pragma unroll
@@ -1452,9 +1480,9 @@ __device__ __forceinline__ uint32_t sum_column_chunk(uint64_t S, uint64_t E, int
             __builtin_amdgcn_sched_barrier(0);
         }
     };
-    uint32_t C = 0;                                                 // this lane's column sum
-    uint32_t jb = 0;                                                // next boundary (uniform)
-    uint32_t gj = (uint32_t)__builtin_amdgcn_readlane((int)g, 0);  // its segment
+    uint32_t C = 0;                                                   // this lane's column sum
+    uint32_t jb = 0;                                                  // next boundary (uniform)
+    uint32_t rj = (uint32_t)__builtin_amdgcn_readlane((int)rel, 0);  // its byte in the run
     auto consume = [&](const u32x4 (&v)[U], uint32_t w) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -1462,10 +1490,15 @@ __device__ __forceinline__ uint32_t sum_column_chunk(uint64_t S, uint64_t E, int
             if (wu >= nwin) break;
             const uint32_t s =
                 halves(v[u][0], halves(v[u][1], halves(v[u][2], halves(v[u][3], 0u))));
-            while (jb <= (uint32_t)cnt && (gj >> 6) == wu) {
-                rows[jb * kWave + (uint32_t)lane] = C + ((uint32_t)lane < (gj & 63u) ? s : 0u);
+            while (jb <= (uint32_t)cnt && (rj >> 10) == wu) {
+                const uint32_t B = (rj >> 4) & 63u;  // the lane holding the boundary's segment
+                rows[jb * kWave + (uint32_t)lane] = C + ((uint32_t)lane < B ? s : 0u);
+                if constexpr (CAPTURE) {
+                    if ((rj & 15u) != 0u && (uint32_t)lane == B)
+                        *reinterpret_cast<u32x4 *>(segs + jb * 4u) = v[u];
+                }
                 ++jb;
-                gj = jb <= (uint32_t)cnt ? (uint32_t)__builtin_amdgcn_readlane((int)g, (int)jb)
+                rj = jb <= (uint32_t)cnt ? (uint32_t)__builtin_amdgcn_readlane((int)rel, (int)jb)
                                          : ~0u;
             }
             C += s;
@@ -1487,10 +1520,13 @@ __device__ __forceinline__ uint32_t sum_column_chunk(uint64_t S, uint64_t E, int
     } else {
         consume(va, gi * U);
     }
-    for (; jb <= (uint32_t)cnt; ++jb) rows[jb * kWave + (uint32_t)lane] = C;  // at the run's end
-    const uint32_t P = halves_below_seg(bseg, o);
+    // boundaries at the run's end (X1 on a segment edge: nothing of its segment below it)
+    for (; jb <= (uint32_t)cnt; ++jb) rows[jb * kWave + (uint32_t)lane] = C;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
+    if (CAPTURE && lane <= cnt && o != 0u)  // every such boundary's window was consumed
+        bseg = *reinterpret_cast<const u32x4 *>(segs + (uint32_t)lane * 4u);
+    const uint32_t P = halves_below_seg(bseg, o);
     // packet j = lane >> ql: its 2^ql lanes add cpk column differences each
     const uint32_t ql = 6u - (uint32_t)__builtin_ctz(cpk);  // cpk: a power of two <= 16
     const uint32_t j = (uint32_t)lane >> ql, part = (uint32_t)lane & ((1u << ql) - 1u);
@@ -1542,8 +1578,8 @@ __device__ __forceinline__ uint32_t sum_gapped_column_chunk(uint64_t s0, int lan
     const uint32_t te = ((rs + d.len - 1u) & 15u) + 1u;
     const uint32_t pkoff = (uint32_t)lane * (uint32_t)d.stride;  // lanes < cnt: < span
     u32x4 fseg = {0u, 0u, 0u, 0u}, lseg = {0u, 0u, 0u, 0u};
-    if (lane < cnt && rs != 0u) fseg = load_segment<false>(rsrc, pkoff, 0u);
-    if (lane < cnt && te != 16u) lseg = load_segment<false>(rsrc, pkoff + 16u * (ns - 1u), 0u);
+    if (lane < cnt && rs != 0u) fseg = load_segment<kEdgeNT>(rsrc, pkoff, 0u);
+    if (lane < cnt && te != 16u) lseg = load_segment<kEdgeNT>(rsrc, pkoff + 16u * (ns - 1u), 0u);
 // windows per group (A/B build switch; A2K 228.9-229.7 us at 6 and 228.9-229.6 at 8,
 // profiles/r05/gcu)
 #ifndef AIPSTACK_GAPCOL_WINDOWS

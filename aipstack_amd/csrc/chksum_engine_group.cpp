@@ -60,6 +60,15 @@ struct Part {
 
 struct Batch {
     std::vector<Part> parts;  // one per engine
+    int waiters = 0;          // _wait calls blocked on this ticket (not the one that owns it)
+};
+
+// The outcome of a batch that completed while other _wait calls were blocked on it: each of
+// them returns it too (then it is dropped). Calls made after the completion return OK.
+struct Finished {
+    int result = AIPSTACK_CHKSUM_OK;
+    std::vector<int> dev_status;
+    int waiters = 0;
 };
 
 // A persistent thread per device: runs the engine submits of its device's ranges, in order.
@@ -83,6 +92,7 @@ struct aipstack_chksum_engine_group {
     std::vector<Region> regions;  // page-locked by the group (portable, mapped)
     std::vector<std::unique_ptr<DevWorker>> workers;
     std::map<uint64_t, Batch> batches;  // tickets not yet completed
+    std::map<uint64_t, Finished> finished;  // completed with waits still blocked on them
     uint64_t next_ticket = 1;
     size_t rr = 0;                      // first device of the next batch that uses fewer
     std::mutex mu;                      // the state above; never held across an engine wait
@@ -203,15 +213,19 @@ int group_submit(aipstack_chksum_engine_group *g, uint64_t n, const void *span_p
 
 // The result of a finished batch (with g->mu held): every device's status into dev_status,
 // the first failure by device order as the return value; the batch record is dropped.
+// Waits still blocked on the ticket get the same outcome (g->finished).
 int finish_batch(aipstack_chksum_engine_group *g, std::map<uint64_t, Batch>::iterator it,
                  int *dev_status) {
     int first = AIPSTACK_CHKSUM_OK;
     const std::vector<Part> &parts = it->second.parts;
+    std::vector<int> st(parts.size());
     for (size_t k = 0; k < parts.size(); ++k) {
-        const int st = parts[k].used ? parts[k].status : AIPSTACK_CHKSUM_OK;
-        if (dev_status) dev_status[k] = st;
-        if (first == AIPSTACK_CHKSUM_OK && st != AIPSTACK_CHKSUM_OK) first = st;
+        st[k] = parts[k].used ? parts[k].status : AIPSTACK_CHKSUM_OK;
+        if (dev_status) dev_status[k] = st[k];
+        if (first == AIPSTACK_CHKSUM_OK && st[k] != AIPSTACK_CHKSUM_OK) first = st[k];
     }
+    if (it->second.waiters > 0)
+        g->finished[it->first] = Finished{first, std::move(st), it->second.waiters};
     g->batches.erase(it);
     return first;
 }
@@ -378,6 +392,7 @@ extern "C" int aipstack_chksum_engine_group_wait(aipstack_chksum_engine_group *g
             return ticket != 0 && ticket < g->next_ticket ? AIPSTACK_CHKSUM_OK
                                                           : AIPSTACK_CHKSUM_EINVAL;
         // every range submitted, and none owned by another thread's wait
+        ++it->second.waiters;
         g->submitted.wait(lock, [&] {
             it = g->batches.find(ticket);
             if (it == g->batches.end()) return true;
@@ -385,7 +400,16 @@ extern "C" int aipstack_chksum_engine_group_wait(aipstack_chksum_engine_group *g
                 if (p.used && (!p.submitted || (p.waiting && !p.done))) return false;
             return true;
         });
-        if (it == g->batches.end()) return AIPSTACK_CHKSUM_OK;  // completed by another thread
+        if (it == g->batches.end()) {  // completed by another thread meanwhile: its outcome
+            const auto f = g->finished.find(ticket);
+            if (f == g->finished.end()) return AIPSTACK_CHKSUM_OK;  // (not reachable)
+            const int r = f->second.result;
+            if (dev_status)
+                std::copy(f->second.dev_status.begin(), f->second.dev_status.end(), dev_status);
+            if (--f->second.waiters == 0) g->finished.erase(f);
+            return r;
+        }
+        --it->second.waiters;
         // this wait owns the open parts: a concurrent _poll treats them as pending, so an
         // engine failure this wait consumes is reported here, once
         for (size_t k = 0; k < it->second.parts.size(); ++k) {

@@ -79,19 +79,22 @@ __global__ __launch_bounds__(kBlock) void chksum_batch_kernel(Desc desc, uint64_
     // gapped column runs (sum_gapped_column_chunk): owners by arithmetic, no gathered stream
     constexpr bool kGapCols = std::is_same<Desc, GappedColDesc>::value;
     constexpr bool kGathered = !Desc::kStream && SU > 0 && !kSlotWin && !kGapCols;
-    __shared__ typename std::conditional<kSlotWin, SlotRows[kWavesPerBlock], char>::type slot_rows;
+    // 16-byte aligned by construction: the tables are read with ds_read_b128 (u32x4)
+    alignas(16) __shared__ typename std::conditional<kSlotWin, SlotRows[kWavesPerBlock], char>::type slot_rows;
     struct GatheredShared {
         GatherLds g[kWavesPerBlock];
         // the byte-mask table, for edges masked in the stream only
         typename std::conditional<Desc::kEdge, char, KeepTable>::type keep;
     };
     __shared__ typename std::conditional<kGathered, GatheredShared, char>::type gsh;
-    // column runs (sum_column_chunk): SU 64 = groups of 8 windows, 48 = groups of 6
-    constexpr bool kColumns = Desc::kStream && (SU == 64 || SU == 48);
-    __shared__ typename std::conditional<kColumns || kGapCols, ColRows[kWavesPerBlock], char>::type
+    // column runs (sum_column_chunk): SU 64 = groups of 8 windows, 48 = groups of 6; 66 / 50
+    // the same with the boundary segments captured from the stream (AIPSTACK_CHKSUM_JUST_WRITTEN)
+    constexpr bool kColumns = Desc::kStream && (SU == 64 || SU == 48 || SU == 66 || SU == 50);
+    constexpr bool kColCapture = SU == 66 || SU == 50;
+    alignas(16) __shared__ typename std::conditional<kColumns || kGapCols, ColRows[kWavesPerBlock], char>::type
         col_rows;
     constexpr bool kSegTab = Desc::kStream && SU == 96;   // segment tables (sum_segtab_chunk)
-    __shared__ typename std::conditional<kSegTab, SegTab[kWavesPerBlock], char>::type seg_tab;
+    alignas(16) __shared__ typename std::conditional<kSegTab, SegTab[kWavesPerBlock], char>::type seg_tab;
     if constexpr (kGathered) {
         if constexpr (!Desc::kEdge) {  // edges masked in the stream: the mask table
             fill_keep_table(gsh.keep);
@@ -145,7 +148,8 @@ __global__ __launch_bounds__(kBlock) void chksum_batch_kernel(Desc desc, uint64_
                     sums = sum_segtab_chunk<NT>(lS, lE, lane, cnt, voff, chunk_packets,
                                                 seg_tab[wave_in_block]);
                 else if constexpr (kColumns)
-                    sums = sum_column_chunk<NT, SU == 48 ? 6 : 8>(lS, lE, lane, cnt, voff,
+                    sums = sum_column_chunk<NT, (SU == 48 || SU == 50) ? 6 : 8, kColCapture>(
+                        lS, lE, lane, cnt, voff,
                                                                    chunk_packets,
                                                                    col_rows[wave_in_block]);
                 else
@@ -705,13 +709,20 @@ int launch_short_runs(const Desc &desc, uint64_t n, uint32_t len, uint16_t *d_ou
         // loaded against 16 in groups of 8; under the driver's protocol B 336.8-337.7 us
         // against 338.3-344.0 (A, 12 KiB chunks, keeps 8: 220.9-221.9 against 222.7-223.1;
         // profiles/r05/colu)
+        // AIPSTACK_CHKSUM_JUST_WRITTEN: the form that reads no line of the batch through the
+        // L2-allocating path (sum_column_chunk CAPTURE)
+        const bool fresh = (flags & AIPSTACK_CHKSUM_JUST_WRITTEN) != 0;
         if constexpr (!Desc::kCsr) {
             if (sh.chunk_packets == 1u && len > 8192u)
-                return launch_k<Desc, 1, 1, true, SEEDED, 48>(desc, n, sh, d_out, flags, stream,
-                                                              true, kShortRunLds);
+                return fresh ? launch_k<Desc, 1, 1, true, SEEDED, 50>(desc, n, sh, d_out, flags,
+                                                                      stream, true, kShortRunLds)
+                             : launch_k<Desc, 1, 1, true, SEEDED, 48>(desc, n, sh, d_out, flags,
+                                                                      stream, true, kShortRunLds);
         }
-        return launch_k<Desc, 1, 1, true, SEEDED, 64>(desc, n, sh, d_out, flags, stream, true,
-                                                      kShortRunLds);
+        return fresh ? launch_k<Desc, 1, 1, true, SEEDED, 66>(desc, n, sh, d_out, flags, stream,
+                                                              true, kShortRunLds)
+                     : launch_k<Desc, 1, 1, true, SEEDED, 64>(desc, n, sh, d_out, flags, stream,
+                                                              true, kShortRunLds);
     }
     if (mode == 1)  // global loads (SU 32)
         return launch_k<Desc, 1, 1, true, SEEDED, 32>(desc, n, sh, d_out, flags, stream, true,

@@ -150,7 +150,53 @@ def parse():
                         "Infinity Cache); frames and ring slots (RX, TX, TXREC, RX2K, TX2K, "
                         "C2K): R copies of the batch at distinct addresses; 1 = one batch "
                         "read by every step")
+    p.add_argument("--fresh", choices=FRESH_WRITERS, default=None,
+                   help="fresh-data mode (DESIGN 6.1): before every launch (warm-ups included) "
+                        "the batch it reads is rewritten from a pristine copy by WRITER -- dma "
+                        "(pinned host -> device copy), nt (a device kernel with nontemporal "
+                        "stores), plain (a device kernel with ordinary stores), d2d "
+                        "(hipMemcpyAsync device -> device). Only the checksum launches are timed "
+                        "(an event pair around each); the line carries 'fresh'")
+    p.add_argument("--just-written", action="store_true",
+                   help="pass the AIPSTACK_CHKSUM_JUST_WRITTEN hint (strided batches)")
     return p.parse_args()
+
+
+FRESH_WRITERS = ("dma", "nt", "plain", "d2d")
+
+
+def fresh_writer(kind, targets, stream):
+    """writer(k): rewrite targets[k mod R] from a pristine copy taken now, on `stream` (the
+    launch stream, so the checksum launch after it reads the new bytes). Bench plumbing."""
+    import torch
+    pristine = [t.clone() for t in targets]
+    if kind == "dma":
+        host = [torch.empty(t.numel(), dtype=torch.uint8, pin_memory=True) for t in targets]
+        for h, t in zip(host, targets):
+            h.copy_(t.cpu())
+    lib = None
+    if kind in ("nt", "plain"):
+        lib = ctypes.CDLL(os.path.join(ROOT, "tools", "build", "libfresh_probe.so"))
+        lib.fp_copy.restype = ctypes.c_int
+        lib.fp_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int,
+                                ctypes.c_void_p]
+    torch.cuda.synchronize()
+
+    def write(k):
+        r = k % len(targets)
+        t, p = targets[r], pristine[r]
+        if kind == "dma":
+            t.copy_(host[r], non_blocking=True)
+        elif kind == "d2d":
+            t.copy_(p)
+        else:
+            body = (t.numel() // 16) * 16
+            if lib.fp_copy(t.data_ptr(), p.data_ptr(), body, int(kind == "nt"),
+                           stream.cuda_stream) != 0:
+                raise SystemExit("fresh writer: fp_copy failed")
+            if body < t.numel():
+                t[body:].copy_(p[body:])
+    return write
 
 
 # Layouts whose batch is synthesised on the host: rotated over copies at other addresses.
@@ -662,7 +708,7 @@ def main():
         step_no[0] = k + 1
         if layout == "strided":
             A.chksum_batch_strided(bufs[k % rot], stride, plen, n, out=outs[k % rot],
-                                   stream=stream)
+                                   stream=stream, just_written=args.just_written)
         elif layout == "csr":
             A.chksum_batch_csr(bufs[k % rot], d_off, out=outs[k % rot], stream=stream)
         elif layout == "rx":
@@ -688,9 +734,38 @@ def main():
             A.tx_fill(fbufs[k % len(fbufs)], d_off, out=status, stream=stream,
                       split=args.tx_split, workspace=tx_ws)
 
+    # fresh-data mode: the buffers each step reads, rewritten before it
+    writer = None
+    if args.fresh:
+        if layout in ("strided", "csr"):
+            targets = bufs
+        elif layout == "chain":
+            targets = [chain["buf"]] + [cc["buf"] for cc in chain_rot]
+        else:
+            targets = fbufs
+        writer = fresh_writer(args.fresh, targets, stream)
+
     for _ in range(args.warmup):
+        if writer:
+            writer(step_no[0])
         step()
     torch.cuda.synchronize()
+
+    # ---- solo phase (N > 1): each rank in turn runs the K steps alone while the others wait
+    # at a barrier -- the per-GPU rate with no other GPU of the node busy, the denominator of
+    # scaling_efficiency (SURVEY.md:445)
+    solo_s = None
+    if world > 1 and not writer:
+        for r in range(world):
+            dist.barrier()
+            if r == rank:
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(args.steps):
+                    step()
+                torch.cuda.synchronize()
+                solo_s = time.perf_counter() - t0
+        dist.barrier()
 
     # ---- timed region: barrier + synchronize on both sides; one HIP event pair on the
     # launch stream brackets the K launches, so the per-launch average includes the
@@ -700,21 +775,37 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
-        step()
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    fresh_us = []
+    if writer:
+        # fresh data: an event pair around each checksum launch, the rewrite before it untimed;
+        # elapsed = the sum of the launches' times
+        pairs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                 for _ in range(args.steps)]
+        for a, b in pairs:
+            writer(step_no[0])
+            a.record(stream)
+            step()
+            b.record(stream)
+        torch.cuda.synchronize()
+        fresh_us = [a.elapsed_time(b) * 1e3 for a, b in pairs]
+        elapsed = sum(fresh_us) / 1e6
+        avg_kernel_s = elapsed / args.steps
+    else:
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        for _ in range(args.steps):
+            step()
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        avg_kernel_s = ev0.elapsed_time(ev1) / 1e3 / args.steps
     if world > 1:
         dist.barrier()
-    avg_kernel_s = ev0.elapsed_time(ev1) / 1e3 / args.steps
 
     # Diagnostic, AFTER the timed region (not part of `value`): per-launch event pairs,
     # to expose outliers / clock ramps that the bracketed average smooths over.
     per_launch = []
-    if args.per_launch:
+    if args.per_launch and not writer:
         pairs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                  for _ in range(args.steps)]
         for a, b in pairs:
@@ -728,9 +819,10 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     max_elapsed = float(t.item())
-    # every rank's own wall time and kernel time (control plane only; after the timed region)
-    mine = torch.tensor([elapsed, avg_kernel_s], dtype=torch.float64)
-    ranks = [torch.zeros(2, dtype=torch.float64) for _ in range(world)]
+    # every rank's own wall time, kernel time and solo time (control plane only; after the
+    # timed region)
+    mine = torch.tensor([elapsed, avg_kernel_s, solo_s or 0.0], dtype=torch.float64)
+    ranks = [torch.zeros(3, dtype=torch.float64) for _ in range(world)]
     if world > 1:
         dist.all_gather(ranks, mine)
     else:
@@ -935,6 +1027,8 @@ def main():
         "per_gpu": {
             "GiB_s": [round(spec.get("payload", total) * args.steps / float(r[0]) / 2**30, 2)
                       for r in ranks],
+            **({"solo_GiB_s": [round(payload * args.steps / float(r[2]) / 2**30, 2)
+                               for r in ranks]} if world > 1 and not writer else {}),
             "kernel_us": [round(float(r[1]) * 1e6, 2) for r in ranks],
             "devices": pcis,
             "arch": [i["arch"] for i in infos],
@@ -946,6 +1040,29 @@ def main():
         "cpu_baseline": cpu,
         "parity": parity,
     }
+    if world > 1 and not writer:
+        # value / (N x mean solo rate): 1.0 = every rank as fast with the node busy as alone
+        solo_mean = sum(payload * args.steps / float(r[2]) / 2**30 for r in ranks) / world
+        result["scaling_efficiency"] = round(value / (world * solo_mean), 4)
+        result["scaling_efficiency_note"] = (
+            "value / (N x mean of each rank's solo GiB/s: the same K steps on its own shard with "
+            "the other ranks idle at a barrier)" + (
+                "; ranks share a device (rehearsal): not a multi-GPU figure"
+                if len(set(pcis)) != world else ""))
+    if writer:
+        srt = sorted(fresh_us)
+        result["fresh"] = {
+            "writer": args.fresh,
+            "just_written_hint": bool(args.just_written),
+            "timing": "checksum launches only: the batch each launch reads was rewritten from a "
+                      "pristine copy right before it (untimed); value and kernel_us from the sum "
+                      "of the launches' event pairs",
+            "kernel_us": {"mean": round(sum(fresh_us) / len(fresh_us), 2),
+                          "median": round(srt[len(srt) // 2], 2), "min": round(srt[0], 2),
+                          "max": round(srt[-1], 2)}}
+        result["metric"] = METRIC + " [fresh data: " + args.fresh + "-written]"
+    elif args.just_written:
+        result["just_written_hint"] = True
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
@@ -1135,7 +1252,7 @@ def e2e(args, rank, world, local_rank, layout, n, plen):
     # Diagnostic, AFTER the timed region (not part of `value`): wall time of each call
     # (every engine call is synchronous: H2D, kernels and D2H of the whole batch).
     per_launch = []
-    if args.per_launch:
+    if args.per_launch and not writer:
         for _ in range(args.steps):
             c0 = time.perf_counter()
             step()

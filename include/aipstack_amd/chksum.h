@@ -53,6 +53,15 @@ extern "C" {
 /* ---- flags for the batch entry points ------------------------------------------ */
 /* Write IpChksum (= ~IpChksumInverted, Chksum.h:122-125) instead of the inverted sum. */
 #define AIPSTACK_CHKSUM_FINAL 1u
+/* Hint (results are identical with or without it): the batch's bytes were written by device
+ * kernels with ordinary (write-back) stores since they were last read -- e.g. segments
+ * assembled on the device just before their checksum. On gfx950 a cached read of such a line
+ * costs the memory side far more than a streaming one, so the batch is then read without
+ * touching any of its lines through the L2-allocating path (config A: 242-258 us against
+ * 285-312 for the default form; the default form is faster on bytes that arrived by DMA or
+ * streaming stores, and on bytes read before). Honoured by aipstack_chksum_batch_strided for
+ * back-to-back packets of >= 1 KiB (column runs); ignored elsewhere. */
+#define AIPSTACK_CHKSUM_JUST_WRITTEN 4u
 
 /* ---- 1. per-packet host hook ----------------------------------------------------- */
 
@@ -338,7 +347,8 @@ int aipstack_chksum_engine_region_mapped(aipstack_chksum_engine *engine, const v
  * The submit_* calls enqueue a batch and return ONE group ticket at once; _poll / _wait
  * complete it: 0 = done, 1 = still running (poll), else the first failure by device order;
  * dev_status (NULL or n_devices ints) then receives each device's status (0 for a device
- * without a range). A ticket is reported once; completing it again returns 0. Each range is
+ * without a range). A ticket is reported once: to the call that completes it and to every
+ * _wait already blocked on it then; completing it again afterwards returns 0. Each range is
  * submitted to its engine on the calling thread when the batch lies in a region registered
  * with the group (the kernels read it in place) or is small, else by a persistent worker
  * thread of its device (pinned, like the engine's own host threads, to the CPUs next to the

@@ -337,6 +337,45 @@ void group_wait_and_poll_of_one_ticket() {
     aipstack_chksum_engine_group_destroy(g);
 }
 
+// Two waits of one ticket, both blocked when it completes with a failure: each returns the
+// failure and every device's status (the second once returned OK, its
+// dev_status untouched). A wait after the completion returns OK.
+void group_two_waits_of_one_ticket() {
+    int devs[2];
+    group_devices(devs);
+    aipstack_chksum_engine_group *g = nullptr;
+    EXPECT(aipstack_chksum_engine_group_create(devs, 2, kChunk, kStreams, &g) == 0, "group create");
+    if (!g) return;
+    const uint64_t n = 8000;  // 12 MB: split over both engines
+    std::vector<unsigned char> a(n * kLen);
+    aipstack_synth_fill_host(a.data(), a.size(), 25, 0);
+    std::vector<uint16_t> oa(n);
+    aipstack_chksum_engine_test_inject_only(aipstack_chksum_engine_group_engine(g, 1));
+    aipstack_chksum_engine_test_inject(0, bit(1));  // engine 1's first piece fails
+    aipstack_chksum_engine_test_wait_delay(200000);  // the owning wait sleeps 200 ms first
+    uint64_t t = 0;
+    EXPECT(aipstack_chksum_engine_group_submit_strided(g, a.data(), kLen, kLen, n, oa.data(), 0,
+                                                       &t) == 0, "group submit");
+    int ds1[2] = {-100, -100}, ds2[2] = {-100, -100};
+    std::atomic<int> w1{1}, w2{1};
+    std::thread first([&] { w1 = aipstack_chksum_engine_group_wait(g, t, ds1); });
+    std::this_thread::sleep_for(std::chrono::milliseconds(50));
+    std::thread second([&] { w2 = aipstack_chksum_engine_group_wait(g, t, ds2); });
+    first.join();
+    second.join();
+    int ds3[2] = {-100, -100};
+    const int w3 = aipstack_chksum_engine_group_wait(g, t, ds3);
+    aipstack_chksum_engine_test_wait_delay(0);
+    aipstack_chksum_engine_test_inject(0, 0);
+    aipstack_chksum_engine_test_inject_only(nullptr);
+    EXPECT(w1.load() < 0 && ds1[0] == 0 && ds1[1] < 0,
+           "the first wait reports device 1's failure (%d; %d / %d)", w1.load(), ds1[0], ds1[1]);
+    EXPECT(w2.load() == w1.load() && ds2[0] == 0 && ds2[1] == ds1[1],
+           "the second wait reports the same (%d; %d / %d)", w2.load(), ds2[0], ds2[1]);
+    EXPECT(w3 == 0, "a wait after the completion returns OK (%d)", w3);
+    aipstack_chksum_engine_group_destroy(g);
+}
+
 }  // namespace
 
 int main() {
@@ -353,6 +392,7 @@ int main() {
     poll_answers_while_submit_is_back_pressured();
     group_ticket_with_one_failing_device();
     group_wait_and_poll_of_one_ticket();
+    group_two_waits_of_one_ticket();
     if (failures) std::fprintf(stderr, "%d failures\n", failures);
     else std::printf("engine_fault_test: OK\n");
     std::fflush(nullptr);

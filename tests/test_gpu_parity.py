@@ -116,6 +116,8 @@ def test_full_size_strided(oracle, cfg, n, plen):
     # FINAL flag = bitwise NOT, packet for packet
     fin = _np(A.chksum_batch_strided(buf, plen, plen, n, final=True))
     assert np.array_equal(fin, ~got)
+    # the JUST_WRITTEN hint reads the batch another way: the same sums
+    assert np.array_equal(_np(A.chksum_batch_strided(buf, plen, plen, n, just_written=True)), got)
 
 
 def test_full_size_mixed_csr(oracle):
@@ -340,7 +342,12 @@ def test_short_runs_large_batches(oracle, plen, n, mode):
         buf = torch.empty(n * plen + 7, dtype=torch.uint8, device=DEV)
         synth.fill_device(buf, 41 + plen)
         got = _np(A.chksum_batch_strided(buf, plen, plen, n, byte_offset=7, final=True))
-        assert np.array_equal(got, oracle.batch_strided(_np(buf)[7:], plen, plen, n, final=True))
+        want = oracle.batch_strided(_np(buf)[7:], plen, plen, n, final=True)
+        assert np.array_equal(got, want)
+        # the JUST_WRITTEN hint (column runs: boundary segments captured from the stream)
+        got = _np(A.chksum_batch_strided(buf, plen, plen, n, byte_offset=7, final=True,
+                                         just_written=True))
+        assert np.array_equal(got, want)
     finally:
         _tune("short_loads", -1)
 
@@ -363,14 +370,45 @@ def test_short_run_forms_ragged(oracle, mode, chunk):
         rng = np.random.default_rng(60 + chunk + 100 * mode)
         for plen in (0, 1, 15, 16, 17, 1023, 1500, 3001):
             n = min(2999, (buf.numel() - 9) // max(plen, 1))
-            got = _np(A.chksum_batch_strided(buf, plen, plen, n, byte_offset=9))
-            assert np.array_equal(got, oracle.batch_strided(hb[9:], plen, plen, n)), plen
+            want = oracle.batch_strided(hb[9:], plen, plen, n)
+            for jw in (False, True):  # (the JUST_WRITTEN hint: column runs capture)
+                got = _np(A.chksum_batch_strided(buf, plen, plen, n, byte_offset=9,
+                                                 just_written=jw))
+                assert np.array_equal(got, want), (plen, jw)
         lens = rng.integers(0, 3000, 5001)
         lens[rng.random(lens.size) < 0.1] = 0
         off = np.concatenate([[3], 3 + np.cumsum(lens)]).astype(np.int64)
         assert off[-1] <= buf.numel()
         got = _np(A.chksum_batch_csr(buf, _d(off), final=True))
         assert np.array_equal(got, oracle.batch_csr(hb, off.astype(np.uint64), final=True))
+    finally:
+        _tune("short_loads", -1)
+        _tune("chunk_packets", 0)
+
+
+@pytest.mark.parametrize("chunk", [1, 4, 16])
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+def test_short_runs_empty_chunks_at_buffer_end(oracle, mode, chunk):
+    """A chunk of only empty packets starting on a 16-byte boundary is an empty run (no
+    segment): it must issue no load. Here such chunks sit at the end of a 16-aligned buffer
+    (ragged CSR batch, then 64 empty packets at offset == numel), in every short-run read form;
+    the global-load form (short_loads 1) once clamped its windows to segment nseg - 1 there,
+    which wrapped for nseg = 0."""
+    _tune("short_loads", mode)
+    _tune("chunk_packets", chunk)
+    try:
+        rng = np.random.default_rng(90 + mode + 10 * chunk)
+        lens = rng.integers(0, 1600, 3000)
+        off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+        size = (int(off[-1]) + 15) & ~15
+        off = np.concatenate([off, np.full(64, size, dtype=np.int64)])
+        off[-65] = size  # the last real packet runs to the aligned end
+        buf = torch.empty(size, dtype=torch.uint8, device=DEV)
+        synth.fill_device(buf, 93)
+        got = _np(A.chksum_batch_csr(buf, _d(off), final=True))
+        want = oracle.batch_csr(_np(buf), off.astype(np.uint64), final=True)
+        assert np.array_equal(got, want), np.nonzero(got != want)[0][:8]
+        assert np.all(got[-64:] == 0xFFFF)  # ~0: IpChksum of nothing
     finally:
         _tune("short_loads", -1)
         _tune("chunk_packets", 0)

@@ -430,12 +430,26 @@ def _exact_halves(buf, s, e):
 
 # ---- column runs (round 5, sum_column_chunk) -------------------------------------------
 
-def column_chunk_model(buf, S, E, cnt, cpk):
+def _below_uniform(raw_seg, o):
+    """halves_below_uniform: the prefix of the dwords below o >> 2 (the window's own sum in
+    dword order), plus dword o >> 2 masked to its o & 3 low bytes."""
+    d = raw_seg.view("<u4").astype(np.uint64)
+    q, m = o >> 2, (1 << (8 * (o & 3))) - 1
+    acc = 0
+    for k in range(q):
+        acc += (int(d[k]) & 0xFFFF) + (int(d[k]) >> 16)
+    x = int(d[q]) & m
+    return acc + (x & 0xFFFF) + (x >> 16)
+
+
+def column_chunk_model(buf, S, E, cnt, cpk, edge_loads=False):
     """sum_column_chunk, step for step: each lane's column sum C_L over the windows consumed,
-    the boundary rows X_{j,L} = C_L + (L < B_j ? s_L : 0) written when boundary j's window is
-    consumed (the rest after the last window), the per-boundary partial P_j from its own
-    segment, then packet j = sum_L (X_{j+1,L} - X_{j,L}) + P_{j+1} - P_j, all mod 2^32; the
-    reduction as the kernel does it (64 / cpk lanes per packet, cpk columns each)."""
+    the boundary rows written when boundary j's window is consumed (the rest after the last
+    window), then packet j = sum_L (X_{j+1,L} - X_{j,L}), all mod 2^32; the reduction as the
+    kernel does it (64 / cpk lanes per packet, cpk columns each). Round 6 (default):
+    X_{j,L} = C_L + (L < B_j ? s_L : L == B_j ? the bytes of the segment below o_j : 0), the
+    partial segment taken from the stream. Round 5 (edge_loads): X_{j,L} = C_L + (L < B_j ?
+    s_L : 0), and the partial P_j from a separate load of boundary j's segment, + P_{j+1} - P_j."""
     X1 = int(E[cnt - 1])
     b = [int(S[j]) if j < cnt else X1 for j in range(64)]
     A = b[0] & ~15
@@ -446,19 +460,24 @@ def column_chunk_model(buf, S, E, cnt, cpk):
     o = [(x - A) & 15 for x in b]
     rows = np.zeros((cnt + 1, 64), dtype=np.uint64)
     C = np.zeros(64, dtype=np.uint64)
+    lanes = np.arange(64)
     jb = 0
     for w in range(nwin):
         s = seg[w * 64:(w + 1) * 64].astype(np.uint64)
         while jb <= cnt and (g[jb] >> 6) == w:
             B = g[jb] & 63
-            rows[jb] = (C + np.where(np.arange(64) < B, s, 0)) & M32
+            x = np.where(lanes < B, s, 0)
+            if not edge_loads:  # lane B: its own segment's bytes below o_j (0 past the run)
+                x[B] = _below_uniform(raw[g[jb] * 16:g[jb] * 16 + 16], o[jb])
+            rows[jb] = (C + x) & M32
             jb += 1
         C = (C + s) & M32
-    while jb <= cnt:
+    while jb <= cnt:  # boundaries past the last window: X1 on a segment edge, o = 0
+        assert o[jb] == 0
         rows[jb] = C
         jb += 1
-    P = [(_below(raw[g[j] * 16:g[j] * 16 + 16], o[j]) if (j <= cnt and o[j]) else 0)
-         for j in range(64)]
+    P = [(_below(raw[g[j] * 16:g[j] * 16 + 16], o[j]) if (edge_loads and j <= cnt and o[j])
+          else 0) for j in range(64)]
     q = 64 // cpk
     sums = []
     for j in range(cnt):
@@ -470,9 +489,10 @@ def column_chunk_model(buf, S, E, cnt, cpk):
     return sums + [0] * (64 - cnt)
 
 
+@pytest.mark.parametrize("edge_loads", [False, True])
 @pytest.mark.parametrize("cpk", [1, 2, 4, 8, 16])
 @pytest.mark.parametrize("case", ["tiny", "mixed", "mtu", "jumbo", "aligned_end"])
-def test_column_model_matches_oracle(oracle, case, cpk):
+def test_column_model_matches_oracle(oracle, case, cpk, edge_loads):
     rng = np.random.default_rng(hash((case, cpk, "col")) % 2**32)
     base = int(rng.integers(0, 16))
     if case == "tiny":
@@ -495,7 +515,7 @@ def test_column_model_matches_oracle(oracle, case, cpk):
         cnt = min(cpk, n - p0)
         S = [int(off[p0 + j]) for j in range(cnt)]
         E = [int(off[p0 + j + 1]) for j in range(cnt)]
-        got[p0:p0 + cnt] = finish(column_chunk_model(buf, S, E, cnt, cpk)[:cnt], S)
+        got[p0:p0 + cnt] = finish(column_chunk_model(buf, S, E, cnt, cpk, edge_loads)[:cnt], S)
     want = oracle.batch_csr(buf, off)
     assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
 

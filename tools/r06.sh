@@ -1,0 +1,120 @@
+#!/bin/bash
+# Round-6 GPU experiments, one mode per gpurun call; output under gpurun_out/r06/<mode>.
+#   fresh   tools/fresh.py: the first read of a freshly written batch, by writer, reader,
+#           granularity and age; plus the counters this box's rocprofv3 offers
+set -e
+mode=${1:?mode}
+out=gpurun_out/r06/$mode
+mkdir -p "$out"
+export TMPDIR=/tmp
+
+case $mode in
+fresh)
+  (timeout -k 10 60 rocprofv3 -L > "$out/avail.txt" 2>&1 || true)
+  timeout -k 10 600 python3 -u tools/fresh.py > "$out/fresh.jsonl" 2> "$out/fresh.err"
+  ;;
+fresh2)  # which reader pays (pure-read modes, the checksum, the edge loads nontemporal), and
+         # per-dispatch counters of the driver's command: launches 1-3 (each batch's first
+         # read) against 4-25
+  timeout -k 10 300 python3 -u tools/fresh.py readers base fresh_kcopy > "$out/readers.jsonl" 2> "$out/readers.err"
+  AIPSTACK_AMD_LIB=$PWD/tools/build/lib_edgent.so timeout -k 10 300 python3 -u tools/fresh.py \
+      readers base fresh_kcopy > "$out/readers_edgent.jsonl" 2> "$out/readers_edgent.err"
+  pmc() {  # pmc NAME COUNTERS...
+    name=$1; shift
+    timeout -s KILL 120 rocprofv3 --kernel-trace --output-format csv -d "$out/pmc_$name" -o run \
+        --pmc "$@" -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-ceiling \
+        --no-parity > "$out/pmc_$name.log" 2>&1
+  }
+  pmc fetch FETCH_SIZE
+  pmc ea TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCC_HIT_sum TCC_MISS_sum
+  pmc probe TCC_PROBE_sum TCC_PROBE_ALL_sum TCC_EA0_RDREQ_DRAM_sum TCC_EA0_WRREQ_DRAM_sum
+  pmc tcp TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum
+  pmc sq SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE
+  ;;
+col6)  # round-6 column runs (partial segments from the stream) against round 5's edge loads:
+       # parity of the forms, fresh-data and steady-state reads, the driver's command
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+      -k "every_read_form or short_runs or full_size or config_d or ragged or lengths or empty_chunks or all_zero" \
+      > "$out/pytest.log" 2>&1
+  for lib in product coledge product coledge; do
+    if [ $lib = product ]; then L=$PWD/aipstack_amd/lib/libaipstack_chksum.so; else L=$PWD/tools/build/lib_$lib.so; fi
+    AIPSTACK_AMD_LIB=$L timeout -k 10 300 python3 -u tools/fresh.py base fresh_synth fresh_d2d \
+        fresh_kcopy fresh_h2d steady >> "$out/fresh_$lib.jsonl" 2>> "$out/fresh_$lib.err"
+    AIPSTACK_AMD_LIB=$L timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 \
+        --per-launch --no-cpu-baseline --no-ceiling >> "$out/bench_$lib.json" 2>> "$out/bench_$lib.err"
+  done
+  ;;
+col6b)  # the same after the window prefixes were shared with the partial segments; occupancy
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+      -k "every_read_form or short_runs or full_size or config_d or ragged or lengths or empty_chunks or all_zero" \
+      > "$out/pytest.log" 2>&1
+  timeout -k 10 300 python3 -u tools/fresh.py base fresh_synth fresh_d2d fresh_kcopy fresh_h2d steady \
+      > "$out/fresh.jsonl" 2> "$out/fresh.err"
+  timeout -k 10 300 python3 tools/ab.py --config A --variants \
+      "gather=1;gather=1,lds_pad=20000;gather=1,lds_pad=30000" > "$out/ab_A.jsonl" 2> "$out/ab_A.err"
+  for i in 1 2; do
+    timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --per-launch --no-cpu-baseline \
+        --no-ceiling >> "$out/bench_A.json" 2>> "$out/bench.err"
+  done
+  timeout -k 10 300 python3 bench.py --config B --steps 20 --warmup 5 --per-launch --no-cpu-baseline \
+      --no-ceiling >> "$out/bench_B.json" 2>> "$out/bench.err"
+  ;;
+col6c)  # column runs capturing the boundary segments from the stream (AIPSTACK_COL_PARTIAL 0)
+        # against round 5's edge loads (lib_colp1), alternating processes
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+      -k "every_read_form or short_runs or full_size or config_d or ragged or lengths or empty_chunks or all_zero" \
+      > "$out/pytest.log" 2>&1
+  timeout -k 10 300 python3 tools/ab.py --config A --variants \
+      "gather=1;gather=1,lds_pad=20000" > "$out/ab_A.jsonl" 2> "$out/ab_A.err"
+  for lib in product colp1 product colp1; do
+    if [ $lib = product ]; then L=$PWD/aipstack_amd/lib/libaipstack_chksum.so; else L=$PWD/tools/build/lib_$lib.so; fi
+    AIPSTACK_AMD_LIB=$L timeout -k 10 300 python3 -u tools/fresh.py base fresh_synth fresh_d2d \
+        fresh_h2d steady >> "$out/fresh_$lib.jsonl" 2>> "$out/fresh_$lib.err"
+    AIPSTACK_AMD_LIB=$L timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 \
+        --per-launch --no-cpu-baseline --no-ceiling >> "$out/bench_$lib.json" 2>> "$out/bench_$lib.err"
+  done
+  timeout -k 10 300 python3 bench.py --config B --steps 20 --warmup 5 --per-launch --no-cpu-baseline \
+      --no-ceiling >> "$out/bench_B.json" 2>> "$out/bench.err"
+  ;;
+pf6)  # column runs: capture (product) / round-5 edge loads (colp1) / capture + scalar touches of
+      # the boundary lines (spf) / capture + default-policy vector touches after group 0 (vpf)
+  timeout -k 10 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+      -k "every_read_form or short_runs or full_size" > "$out/pytest.log" 2>&1
+  for r in 1 2; do
+    for lib in ${LIBS:-product spf vpf}; do
+      if [ $lib = product ]; then L=$PWD/aipstack_amd/lib/libaipstack_chksum.so; else L=$PWD/tools/build/lib_$lib.so; fi
+      AIPSTACK_AMD_LIB=$L timeout -k 10 300 python3 -u tools/fresh.py fresh_synth fresh_d2d steady \
+          >> "$out/fresh_$lib.jsonl" 2>> "$out/fresh_$lib.err"
+      AIPSTACK_AMD_LIB=$L timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 \
+          --per-launch --no-cpu-baseline --no-ceiling >> "$out/bench_$lib.json" 2>> "$out/bench_$lib.err"
+    done
+  done
+  ;;
+pmc6)  # per-dispatch counters, column runs with and without the round-5 edge loads
+  pmc() {  # pmc LIB NAME COUNTERS...
+    lib=$1; name=$2; shift 2
+    if [ $lib = product ]; then L=$PWD/aipstack_amd/lib/libaipstack_chksum.so; else L=$PWD/tools/build/lib_$lib.so; fi
+    AIPSTACK_AMD_LIB=$L timeout -s KILL 120 rocprofv3 --kernel-trace --output-format csv \
+        -d "$out/${lib}_$name" -o run --pmc "$@" -- python3 bench.py --steps 20 --warmup 5 \
+        --no-cpu-baseline --no-ceiling --no-parity > "$out/${lib}_$name.log" 2>&1
+  }
+  for lib in ${LIBS:-product colp1}; do
+    pmc $lib fetch FETCH_SIZE
+    pmc $lib ea TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_128B_sum TCC_HIT_sum TCC_MISS_sum
+    pmc $lib req TCC_REQ_sum TCC_STREAMING_REQ_sum TCC_READ_sum TCC_EA0_RDREQ_DRAM_sum
+    pmc $lib sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE
+    pmc $lib tcp TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_NC_READ_REQ_sum
+  done
+  ;;
+abp0)  # shapes of the capture form (product) at steady state, interleaved in one process
+  timeout -k 10 120 tests/cpp/build/engine_fault_test > "$out/engine_fault.log" 2>&1
+  timeout -k 10 300 tests/cpp/build/engine_fault_test_asan > "$out/engine_fault_asan.log" 2>&1
+  timeout -k 10 400 python3 tools/ab.py --config A --variants \
+      "gather=1;gather=1,chunk_packets=16;gather=1,chunk_packets=4;gather=1,lds_pad=30000;gather=1,short_loads=0;gather=0" \
+      > "$out/ab_A.jsonl" 2> "$out/ab_A.err"
+  AIPSTACK_AMD_LIB=$PWD/tools/build/lib_colp1.so timeout -k 10 400 python3 tools/ab.py --config A --variants \
+      "gather=1;gather=1,chunk_packets=16;gather=1,lds_pad=30000" > "$out/ab_A_colp1.jsonl" 2> "$out/ab_A_colp1.err"
+  ;;
+*)
+  echo "unknown mode $mode"; exit 2 ;;
+esac
