@@ -454,7 +454,14 @@ struct HeaderCapture {
         }
     }
     // The store runs under exec = the window's mask, set and restored inside one asm
-    // statement (the compiler would test each lane's bit with VALU instead).
+    // statement (the compiler would test each lane's bit with VALU instead). The statement
+    // declares SCC clobbered (s_and_saveexec_b64 writes it): without that, LLVM may keep a
+    // scalar compare's SCC live across it -- an s_cmp before, an s_cselect after, selecting
+    // between the masks of two windows in flight. Round 5's copy of this store in the gathered
+    // stream lacked the clobber and did swap two windows' start masks; EXEC is
+    // restored inside the statement, and LDS stores complete in order, so the compiler's own
+    // lgkmcnt waits stay conservative. tools/asm_scc_scan.py checks a build for SCC read after
+    // any such statement before it is written again.
     __device__ __forceinline__ void window(const u32x4 &v, uint32_t w, uint32_t hv) {
         static_assert(U <= 8, "wmask holds 8 zero words past the last window");
         const uint64_t m = mk[w & (uint32_t)(U - 1)];
@@ -473,7 +480,7 @@ struct HeaderCapture {
                 "s_mov_b64 exec, %0"
                 : "=&s"(save)
                 : "v"(addr), "s"(m), "v"(v), "v"(haddr), "v"(hv)
-                : "memory");
+                : "memory", "scc");
         } else {
             asm volatile(
                 "s_and_saveexec_b64 %0, %2\n\t"
@@ -481,7 +488,7 @@ struct HeaderCapture {
                 "s_mov_b64 exec, %0"
                 : "=&s"(save)
                 : "v"(addr), "s"(m), "v"(v)
-                : "memory");
+                : "memory", "scc");
         }
         count += (uint32_t)__builtin_popcountll(m);
     }

@@ -1141,6 +1141,57 @@ def test_fill_then_verify_on_gpu():
     assert set(np.unique(v).tolist()) <= {0, 3, 6, 8}
 
 
+def _capture_group_crossings(off, shift, cpk=32, U=4):
+    """Frames whose captured header segments span windows of two different groups of U
+    windows in the frames' double-buffered stream (frame_kernels.hip, HeaderCapture: the
+    masks of windows w and w + U share mk[w & (U - 1)]). Chunks of cpk frames; the batch
+    starts `shift` bytes past a 16-aligned address; kHdrNeed = 97."""
+    n = off.size - 1
+    count = 0
+    for c0 in range(0, n, cpk):
+        S = off[c0:min(c0 + cpk, n)].astype(np.int64) + shift
+        base = int(S[0]) & ~15
+        a0_32 = S & 16
+        hb_end = ((a0_32 + (S & 15) + 97 + 31) & ~31) - a0_32
+        r0 = ((S & ~15) - base) >> 4
+        r1 = r0 + (hb_end >> 4)
+        count += int(np.count_nonzero((r0 >> 6) // U != ((r1 - 1) >> 6) // U))
+    return count
+
+
+@pytest.mark.parametrize("maxp", [0, 120, 600, 1460])
+def test_frames_header_capture_across_groups(oracle, maxp):
+    """the frames' header capture (an exec-setting inline-asm LDS
+    store per window) driven through frames whose header segments span the last window of
+    one group and the first of the next, in the double-buffered loop, at every byte shift 0-15
+    and ragged chunk edges: Rx verdicts, Tx records and the in-place fill against the oracle.
+    The test counts those frames and requires some (the case is exercised, not just random)."""
+    crossings = 0
+    for shift in range(16):
+        buf, off = synth.frames_host(2049, seed=7000 + 16 * maxp + shift, max_payload=maxp)
+        oracle.tx_fill_batch(buf, off)       # valid frames, then one flipped bit in 10 %
+        _corrupt(buf, off, 0.10, shift)
+        big = np.zeros(buf.size + shift + 16, dtype=np.uint8)
+        big[shift:shift + buf.size] = buf
+        dbig = _d(big)
+        assert dbig.data_ptr() % 16 == 0
+        doff = _d(off + np.uint64(shift))
+        crossings += _capture_group_crossings(off, shift)
+        got = _np(A.rx_verify(dbig, doff))
+        assert np.array_equal(got, oracle.rx_verify_batch(buf, off)), (shift, maxp)
+        rec = _np(A.tx_fill_records(dbig, doff))
+        filled = buf.copy()
+        st = A.apply_tx_records(filled, off, rec)
+        want = buf.copy()
+        want_st = oracle.tx_fill_batch(want, off)
+        assert np.array_equal(st, want_st) and np.array_equal(filled, want), (shift, maxp)
+        st2 = _np(A.tx_fill(dbig, doff))
+        assert np.array_equal(st2, want_st), (shift, maxp)
+        assert np.array_equal(_np(dbig)[shift:shift + buf.size], want), (shift, maxp)
+    if maxp >= 600:  # (chunks of 32 short frames stay inside one group of 4 KiB)
+        assert crossings > 100, crossings
+
+
 def _edge_frames(seed, n):
     sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
     import frame_cases

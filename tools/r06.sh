@@ -115,6 +115,37 @@ abp0)  # shapes of the capture form (product) at steady state, interleaved in on
   AIPSTACK_AMD_LIB=$PWD/tools/build/lib_colp1.so timeout -k 10 400 python3 tools/ab.py --config A --variants \
       "gather=1;gather=1,chunk_packets=16;gather=1,lds_pad=30000" > "$out/ab_A_colp1.jsonl" 2> "$out/ab_A_colp1.err"
   ;;
+fresh6)  # the GPU suite; fresh-data lines per writer (with and without the JUST_WRITTEN hint)
+         # for A, C, A2K, CHAIN, RX; the driver's command
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+      > "$out/pytest_gpu.log" 2>&1
+  b() {  # b NAME ARGS...
+    name=$1; shift
+    timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-ceiling "$@" \
+        >> "$out/$name.json" 2>> "$out/$name.err"
+  }
+  b driver_A --gpus 1 --per-launch
+  timeout -k 10 300 python3 -u tools/tx_ceiling.py > "$out/tx_ceiling.jsonl" 2> "$out/tx_ceiling.err"
+  AIPSTACK_AMD_LIB=$PWD/tools/build/lib_txnt.so timeout -k 10 300 python3 -u tools/tx_ceiling.py \
+      > "$out/tx_ceiling_txnt.jsonl" 2> "$out/tx_ceiling_txnt.err"
+  # in-place Tx fills: field stores plain / nontemporal (lib_txnt), field-line touches on / off
+  for i in 1 2; do
+    b tx_plain --config TX --per-launch
+    AIPSTACK_CHKSUM_TX_GATHER=1 b tx_plain_notouch --config TX --per-launch
+    AIPSTACK_AMD_LIB=$PWD/tools/build/lib_txnt.so b tx_nt --config TX --per-launch
+    AIPSTACK_AMD_LIB=$PWD/tools/build/lib_txnt.so AIPSTACK_CHKSUM_TX_GATHER=1 b tx_nt_notouch --config TX --per-launch
+    b tx2k_plain --config TX2K --per-launch
+    AIPSTACK_AMD_LIB=$PWD/tools/build/lib_txnt.so b tx2k_nt --config TX2K --per-launch
+  done
+  for w in dma nt plain d2d; do
+    b fresh_A --fresh $w
+    b fresh_A --fresh $w --just-written
+  done
+  for cfg in C A2K CHAIN RX B; do
+    for w in dma plain; do b fresh_$cfg --config $cfg --fresh $w; done
+  done
+  b driver_A --gpus 1 --per-launch
+  ;;
 *)
   echo "unknown mode $mode"; exit 2 ;;
 esac
