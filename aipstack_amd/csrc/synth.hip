@@ -16,6 +16,9 @@ namespace {
 
 // Thread t writes 16 bytes: words 2t and 2t+1 of the (byte_offset-aligned) stream.
 // Handles a byte_offset that is not a multiple of 8 by per-byte extraction at the edges.
+// Nontemporal stores: the bytes land the way the Rx path's DMA delivers them. A batch written
+// by ordinary (write-back) stores reads slower the first time (config A 285-312
+// us against 221-231 after DMA or nontemporal stores); bench.py --fresh measures each writer.
 __global__ __launch_bounds__(256) void synth_fill_kernel(uint8_t *__restrict__ buf,
                                                          uint64_t nbytes, uint64_t seed,
                                                          uint64_t byte_offset) {
@@ -26,12 +29,13 @@ __global__ __launch_bounds__(256) void synth_fill_kernel(uint8_t *__restrict__ b
         const uint64_t k = (byte_offset + i0) >> 3;
         typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
         u64x2 v = {aipstack_synth_word(seed, k), aipstack_synth_word(seed, k + 1)};
-        *reinterpret_cast<u64x2 *>(buf + i0) = v;
+        __builtin_nontemporal_store(v, reinterpret_cast<u64x2 *>(buf + i0));
         return;
     }
     for (uint64_t i = i0; i < i0 + 16 && i < nbytes; ++i) {
         const uint64_t g = byte_offset + i;
-        buf[i] = (uint8_t)(aipstack_synth_word(seed, g >> 3) >> (8 * (g & 7)));
+        __builtin_nontemporal_store((uint8_t)(aipstack_synth_word(seed, g >> 3) >> (8 * (g & 7))),
+                                    buf + i);
     }
 }
 
@@ -46,8 +50,8 @@ __global__ __launch_bounds__(256) void synth_classes_kernel(uint8_t *__restrict_
     const uint32_t cls = aipstack_synth_class(len_seed, first_packet + p);
     if (cls > 2) return;
     const uint64_t s = off[p], e = off[p + 1];
-    for (uint64_t j = lane; j < e - s; j += 64)
-        buf[s + j] = (uint8_t)aipstack_synth_class_byte(cls, j, e - s);
+    for (uint64_t j = lane; j < e - s; j += 64)  // (nontemporal, as synth_fill_kernel)
+        __builtin_nontemporal_store((uint8_t)aipstack_synth_class_byte(cls, j, e - s), buf + s + j);
 }
 
 }  // namespace

@@ -288,6 +288,29 @@ def algorithmic_bytes(layout, n, total_payload):
     return b
 
 
+def dma_copy(t):
+    """A copy of device tensor `t` at another address, written by DMA (pinned host -> device):
+    the way the Rx path's bytes arrive. A device-side clone (ordinary stores) would leave its
+    lines slow to read the first time."""
+    import torch
+    h = torch.empty(t.numel(), dtype=t.dtype, pin_memory=True)
+    h.copy_(t)
+    out = torch.empty_like(t)
+    out.copy_(h, non_blocking=True)
+    torch.cuda.synchronize()
+    return out
+
+
+def dma_to(arr, dev):
+    """numpy array -> device tensor through pinned host memory (DMA)."""
+    import torch
+    h = torch.from_numpy(arr).pin_memory()
+    out = torch.empty(h.shape, dtype=h.dtype, device=dev)
+    out.copy_(h, non_blocking=True)
+    torch.cuda.synchronize()
+    return out
+
+
 def make_chains(spec, dev):
     """CHAIN workload: chain i = a 20-B header node (TCP header, 32-B stride header area)
     + 1460 payload bytes split into two chunks at a random point (a send ring wrapping,
@@ -651,7 +674,7 @@ def main():
     spec = shard_spec(args.config, rank, world)
     if layout in ("rx", "tx", "txrec"):
         frames_host = host_shard(spec)          # frames are synthesised on the host
-        buf = torch.from_numpy(frames_host).to(dev)
+        buf = dma_to(frames_host, dev)
         d_off = torch.from_numpy(spec["offsets"]).to(dev)
         status = torch.empty(n, dtype=torch.uint8, device=dev)
         tx_ws = torch.empty(8 * n, dtype=torch.uint8, device=dev)  # split fill's records
@@ -660,7 +683,7 @@ def main():
         # the shard's frames / packets laid into 2048-B ring slots (slack = random bytes)
         compact_host = host_shard(spec)
         ring_host, lens_host = synth.to_slots(compact_host, spec["offsets"], SLOT_STRIDE[args.config])
-        buf = torch.from_numpy(ring_host).to(dev)
+        buf = dma_to(ring_host, dev)
         d_lens = torch.from_numpy(lens_host.view(np.int32)).to(dev)
         status = torch.empty(n, dtype=torch.uint8, device=dev)
         tx_ws = torch.empty(8 * n, dtype=torch.uint8, device=dev)  # slotted split's records
@@ -692,13 +715,13 @@ def main():
     chain_rot = []  # chains: copies of the buffer, each with its chunk table rebased onto it
     if layout == "chain" and rot > 1:
         for _ in range(rot - 1):
-            bc = chain["buf"].clone()
+            bc = dma_copy(chain["buf"])
             delta = bc.data_ptr() - chain["base"]
             chain_rot.append({"buf": bc, "addr": chain["addr"] + delta,
                               "fields": chain["fields"] + delta})
     fbufs = [buf] if layout in FRAME_LAYOUTS else []  # frame / ring-slot batches: R copies
     if layout in FRAME_LAYOUTS and rot > 1:               # at distinct addresses
-        fbufs += [buf.clone() for _ in range(rot - 1)]
+        fbufs += [dma_copy(buf) for _ in range(rot - 1)]
     out = outs[0] if outs else torch.empty(n, dtype=torch.uint16, device=dev)
     torch.cuda.synchronize()
     step_no = [0]
@@ -954,14 +977,20 @@ def main():
         if ceil:
             slot_ceiling_fields["measured_peak"] = dict(
                 ceil, frac=round(alg / avg_kernel_s / 1e9 / ceil["GBps"], 4))
+    if layout in ("tx", "txslot") and rank == 0 and not args.tx_split and not args.no_ceiling:
+        fc = fill_ceiling(layout, fbufs, d_off if layout == "tx" else None,
+                          d_lens if layout == "txslot" else None, n, stream)
+        if fc:
+            slot_ceiling_fields["fill_ceiling"] = fc
+            slot_ceiling_fields["frac_of_fill_ceiling"] = round(fc["us"] / (avg_kernel_s * 1e6), 4)
     if layout in ("rxslot", "csrslot", "txslot") and rank == 0:
         ceil = slot_read_ceiling(args.config, spec)
         if ceil:
             kernel_gbps = payload / avg_kernel_s / 1e9
-            slot_ceiling_fields = {"slot_read_ceiling": ceil,
-                                   "payload_GBps": round(kernel_gbps, 1),
-                                   "frac_of_slot_read_ceiling":
-                                       round(kernel_gbps / ceil["payload_GBps"], 4)}
+            slot_ceiling_fields.update({"slot_read_ceiling": ceil,
+                                        "payload_GBps": round(kernel_gbps, 1),
+                                        "frac_of_slot_read_ceiling":
+                                            round(kernel_gbps / ceil["payload_GBps"], 4)})
     bytes_all = payload * world  # weak scaling: every rank holds the same-size shard
     value = bytes_all * args.steps / max_elapsed / 2**30
     achieved = alg / avg_kernel_s / 1e9
@@ -1406,6 +1435,46 @@ def slot_read_ceiling(config, spec):
         return d
     except (OSError, ValueError, IndexError, subprocess.SubprocessError):
         return None
+
+
+def fill_ceiling(layout, fbufs, d_off, d_lens, n, stream):
+    """The in-place Tx fills' own ceiling (after the timed region): fp_fill of
+    tools/fresh_probe.hip -- the fill's read pattern (TX: the chunk's frames streamed as one run;
+    TX2K: each slot's frame bytes) plus the two 2-byte field stores per frame, ordinary stores
+    as the fill's, no checksum arithmetic -- over copies of the rotation batches, median of 30
+    launches after 6. None when the probe library is absent."""
+    import statistics
+    import torch
+    path = os.path.join(ROOT, "tools", "build", "libfresh_probe.so")
+    if not os.path.exists(path):
+        return None
+    fp = ctypes.CDLL(path)
+    fp.fp_fill.restype = ctypes.c_int
+    fp.fp_fill.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                           ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p,
+                           ctypes.c_void_p]
+    copies = [b.clone() for b in fbufs]  # the probe's stores write junk into the fields
+    scratch = torch.zeros(1 << 16, dtype=torch.uint32, device=copies[0].device)
+    ts = []
+    for k in range(36):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        st = fp.fp_fill(copies[k % len(copies)].data_ptr(),
+                        d_off.data_ptr() if layout == "tx" else None,
+                        0 if layout == "tx" else SLOT_STRIDE["TX2K"],
+                        None if layout == "tx" else d_lens.data_ptr(), n, 1, 1,
+                        scratch.data_ptr(), stream.cuda_stream)
+        b.record(stream)
+        b.synchronize()
+        if st != 0:
+            return None
+        if k >= 6:
+            ts.append(a.elapsed_time(b) * 1e3)
+    del copies
+    return {"us": round(statistics.median(ts), 2),
+            "source": "tools/build/libfresh_probe.so fp_fill: the fill's read pattern plus its two "
+                      "2-byte field stores per frame (ordinary stores), no checksum arithmetic, "
+                      f"over {len(fbufs)} rotated copies, median of 30 launches after 6"}
 
 
 def hbm_read_ceiling():

@@ -1175,7 +1175,7 @@ def test_frames_header_capture_across_groups(oracle, maxp):
         big[shift:shift + buf.size] = buf
         dbig = _d(big)
         assert dbig.data_ptr() % 16 == 0
-        doff = _d(off + np.uint64(shift))
+        doff = _d((off + shift).astype(off.dtype))
         crossings += _capture_group_crossings(off, shift)
         got = _np(A.rx_verify(dbig, doff))
         assert np.array_equal(got, oracle.rx_verify_batch(buf, off)), (shift, maxp)

@@ -115,10 +115,8 @@ abp0)  # shapes of the capture form (product) at steady state, interleaved in on
   AIPSTACK_AMD_LIB=$PWD/tools/build/lib_colp1.so timeout -k 10 400 python3 tools/ab.py --config A --variants \
       "gather=1;gather=1,chunk_packets=16;gather=1,lds_pad=30000" > "$out/ab_A_colp1.jsonl" 2> "$out/ab_A_colp1.err"
   ;;
-fresh6)  # the GPU suite; fresh-data lines per writer (with and without the JUST_WRITTEN hint)
-         # for A, C, A2K, CHAIN, RX; the driver's command
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
-      > "$out/pytest_gpu.log" 2>&1
+fresh6)  # fresh-data lines per writer (with and without the JUST_WRITTEN hint) for A, C, A2K,
+         # CHAIN, RX; Tx fill ceiling; the driver's command; then the GPU suite
   b() {  # b NAME ARGS...
     name=$1; shift
     timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-ceiling "$@" \
@@ -145,6 +143,23 @@ fresh6)  # the GPU suite; fresh-data lines per writer (with and without the JUST
     for w in dma plain; do b fresh_$cfg --config $cfg --fresh $w; done
   done
   b driver_A --gpus 1 --per-launch
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+      > "$out/pytest_gpu.log" 2>&1
+  ;;
+check6)  # NT-written synthetic batches and DMA-written copies: the driver's command, its rocprof
+         # average over all 25 launches, the Tx lines with their fill ceiling
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+      -k "synth or full_size or header_capture or tx_fill_matches or rx_verify_matches or chain_many" \
+      > "$out/pytest.log" 2>&1
+  b() {  # b NAME ARGS...
+    name=$1; shift
+    timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 "$@" >> "$out/$name.json" 2>> "$out/$name.err"
+  }
+  b A --gpus 1 --per-launch
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/rocprof_A" -o run \
+      -- python3 bench.py --gpus 1 --steps 20 --warmup 5 > "$out/rocprof_A.log" 2>&1
+  for cfg in TX TX2K C CHAIN RX; do b $cfg --config $cfg --per-launch --no-cpu-baseline; done
+  b A --gpus 1 --per-launch --no-cpu-baseline
   ;;
 *)
   echo "unknown mode $mode"; exit 2 ;;
