@@ -424,6 +424,30 @@ def test_overlapping_and_zero_stride(oracle):
         assert np.array_equal(got, want), (stride, plen)
 
 
+@pytest.mark.parametrize("chunk", [1, 4, 8, 16])
+def test_gapped_columns_overlapping_and_zero_strides(oracle, chunk):
+    """Gapped column runs (strides that are multiples of 16) with strides below 16 x the
+    packet's segments -- packets overlapping, the gap negative -- and stride 0 (every packet
+    the same bytes), forced onto the column kernel with chunk_packets on a small batch
+    (ADVICE round 5), at odd and even bases, against the oracle."""
+    _tune("chunk_packets", chunk)
+    try:
+        buf = torch.empty(1 << 20, dtype=torch.uint8, device=DEV)
+        synth.fill_device(buf, 78 + chunk)
+        hb = _np(buf)
+        for stride, plen in ((16, 1500), (0, 777), (0, 1500), (32, 9000), (48, 100),
+                             (1504, 1500), (16, 1), (64, 65535)):
+            for base in (0, 5):
+                n = 300
+                if base + (n - 1) * stride + plen > buf.numel():
+                    n = (buf.numel() - base - plen) // max(stride, 1) + 1
+                got = _np(A.chksum_batch_strided(buf, stride, plen, n, byte_offset=base))
+                want = oracle.batch_strided(hb[base:], stride, plen, n)
+                assert np.array_equal(got, want), (stride, plen, base, np.nonzero(got != want)[0][:8])
+    finally:
+        _tune("chunk_packets", 0)
+
+
 def test_all_zero_and_all_ff_batches():
     for fill, want in ((0x00, 0x0000), (0xFF, 0xFFFF)):
         buf = torch.full((1500 * 4096,), fill, dtype=torch.uint8, device=DEV)

@@ -8,6 +8,9 @@ equal to the first's. Not part of the product.
 
 A variant is a list of aipstack_chksum_tune keys (0 / absent = automatic). Prints one JSON
 line per variant: median / min kernel us and payload GB/s.
+
+Sweep-only tunables (unroll, packets, nontemporal, frames) need a library built with
+-DAIPSTACK_ALL_VARIANTS (tools/build_variant.sh), passed with --lib (tools/sweep_common.py).
 """
 from __future__ import annotations
 
@@ -20,6 +23,8 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import sweep_common  # noqa: E402
 
 KEYS = ("waves_per_cu", "chunks_per_wave", "unroll", "packets", "frames", "stream",
         "chunk_packets", "tx_gather")
@@ -74,6 +79,8 @@ def main():
     for spec in args.variants.split(";"):
         kv = dict(x.split("=") for x in spec.split(",") if x)
         variants.append({k: int(v) for k, v in kv.items()})
+
+    sweep_common.require_variants(lib, variants)  # sweep-only keys need an ALL_VARIANTS build
 
     def apply(v):
         for k in KEYS:

@@ -9,6 +9,10 @@ to the first one's and, for a prefix, to the oracle. Prints one JSON object per 
 
     python tools/sweep.py --config A --rounds 8 [--variants "U,P,NT,WPC;..."]
     python tools/sweep.py --config RX [--variants "F,WPC;..."]   (frames in flight, waves/CU)
+
+U, P, NT and F (unroll, packets, nontemporal, frames) other than their defaults need a build
+with every variant: tools/build_variant.sh NAME -DAIPSTACK_ALL_VARIANTS, then --lib
+tools/build/lib_NAME.so (tools/sweep_common.py checks and says so).
 """
 from __future__ import annotations
 
@@ -22,6 +26,8 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import sweep_common  # noqa: E402
 
 DEFAULT_VARIANTS = {
     "A": "0,0,1,0;0,0,1,0,-1;0,0,1,0,2;0,0,1,0,8;0,0,1,32;0,0,1,128;0,0,1,256;0,0,1,32,8",
@@ -136,6 +142,8 @@ def main():
         su = f[4] if len(f) > 4 else 0
         variants.append({"unroll": u, "packets": p, "nontemporal": nt, "waves_per_cu": wpc,
                          "stream": su})
+
+    sweep_common.require_variants(lib, variants)  # sweep-only keys need an ALL_VARIANTS build
 
     def apply(v):
         lib.aipstack_chksum_tune(b"chunks_per_wave", 0)

@@ -11,6 +11,9 @@ Every variant's first launch is checked against the frame oracle (filled bytes a
 then rounds of `--reps` launches per variant, each bracketed by HIP events on the launch
 stream. Prints one JSON line per variant: median / min us per fill, fraction of 8 TB/s of
 the algorithmic bytes (frame bytes + 8 B offset or 4 B length + 1 B status + 4 B fields).
+
+Sweep-only tunables (unroll, packets, nontemporal, frames) need a library built with
+-DAIPSTACK_ALL_VARIANTS (tools/build_variant.sh), passed with --lib (tools/sweep_common.py).
 """
 from __future__ import annotations
 
@@ -24,6 +27,8 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import sweep_common  # noqa: E402
 
 ALIAS = {"store": "tx_store", "gather": "tx_gather"}
 
@@ -76,6 +81,8 @@ def main():
     for spec in args.variants.split(";"):
         kv = dict(x.split("=") for x in spec.split(",") if x)
         variants.append({ALIAS.get(k, k): int(v) for k, v in kv.items()})
+
+    sweep_common.require_variants(lib, variants)  # sweep-only keys need an ALL_VARIANTS build
 
     def apply(v):
         for k in ("tx_store", "tx_gather"):
