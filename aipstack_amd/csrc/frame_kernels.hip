@@ -32,6 +32,11 @@ constexpr int kHdrSegs = 8;
 constexpr int kHdrDwords = 23;  // frame bytes [0, 92) realigned to the frame start
 constexpr uint32_t kHdrNeed = 97;
 constexpr uint64_t kMaxSlotStride = AIPSTACK_CHKSUM_MAX_SLOT_STRIDE;
+// Records (the split fill's read pass, the records-only pass): nontemporal stores (1) or
+// ordinary ones (0), an A/B build switch.
+#ifndef AIPSTACK_FRAME_REC_NT
+#define AIPSTACK_FRAME_REC_NT 1
+#endif
 // The in-place Tx fills' field stores by default (tunable "tx_store", FieldSectors below).
 #ifndef AIPSTACK_TX_STORE_DEFAULT
 #define AIPSTACK_TX_STORE_DEFAULT 0
@@ -939,6 +944,13 @@ __global__ __launch_bounds__(kBlock, TX ? AIPSTACK_FRAME_WAVES_PER_SIMD
             if constexpr (SPLIT)
 #if AIPSTACK_EXP_NO_RECORDS  // experiment: price of the record stores (wrong output)
                 asm volatile("" ::"v"(o.w0), "v"(o.w1));
+#elif AIPSTACK_FRAME_REC_NT
+                // nontemporal (round 6): the records pass 126.5-130.9 us against 128.3-130.3
+                // (profiles/r06/recnt), its probe 127.7 against 130.1; and a reader of the
+                // records (the scatter pass, a D2H copy) then finds no freshly written lines
+                // 
+                __builtin_nontemporal_store((uint64_t)o.w0 | (uint64_t)o.w1 << 32,
+                                            records + p0 + lane);
 #else
                 records[p0 + lane] = (uint64_t)o.w0 | (uint64_t)o.w1 << 32;
 #endif

@@ -7,7 +7,7 @@ synthetic packets already resident in HBM. Default workload = BASELINE.json conf
 (config A): 1 M x 1500-byte packets per GPU. For A, B and C the timed loop rotates over
 R = 3 distinct resident batches (--rotate; step k reads batch k mod R, every batch checked),
 so that no launch finds its bytes in the 256 MiB Infinity Cache; the line also
-carries the same box's measured streaming-read ceiling (roofline.measured_peak).
+carries the same box's pure-read probe rate (roofline.measured_peak: a reference, not a bound).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config A|B|C]
     torchrun --nproc-per-node N ... bench.py --gpus N     (one rank per GPU)
@@ -143,7 +143,7 @@ def parse():
                         "AIPSTACK_BENCH_FORCE_DEVICE), the batch split into N ranges")
     p.add_argument("--e2e-chunk-mib", type=int, default=64)
     p.add_argument("--no-ceiling", action="store_true",
-                   help="skip the measured streaming-read ceiling (roofline.measured_peak)")
+                   help="skip the pure-read probe (roofline.measured_peak) and the Tx / records ceilings")
     p.add_argument("--rotate", type=int, default=3, metavar="R",
                    help="A, B, C, A2K: R distinct resident batches, step k reads batch k mod R "
                         "(3 x 1.5 GB for A: no launch can find its bytes in the 256 MiB "
@@ -976,13 +976,21 @@ def main():
         ceil = hbm_read_ceiling()
         if ceil:
             slot_ceiling_fields["measured_peak"] = dict(
-                ceil, frac=round(alg / avg_kernel_s / 1e9 / ceil["GBps"], 4))
+                ceil, frac=round(alg / avg_kernel_s / 1e9 / ceil["GBps"], 4),
+                kind="pure-read probe in the kernels' load shapes on this box -- a reference "
+                     "rate, not an upper bound: the checksum kernel can read faster (frac > 1)")
     if layout in ("tx", "txslot") and rank == 0 and not args.tx_split and not args.no_ceiling:
         fc = fill_ceiling(layout, fbufs, d_off if layout == "tx" else None,
                           d_lens if layout == "txslot" else None, n, stream)
         if fc:
             slot_ceiling_fields["fill_ceiling"] = fc
             slot_ceiling_fields["frac_of_fill_ceiling"] = round(fc["us"] / (avg_kernel_s * 1e6), 4)
+    if layout == "txrec" and rank == 0 and not args.no_ceiling:
+        rc = records_ceiling(fbufs, d_off, n, stream)
+        if rc:
+            slot_ceiling_fields["records_ceiling"] = rc
+            slot_ceiling_fields["frac_of_records_ceiling"] = round(
+                rc["us"] / (avg_kernel_s * 1e6), 4)
     if layout in ("rxslot", "csrslot", "txslot") and rank == 0:
         ceil = slot_read_ceiling(args.config, spec)
         if ceil:
@@ -1475,6 +1483,42 @@ def fill_ceiling(layout, fbufs, d_off, d_lens, n, stream):
             "source": "tools/build/libfresh_probe.so fp_fill: the fill's read pattern plus its two "
                       "2-byte field stores per frame (ordinary stores), no checksum arithmetic, "
                       f"over {len(fbufs)} rotated copies, median of 30 launches after 6"}
+
+
+def records_ceiling(fbufs, d_off, n, stream):
+    """The records pass's own ceiling (after the timed region): fp_fill_rec of
+    tools/fresh_probe.hip -- the frames' read pattern plus an 8-byte record per frame to a
+    separate array (ordinary stores, coalesced), no checksum arithmetic -- over the rotation
+    copies (read only), median of 30 launches after 6. None without the probe library."""
+    import statistics
+    import torch
+    path = os.path.join(ROOT, "tools", "build", "libfresh_probe.so")
+    if not os.path.exists(path):
+        return None
+    fp = ctypes.CDLL(path)
+    fp.fp_fill_rec.restype = ctypes.c_int
+    fp.fp_fill_rec.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                               ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int,
+                               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    dev = fbufs[0].device
+    scratch = torch.zeros(1 << 16, dtype=torch.uint32, device=dev)
+    rec = torch.empty(n, dtype=torch.int64, device=dev)
+    ts = []
+    for k in range(36):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        st = fp.fp_fill_rec(fbufs[k % len(fbufs)].data_ptr(), d_off.data_ptr(), 0, None, n, 1, 3,
+                            scratch.data_ptr(), rec.data_ptr(), stream.cuda_stream)
+        b.record(stream)
+        b.synchronize()
+        if st != 0:
+            return None
+        if k >= 6:
+            ts.append(a.elapsed_time(b) * 1e3)
+    return {"us": round(statistics.median(ts), 2),
+            "source": "tools/build/libfresh_probe.so fp_fill_rec: the frames' read pattern plus an "
+                      "8-byte record per frame (ordinary stores, 256 B per wave), no checksum "
+                      f"arithmetic, over {len(fbufs)} rotated copies, median of 30 launches after 6"}
 
 
 def hbm_read_ceiling():

@@ -75,12 +75,14 @@ __global__ __launch_bounds__(256) void copy_kernel(u32x4 *__restrict__ dst,
 // bytes as one run (16-byte nontemporal buffer loads, 64 per window, 8 windows per group),
 // then lane j writes two bytes at frame j's bytes 24 and 50 (the IPv4 and, behind a 20-byte
 // header, the L4 checksum field) when its frame index is a multiple of `density`. STORE: 0
-// none (the pure read), 1 ordinary 2-byte stores (the product's), 2 nontemporal.
+// none (the pure read), 1 ordinary 2-byte stores (the product's), 2 nontemporal; 3 / 4: no
+// field store, an 8-byte record per frame to a separate array instead (the records pass's
+// output, coalesced: 256 B per wave), ordinary / nontemporal.
 template <int STORE>
 __global__ __launch_bounds__(256) void fill_csr_kernel(uint8_t *__restrict__ base,
                                                        const uint64_t *__restrict__ off,
                                                        uint64_t n, uint32_t density,
-                                                       uint32_t *out) {
+                                                       uint32_t *out, uint64_t *rec) {
     constexpr int kFr = 32, U = 8;
     const int lane = threadIdx.x & 63;
     const uint64_t wave = (uint64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -106,7 +108,14 @@ __global__ __launch_bounds__(256) void fill_csr_kernel(uint8_t *__restrict__ bas
 #pragma unroll
         for (int u = 0; u < U; ++u) acc ^= v[u][0] + v[u][1] + v[u][2] + v[u][3];
     }
-    if (STORE != 0 && lane < cnt && (p0 + (uint64_t)lane) % density == 0) {
+    if (STORE >= 3 && lane < cnt) {
+        const uint64_t r = (uint64_t)acc << 32 | (uint32_t)S;
+        if (STORE == 4)
+            __builtin_nontemporal_store(r, rec + p0 + lane);
+        else
+            rec[p0 + lane] = r;
+    }
+    if ((STORE == 1 || STORE == 2) && lane < cnt && (p0 + (uint64_t)lane) % density == 0) {
         uint16_t *f0 = reinterpret_cast<uint16_t *>(base + S + 24);
         uint16_t *f1 = reinterpret_cast<uint16_t *>(base + S + 50);
         if (STORE == 2) {
@@ -209,10 +218,13 @@ extern "C" int fp_copy(void *dst, const void *src, uint64_t nbytes, int nontempo
     return (int)hipGetLastError();
 }
 
-// fill probes: d_off = n + 1 CSR offsets (TX), or d_lens + stride (TX2K; d_off null)
-extern "C" int fp_fill(void *buf, const uint64_t *d_off, uint64_t stride, const uint32_t *d_lens,
-                       uint64_t n, uint32_t density, int store, void *scratch, void *stream) {
-    if (n == 0 || density == 0 || store < 0 || store > 2) return -1;
+// fill probes: d_off = n + 1 CSR offsets (TX), or d_lens + stride (TX2K; d_off null);
+// store 3 / 4 (CSR only): 8-byte records to d_rec (n entries) instead of field stores
+extern "C" int fp_fill_rec(void *buf, const uint64_t *d_off, uint64_t stride,
+                           const uint32_t *d_lens, uint64_t n, uint32_t density, int store,
+                           void *scratch, uint64_t *d_rec, void *stream) {
+    if (n == 0 || density == 0 || store < 0 || store > 4) return -1;
+    if (store >= 3 && (!d_off || !d_rec)) return -1;
     const uint64_t waves = (n + 31) / 32;
     const dim3 grid((unsigned)((waves + 3) / 4));
     const hipStream_t s = (hipStream_t)stream;
@@ -220,9 +232,11 @@ extern "C" int fp_fill(void *buf, const uint64_t *d_off, uint64_t stride, const 
     uint32_t *o = (uint32_t *)scratch;
     if (d_off) {
         switch (store) {
-        case 0: hipLaunchKernelGGL(fill_csr_kernel<0>, grid, dim3(256), 0, s, b, d_off, n, density, o); break;
-        case 1: hipLaunchKernelGGL(fill_csr_kernel<1>, grid, dim3(256), 0, s, b, d_off, n, density, o); break;
-        default: hipLaunchKernelGGL(fill_csr_kernel<2>, grid, dim3(256), 0, s, b, d_off, n, density, o); break;
+        case 0: hipLaunchKernelGGL(fill_csr_kernel<0>, grid, dim3(256), 0, s, b, d_off, n, density, o, d_rec); break;
+        case 1: hipLaunchKernelGGL(fill_csr_kernel<1>, grid, dim3(256), 0, s, b, d_off, n, density, o, d_rec); break;
+        case 2: hipLaunchKernelGGL(fill_csr_kernel<2>, grid, dim3(256), 0, s, b, d_off, n, density, o, d_rec); break;
+        case 3: hipLaunchKernelGGL(fill_csr_kernel<3>, grid, dim3(256), 0, s, b, d_off, n, density, o, d_rec); break;
+        default: hipLaunchKernelGGL(fill_csr_kernel<4>, grid, dim3(256), 0, s, b, d_off, n, density, o, d_rec); break;
         }
     } else {
         if (!d_lens || stride == 0) return -1;
@@ -233,4 +247,10 @@ extern "C" int fp_fill(void *buf, const uint64_t *d_off, uint64_t stride, const 
         }
     }
     return (int)hipGetLastError();
+}
+
+extern "C" int fp_fill(void *buf, const uint64_t *d_off, uint64_t stride, const uint32_t *d_lens,
+                       uint64_t n, uint32_t density, int store, void *scratch, void *stream) {
+    if (store > 2) return -1;
+    return fp_fill_rec(buf, d_off, stride, d_lens, n, density, store, scratch, nullptr, stream);
 }

@@ -161,6 +161,51 @@ check6)  # NT-written synthetic batches and DMA-written copies: the driver's com
   for cfg in TX TX2K C CHAIN RX; do b $cfg --config $cfg --per-launch --no-cpu-baseline; done
   b A --gpus 1 --per-launch --no-cpu-baseline
   ;;
+txrec6)  # the records pass against Rx verify on the same frames: times, the records' price
+         # (lib_norec: no record stores, wrong output), counters
+  b() {  # b NAME ARGS...
+    name=$1; shift
+    timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline "$@" >> "$out/$name.json" 2>> "$out/$name.err"
+  }
+  for i in 1 2; do
+    b RX --config RX --per-launch
+    b TXREC --config TXREC --per-launch
+    AIPSTACK_AMD_LIB=$PWD/tools/build/lib_norec.so b TXREC_norec --config TXREC --per-launch --no-parity
+  done
+  pmc() {  # pmc CFG NAME COUNTERS...
+    cfg=$1; name=$2; shift 2
+    timeout -s KILL 120 rocprofv3 --kernel-trace --output-format csv -d "$out/${cfg}_$name" -o run \
+        --pmc "$@" -- python3 bench.py --config $cfg --steps 20 --warmup 5 --no-cpu-baseline \
+        --no-parity > "$out/${cfg}_$name.log" 2>&1
+  }
+  for cfg in RX TXREC; do
+    pmc $cfg sq1 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES
+    pmc $cfg sq2 SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS
+    pmc $cfg tcc FETCH_SIZE TCC_EA0_WRREQ_sum
+  done
+  ;;
+rank8)  # the multi-rank flow rehearsed on this one GPU (every rank on device 0): the solo phase
+        # and scaling_efficiency; the records pass with its ceiling; the Tx probe sweep
+  for N in 2 8; do
+    AIPSTACK_BENCH_FORCE_DEVICE=0 timeout -k 10 400 python3 -m torch.distributed.run --nnodes=1 \
+        --nproc-per-node $N --master-addr 127.0.0.1 --master-port $((29600 + N)) bench.py \
+        --gpus $N --steps 20 --warmup 5 --no-cpu-baseline --no-ceiling > "$out/bench${N}_A.json" \
+        2> "$out/bench${N}_A.err"
+  done
+  timeout -k 10 300 python3 bench.py --config TXREC --steps 20 --warmup 5 --no-cpu-baseline \
+      --per-launch > "$out/TXREC.json" 2> "$out/TXREC.err"
+  timeout -k 10 300 python3 -u tools/tx_ceiling.py TX > "$out/tx_ceiling.jsonl" 2> "$out/tx_ceiling.err"
+  ;;
+recnt)  # the records pass with nontemporal record stores (lib_recnt) against ordinary ones
+  b() {  # b NAME ARGS...
+    name=$1; shift
+    timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline "$@" >> "$out/$name.json" 2>> "$out/$name.err"
+  }
+  for i in 1 2 3; do
+    b TXREC --config TXREC --per-launch --no-ceiling
+    AIPSTACK_AMD_LIB=$PWD/tools/build/lib_recnt.so b TXREC_nt --config TXREC --per-launch --no-ceiling
+  done
+  ;;
 *)
   echo "unknown mode $mode"; exit 2 ;;
 esac

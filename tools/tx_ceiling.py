@@ -30,6 +30,10 @@ def main():
     import bench
 
     fp = ctypes.CDLL(os.path.join(ROOT, "tools", "build", "libfresh_probe.so"))
+    fp.fp_fill_rec.restype = ctypes.c_int
+    fp.fp_fill_rec.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                               ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p,
+                               ctypes.c_void_p, ctypes.c_void_p]
     fp.fp_fill.restype = ctypes.c_int
     fp.fp_fill.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                            ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p,
@@ -97,6 +101,19 @@ def main():
                                   "store": name, "density": density, "us": round(t, 2),
                                   "ns_per_store_over_read": round((t - t_read) * 1e3 / stores, 4)}),
                       flush=True)
+        if cfg == "TX":  # the records pass's pattern: the read plus an 8-byte record per frame
+            rec = torch.empty(n, dtype=torch.int64, device=dev)
+            for store, name in ((3, "ordinary"), (4, "nontemporal")):
+                def run(r, store=store):
+                    if fp.fp_fill_rec(copies[r].data_ptr(), d_off.data_ptr(), 0, None, n, 1, store,
+                                      scratch.data_ptr(), rec.data_ptr(), sh) != 0:
+                        raise SystemExit("fp_fill_rec")
+                t = timed(run)
+                print(json.dumps({"config": cfg, "what": "probe read + 8-byte records",
+                                  "store": name, "us": round(t, 2)}), flush=True)
+            t = timed(lambda r: A.tx_fill_records(copies[r], d_off, out=rec, stream=stream))
+            print(json.dumps({"config": cfg, "what": "product records pass", "us": round(t, 2)}),
+                  flush=True)
         # the product on the same copies (the probe's junk fields are rewritten by the fill)
         for kind in ("fill", "verify"):
             t = product(kind)
