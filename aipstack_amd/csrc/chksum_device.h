@@ -967,6 +967,29 @@ __device__ __forceinline__ int wave_max_scan(int v) {
     return v;
 }
 
+// Exact halves-sum of lane j's own short chunk [a, a + l) (l <= 128 B here: at most 9
+// segments), read by the lane itself: its aligned 16-byte segments, nontemporal, the bytes
+// outside the chunk masked off; kmax = the wave's largest segment count (uniform). The chain
+// kernel's header nodes (round 6, chain runs): side by side in memory, adjacent lanes read
+// adjacent segments, so one wave instruction fetches whole lines.
+__device__ __forceinline__ uint32_t sum_own_short_chunk(uint64_t a, uint32_t l, uint32_t kmax) {
+    typedef __attribute__((address_space(1))) const u32x4 gseg;
+    const uint32_t rs = (uint32_t)a & 15u;
+    const uint32_t nsg = l ? (rs + l + 15u) >> 4 : 0u;
+    const uint32_t te = ((rs + l - 1u) & 15u) + 1u;  // the chunk's end in its last segment
+    const gseg *p = (const gseg *)(a & ~(uint64_t)15);
+    uint32_t acc = 0;
+    for (uint32_t k = 0; k < kmax; ++k) {
+        if (k < nsg) {
+            const u32x4 x = __builtin_nontemporal_load(p + k);
+            const int lo = k == 0 ? (int)rs : 0, hi = k + 1 == nsg ? (int)te : 16;
+#pragma unroll
+            for (int d = 0; d < 4; ++d) acc = halves(x[d] & dword_keep(lo - 4 * d, hi - 4 * d), acc);
+        }
+    }
+    return acc;
+}
+
 // ---------------------------------------------------------------------------------
 // Gathered stream (the chain kernel): up to 64 chunks anywhere in memory (lane j: chunk
 // [a_j, a_j + l_j), l_j <= 65535, empty chunks allowed) read as ONE stream of just their

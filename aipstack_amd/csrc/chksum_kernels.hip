@@ -231,6 +231,15 @@ __device__ __forceinline__ uint32_t parity_below(uint64_t mask, uint32_t s) {  /
 
 // SU = 4 (the default since round 4) holds four more segment quads per lane than SU = 2 and
 // gets 4 waves per SIMD (at 5 it spilled 68 bytes per lane at 96 VGPRs); SU = 2 keeps 5.
+// Chain runs (round 6; A/B build switch AIPSTACK_CHAIN_RUNS): long chunks that lie back to
+// back read as one stream-prefix run, short ones by their own lanes. Bit-exact (the chain
+// tests), but slower on CHAIN: 261.0-261.5 us against 251.8-254.5 for the gathered stream
+// (profiles/r06/chain6): a 31 KiB run with 43 boundaries per group costs the stream prefixes'
+// per-window scan and boundary evaluation more than the gathered stream's owner lookup. Off.
+#ifndef AIPSTACK_CHAIN_RUNS
+#define AIPSTACK_CHAIN_RUNS 0
+#endif
+constexpr bool kChainRuns = AIPSTACK_CHAIN_RUNS != 0;
 template <bool NT, int SU>
 __global__ __launch_bounds__(kBlock, SU > 2 ? 4 : 5) void chksum_chain_kernel(
     const uint64_t *__restrict__ chunk_addr, const uint32_t *__restrict__ chunk_len,
@@ -250,6 +259,7 @@ __global__ __launch_bounds__(kBlock, SU > 2 ? 4 : 5) void chksum_chain_kernel(
     const bool final_flag = (flags & AIPSTACK_CHKSUM_FINAL) != 0;
     uint64_t *acc = lds_acc[wave_in_block];
     int *mark = lds_mark[wave_in_block];
+    const uint32_t voff = (uint32_t)lane * 16u;  // (chain runs: this lane's segment in a window)
     CsrDesc idx_desc{0, index};  // the chain index walks like CSR offsets
 
     for (; c < c_end; ++c) {
@@ -313,9 +323,47 @@ __global__ __launch_bounds__(kBlock, SU > 2 ? 4 : 5) void chksum_chain_kernel(
             // the next header's turn). Any order gives the same sums: each chunk's sum
             // returns to its lane through the inverse permutation. CHAIN: FETCH_SIZE -1.3 %,
             // 241.0-241.7 vs 241.9-242.9 us (profiles/r04/short, probe).
-            uint32_t sums;
+            uint32_t sums = 0;
             const uint32_t lv = valid ? l : 0u;
-            if (short_first) {
+            bool done = false;
+            if constexpr (kChainRuns && SU > 2) {  // (SU 2, 5 waves per SIMD: would spill)
+                // Chain runs (round 6): when the group's long chunks, in table order, lie back
+                // to back -- the payload pieces of consecutive segments cut from one send
+                // buffer, tcp/IpTcpProto_output.h:1251-1277 -- they are read as ONE run with
+                // stream prefixes (sum_stream_chunk, C's loader: no owner lookup, no 64-bit
+                // address per window) in lanes 0..nl-1, and the short ones (header nodes, at
+                // most short_first bytes) each by its own lane. Any other layout: the gathered
+                // stream below. Each chunk's sum returns to its lane through the inverse
+                // permutation, as there.
+                const bool shortc = short_first != 0u && lv != 0u && lv <= short_first;
+                const uint64_t lm = __builtin_amdgcn_ballot_w64(lv != 0u && !shortc);
+                const uint32_t nl = (uint32_t)__builtin_popcountll(lm);
+                const uint32_t below_l = __builtin_amdgcn_mbcnt_hi(
+                    (uint32_t)(lm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)lm, 0u));
+                const bool longc = ((lm >> lane) & 1ull) != 0;
+                const uint32_t rank = longc ? below_l : nl + (uint32_t)lane - below_l;
+                const int to = (int)(rank << 2);
+                const uint32_t a_lo = (uint32_t)__builtin_amdgcn_ds_permute(to, (int)(uint32_t)a);
+                const uint32_t a_hi = (uint32_t)__builtin_amdgcn_ds_permute(to, (int)(uint32_t)(a >> 32));
+                const uint32_t l_p = (uint32_t)__builtin_amdgcn_ds_permute(to, (int)lv);
+                const uint64_t a_p = ((uint64_t)a_hi << 32) | a_lo;
+                if (nl != 0u && stream_ok(a_p, a_p + l_p, lane, (int)nl)) {
+                    const uint32_t s_long = sum_stream_chunk<16, NT>(a_p, a_p + l_p, lane,
+                                                                     (int)nl, voff);
+                    // the short ones: lanes nl.. hold them (and the empty chunks, l_p = 0)
+                    const uint32_t nsg = ((uint32_t)lane >= nl && l_p)
+                                             ? (((uint32_t)a_p & 15u) + l_p + 15u) >> 4 : 0u;
+                    const uint32_t kmax = (uint32_t)__builtin_amdgcn_readlane(
+                        wave_max_scan((int)nsg), kWave - 1);
+                    const uint32_t s_short = sum_own_short_chunk(a_p, (uint32_t)lane >= nl ? l_p : 0u,
+                                                                 kmax);
+                    const uint32_t s_p = (uint32_t)lane < nl ? s_long : s_short;
+                    sums = (uint32_t)__builtin_amdgcn_ds_bpermute(to, (int)s_p);
+                    done = true;
+                }
+            }
+            if (done) {
+            } else if (short_first) {
                 // a short chunk goes first only if it shares no line with its neighbours in
                 // the table (a header node apart from the payload; a short payload piece
                 // stays beside the pieces it shares lines with)

@@ -899,8 +899,9 @@ def main():
     elif layout == "chain":
         if chain_rot and not args.no_parity:
             # each copy once more into its own output: the same sums as copy 0 (and, for the
-            # fill, the same headers afterwards)
-            while step_no[0] < rot:
+            # fill, the same headers afterwards). A fill sums its field, so two fills restore
+            # it: every copy must have been filled equally often (step count a multiple of R)
+            while step_no[0] < rot or step_no[0] % rot != 0:
                 step()
             ref = A.chksum_batch_chain(chain["addr"], chain["len"], chain["index"],
                                        chain["states"], final=True, stream=stream)

@@ -206,6 +206,27 @@ recnt)  # the records pass with nontemporal record stores (lib_recnt) against or
     AIPSTACK_AMD_LIB=$PWD/tools/build/lib_recnt.so b TXREC_nt --config TXREC --per-launch --no-ceiling
   done
   ;;
+chain6)  # chain runs (long chunks back to back as one stream-prefix run, short ones per lane)
+         # against the gathered stream (lib_chain0): the chain tests, then alternating benches
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+      -k "chain" > "$out/pytest.log" 2>&1
+  b() {  # b NAME ARGS...
+    name=$1; shift
+    timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline "$@" >> "$out/$name.json" 2>> "$out/$name.err"
+  }
+  for i in 1 2; do
+    b CHAIN --config CHAIN --per-launch
+    AIPSTACK_AMD_LIB=$PWD/tools/build/lib_chain0.so b CHAIN0 --config CHAIN --per-launch
+  done
+  b CHAINFILL --config CHAIN --chain-fill
+  AIPSTACK_AMD_LIB=$PWD/tools/build/lib_chain0.so b CHAINFILL0 --config CHAIN --chain-fill
+  timeout -s KILL 120 rocprofv3 --kernel-trace --output-format csv -d "$out/pmc_CHAIN" -o run \
+      --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES -- python3 bench.py --config CHAIN \
+      --steps 20 --warmup 5 --no-cpu-baseline --no-parity > "$out/pmc_CHAIN.log" 2>&1
+  timeout -s KILL 120 rocprofv3 --kernel-trace --output-format csv -d "$out/fetch_CHAIN" -o run \
+      --pmc FETCH_SIZE -- python3 bench.py --config CHAIN --steps 20 --warmup 5 --no-cpu-baseline \
+      --no-parity > "$out/fetch_CHAIN.log" 2>&1
+  ;;
 *)
   echo "unknown mode $mode"; exit 2 ;;
 esac
