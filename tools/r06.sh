@@ -227,6 +227,54 @@ chain6)  # chain runs (long chunks back to back as one stream-prefix run, short 
       --pmc FETCH_SIZE -- python3 bench.py --config CHAIN --steps 20 --warmup 5 --no-cpu-baseline \
       --no-parity > "$out/fetch_CHAIN.log" 2>&1
   ;;
+final_bench)  # every config under the driver's protocol (A first, as the box's first GPU
+              # process), with the CPU baseline, the read probe and the Tx / records / slot ceilings
+  for c in A B C A2K C2K CHAIN RX RX2K TXREC TX TX2K; do
+    timeout -k 10 300 python3 bench.py --config $c --steps 20 --warmup 5 --per-launch \
+        >> "$out/bench_$c.json" 2>> "$out/bench_$c.err"
+  done
+  timeout -k 10 120 tools/build/hbm_peak ceiling > "$out/ceiling.jsonl"
+  ;;
+final_prof)  # rocprofv3 --kernel-trace --stats of each config's driver-protocol command
+  for c in A B C A2K C2K CHAIN RX RX2K TXREC TX TX2K; do
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/prof_$c" -o run \
+        -- python3 bench.py --config $c --steps 20 --warmup 5 --no-cpu-baseline --no-ceiling \
+        > "$out/prof_$c.log" 2>&1
+  done
+  ;;
+final_pmc1)  # PMC passes (tools/pmc_run.sh), first half of the configs
+  for c in A B C A2K C2K CHAIN; do tools/pmc_run.sh $c "$out/pmc_$c"; done
+  ;;
+final_pmc2)
+  for c in RX RX2K TXREC TX TX2K; do tools/pmc_run.sh $c "$out/pmc_$c"; done
+  ;;
+final_misc)  # small batches, end to end, the chain fill, fresh A, the 8-rank launch rehearsed
+  for n in 64 4096; do
+    for c in A RX TX; do
+      timeout -k 10 120 python3 bench.py --config $c --small $n >> "$out/small.jsonl" 2>> "$out/small.err"
+    done
+  done
+  for c in A C RX TX C2K; do
+    timeout -k 10 300 python3 bench.py --e2e --config $c --steps 5 --warmup 1 >> "$out/e2e.jsonl" 2>> "$out/e2e.err"
+  done
+  timeout -k 10 300 python3 bench.py --config CHAIN --chain-fill --steps 20 --warmup 5 \
+      --no-cpu-baseline > "$out/bench_CHAINFILL.json" 2> "$out/bench_CHAINFILL.err"
+  for w in dma plain; do
+    timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --fresh $w \
+        >> "$out/fresh_A.json" 2>> "$out/fresh_A.err"
+  done
+  timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --fresh plain \
+      --just-written >> "$out/fresh_A.json" 2>> "$out/fresh_A.err"
+  AIPSTACK_BENCH_FORCE_DEVICE=0 timeout -k 10 400 python3 -m torch.distributed.run --nnodes=1 \
+      --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29631 bench.py --gpus 8 \
+      --steps 20 --warmup 5 --cpu-reps 3 > "$out/bench8_A.json" 2> "$out/bench8_A.err"
+  ;;
+final_test)  # the round-end gate on this tree
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+      > "$out/pytest_gpu.log" 2>&1
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.log" 2>&1
+  timeout -k 10 120 tests/cpp/build/engine_fault_test > "$out/engine_fault.log" 2>&1
+  ;;
 *)
   echo "unknown mode $mode"; exit 2 ;;
 esac
