@@ -349,7 +349,7 @@ def _require_lens(lens, n_slots_bytes, slot_stride, buf):
 
 
 def chksum_batch_slotted(buf, slot_stride: int, lens, *, out=None, final: bool = False,
-                         stream=None):
+                         stream=None, just_written: bool = False):
     """Ring slots on the GPU: ``out[i] = IpChksumInverted(buf[i*slot_stride:][:lens[i]])``
     (``IpChksum`` with ``final=True``). ``lens``: int32/uint32 device tensor of n lengths,
     each <= min(slot_stride, 65535); ``buf`` holds n whole slots."""
@@ -358,7 +358,8 @@ def chksum_batch_slotted(buf, slot_stride: int, lens, *, out=None, final: bool =
     out = _out_tensor(out, n, buf)
     _check(_lib.load().aipstack_chksum_batch_slotted(
         buf.data_ptr(), slot_stride, lens.data_ptr(), n, out.data_ptr(),
-        AIPSTACK_CHKSUM_FINAL if final else 0, _stream_handle(stream, buf)),
+        (AIPSTACK_CHKSUM_FINAL if final else 0) | (AIPSTACK_CHKSUM_JUST_WRITTEN if just_written else 0),
+        _stream_handle(stream, buf)),
         "aipstack_chksum_batch_slotted")
     return out
 
@@ -986,7 +987,7 @@ class ChksumEngineGroup:
 
 
 def chksum_batch_chain(chunk_addr, chunk_len, chunk_index, states=None, *, out=None,
-                       final: bool = False, stream=None):
+                       final: bool = False, stream=None, just_written: bool = False):
     """Chained (scatter-gather) batch on the GPU: chain i = chunks
     ``[chunk_index[i], chunk_index[i+1])``, chunk k = ``chunk_len[k]`` bytes at DEVICE
     address ``chunk_addr[k]``. ``final=True`` gives
@@ -1010,19 +1011,22 @@ def chksum_batch_chain(chunk_addr, chunk_len, chunk_index, states=None, *, out=N
     out = _out_tensor(out, n, chunk_index)
     st = _lib.load().aipstack_chksum_batch_chain(
         chunk_addr.data_ptr(), chunk_len.data_ptr(), chunk_index.data_ptr(), sp or None, n,
-        out.data_ptr(), AIPSTACK_CHKSUM_FINAL if final else 0, _stream_handle(stream, chunk_index))
+        out.data_ptr(),
+        (AIPSTACK_CHKSUM_FINAL if final else 0) | (AIPSTACK_CHKSUM_JUST_WRITTEN if just_written else 0),
+        _stream_handle(stream, chunk_index))
     _check(st, "aipstack_chksum_batch_chain")
     return out
 
 
 def chksum_chain_fill(chunk_addr, chunk_len, chunk_index, states, fields, *, out=None,
-                      zero_as_ffff: bool = False, stream=None):
+                      zero_as_ffff: bool = False, stream=None, just_written: bool = False):
     """The Tx form of :func:`chksum_batch_chain`: chain i's final checksum
     (``IpChksumAccumulator(State(states[i])).getChksum(chain i)``) is stored big-endian at
     DEVICE address ``fields[i]`` (int64 tensor; 0 = no store) -- the checksum field of the
     header the chain starts with, which must read 0 when the batch runs, as the reference
     sets it before summing (tcp/IpTcpProto_output.h:1251-1277, udp/IpUdpProto.h:164-179).
-    ``zero_as_ffff`` sends a computed 0 as 0xFFFF (UDP). Returns the checksums (``out``)."""
+    ``zero_as_ffff`` sends a computed 0 as 0xFFFF (UDP). ``just_written``: the
+    AIPSTACK_CHKSUM_JUST_WRITTEN hint (results unchanged). Returns the checksums (``out``)."""
     for t, name in ((chunk_addr, "chunk_addr"), (chunk_len, "chunk_len"),
                     (chunk_index, "chunk_index"), (fields, "fields")):
         _require_device(t, name)
@@ -1043,7 +1047,9 @@ def chksum_chain_fill(chunk_addr, chunk_len, chunk_index, states, fields, *, out
     out = _out_tensor(out, n, chunk_index)
     st = _lib.load().aipstack_chksum_batch_chain_fill(
         chunk_addr.data_ptr(), chunk_len.data_ptr(), chunk_index.data_ptr(), sp or None,
-        fields.data_ptr(), n, out.data_ptr(), AIPSTACK_CHKSUM_ZERO_AS_FFFF if zero_as_ffff else 0,
+        fields.data_ptr(), n, out.data_ptr(),
+        (AIPSTACK_CHKSUM_ZERO_AS_FFFF if zero_as_ffff else 0) |
+        (AIPSTACK_CHKSUM_JUST_WRITTEN if just_written else 0),
         _stream_handle(stream, chunk_index))
     _check(st, "aipstack_chksum_batch_chain_fill")
     return out

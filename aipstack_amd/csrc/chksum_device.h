@@ -572,13 +572,19 @@ __device__ __forceinline__ uint32_t dword_keep(int a, int b) {
 #endif
 constexpr bool kEdgeNT = AIPSTACK_EDGE_NT != 0;
 
-__device__ __forceinline__ u32x4 load_edge_segment(uint64_t addr) {
+// `nt` (wave-uniform, run time): the AIPSTACK_CHKSUM_JUST_WRITTEN hint -- on lines ordinary
+// stores wrote since they were last read, a cached read is the expensive one.
+__device__ __forceinline__ u32x4 load_edge_segment(uint64_t addr, bool nt = false) {
     typedef __attribute__((address_space(1))) const u32x4 gseg;
     const gseg *p = (const gseg *)addr;
-    if constexpr (kEdgeNT)
+    if (kEdgeNT || nt)
         return __builtin_nontemporal_load(p);
     else
         return *p;
+}
+__device__ __forceinline__ u32x4 load_edge_segment(__amdgpu_buffer_rsrc_t rsrc, uint32_t voff,
+                                                   bool nt = false) {
+    return (kEdgeNT || nt) ? load_segment<true>(rsrc, voff, 0u) : load_segment<false>(rsrc, voff, 0u);
 }
 
 template <bool NT>
@@ -1129,7 +1135,8 @@ struct ChunkLoader {
 template <int U, bool NT, bool EDGE = true>
 __device__ __forceinline__ uint32_t sum_gathered_chunks(uint64_t a, uint32_t l, int lane,
                                                         GatherLds *glds,
-                                                        const KeepTable *keep_table) {
+                                                        const KeepTable *keep_table,
+                                                        bool edge_nt = false) {
     const uint32_t rs = (uint32_t)a & 15u;
     const uint32_t ns = l ? (rs + l + 15u) >> 4 : 0u;
     const uint32_t ns_incl = wave_incl_scan(ns);
@@ -1199,8 +1206,8 @@ __device__ __forceinline__ uint32_t sum_gathered_chunks(uint64_t a, uint32_t l, 
     u32x4 fseg = {0u, 0u, 0u, 0u}, lseg = {0u, 0u, 0u, 0u};
     const uint32_t te = ((rs + l - 1u) & 15u) + 1u;  // the chunk's end in its last segment
     if constexpr (EDGE) {
-        if (ns && rs != 0u) fseg = load_edge_segment(a & ~(uint64_t)15);
-        if (ns && te != 16u) lseg = load_edge_segment((a + l - 1u) & ~(uint64_t)15);
+        if (ns && rs != 0u) fseg = load_edge_segment(a & ~(uint64_t)15, edge_nt);
+        if (ns && te != 16u) lseg = load_edge_segment((a + l - 1u) & ~(uint64_t)15, edge_nt);
     }
     ld.issue(0, va, ka);
     const uint32_t foreign = EDGE && ns ? foreign_halves(fseg, lseg, (int)rs, (int)te) : 0u;
@@ -1588,7 +1595,8 @@ __device__ __forceinline__ uint32_t sum_column_chunk(uint64_t S, uint64_t E, int
 template <bool NT>
 __device__ __forceinline__ uint32_t sum_gapped_column_chunk(uint64_t s0, int lane, int cnt,
                                                             uint32_t cpk, uint32_t *rows,
-                                                            const GappedColDesc &d) {
+                                                            const GappedColDesc &d,
+                                                            bool edge_nt = false) {
     const uint32_t ns = d.ns;
     const uint32_t rs = (uint32_t)s0 & 15u;
     const uint64_t B0 = s0 & ~(uint64_t)15;
@@ -1601,8 +1609,8 @@ __device__ __forceinline__ uint32_t sum_gapped_column_chunk(uint64_t s0, int lan
     const uint32_t te = ((rs + d.len - 1u) & 15u) + 1u;
     const uint32_t pkoff = (uint32_t)lane * (uint32_t)d.stride;  // lanes < cnt: < span
     u32x4 fseg = {0u, 0u, 0u, 0u}, lseg = {0u, 0u, 0u, 0u};
-    if (lane < cnt && rs != 0u) fseg = load_segment<kEdgeNT>(rsrc, pkoff, 0u);
-    if (lane < cnt && te != 16u) lseg = load_segment<kEdgeNT>(rsrc, pkoff + 16u * (ns - 1u), 0u);
+    if (lane < cnt && rs != 0u) fseg = load_edge_segment(rsrc, pkoff, edge_nt);
+    if (lane < cnt && te != 16u) lseg = load_edge_segment(rsrc, pkoff + 16u * (ns - 1u), edge_nt);
 // windows per group (A/B build switch; A2K 228.9-229.7 us at 6 and 228.9-229.6 at 8,
 // profiles/r05/gcu)
 #ifndef AIPSTACK_GAPCOL_WINDOWS

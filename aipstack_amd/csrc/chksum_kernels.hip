@@ -69,6 +69,8 @@ __global__ __launch_bounds__(kBlock) void chksum_batch_kernel(Desc desc, uint64_
     uint64_t c = wave * chunks_per_wave;
     const uint64_t c_end = min(c + chunks_per_wave, nchunks);
     const bool final_flag = (flags & AIPSTACK_CHKSUM_FINAL) != 0;
+    // the JUST_WRITTEN hint: the read forms' few loads outside their streams nontemporal too
+    const bool edge_nt = (flags & AIPSTACK_CHKSUM_JUST_WRITTEN) != 0;
     const uint32_t voff = (uint32_t)lane * 16u;          // this lane's segment in a slot
     const uint32_t not_lane0 = lane == 0 ? 0u : ~0u;     // head-mask lane select
     // Ring slots with SU > 0: the chunk's 64 packets read as ONE gathered stream of just
@@ -123,14 +125,15 @@ __global__ __launch_bounds__(kBlock) void chksum_batch_kernel(Desc desc, uint64_
             streamed = true;
         } else if constexpr (kGapCols) {
             sums = sum_gapped_column_chunk<NT>(chunk.s0, lane, cnt, chunk_packets,
-                                               col_rows[wave_in_block], desc);
+                                               col_rows[wave_in_block], desc, edge_nt);
             streamed = true;
         } else if constexpr (kGathered) {
             // (CSR: every packet within the contract, else the wave mode below)
             if (!Desc::kCsr || __builtin_amdgcn_ballot_w64(lE - lS > (uint64_t)AIPSTACK_CHKSUM_MAX_LEN) == 0) {
                 if constexpr (Desc::kEdge)
                     sums = sum_gathered_chunks<SU, NT, true>(lS, (uint32_t)(lE - lS), lane,
-                                                             &gsh.g[wave_in_block], nullptr);
+                                                             &gsh.g[wave_in_block], nullptr,
+                                                             edge_nt);
                 else
                     sums = sum_gathered_chunks<SU, NT, false>(lS, (uint32_t)(lE - lS), lane,
                                                               &gsh.g[wave_in_block], &gsh.keep);
@@ -207,6 +210,9 @@ __global__ __launch_bounds__(kBlock) void chksum_batch_kernel(Desc desc, uint64_
 // ---------------------------------------------------------------------------------
 
 // A 16-bit store at any byte address (one global_store_short: gfx9 runs in unaligned mode).
+#ifndef AIPSTACK_CHAIN_FIELD_NT
+#define AIPSTACK_CHAIN_FIELD_NT 1
+#endif
 typedef uint16_t u16_any_align __attribute__((aligned(1)));
 
 // Second pass of the chain fill: chain i's checksum (from the chained batch's output) stored
@@ -220,7 +226,13 @@ __global__ __launch_bounds__(kBlock) void chain_field_scatter_kernel(
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
     for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
         const uint64_t fa = fields[i];
+#if AIPSTACK_CHAIN_FIELD_NT  // nontemporal field stores (round 6): the header lines they write
+                             // carry no first-read cost into the next batch: chain
+                             // fill 265.6-265.8 us against 307.1-308.3 (profiles/r06/hint6)
+        if (fa) __builtin_nontemporal_store((uint16_t)bswap16(sums[i]), reinterpret_cast<u16_any_align *>(fa));
+#else
         if (fa) *reinterpret_cast<u16_any_align *>(fa) = (uint16_t)bswap16(sums[i]);
+#endif
     }
 }
 
@@ -257,6 +269,7 @@ __global__ __launch_bounds__(kBlock, SU > 2 ? 4 : 5) void chksum_chain_kernel(
     uint64_t c = wave * chunks_per_wave;
     const uint64_t c_end = min(c + chunks_per_wave, ngroups);
     const bool final_flag = (flags & AIPSTACK_CHKSUM_FINAL) != 0;
+    const bool edge_nt = (flags & AIPSTACK_CHKSUM_JUST_WRITTEN) != 0;  // 
     uint64_t *acc = lds_acc[wave_in_block];
     int *mark = lds_mark[wave_in_block];
     const uint32_t voff = (uint32_t)lane * 16u;  // (chain runs: this lane's segment in a window)
@@ -385,11 +398,12 @@ __global__ __launch_bounds__(kBlock, SU > 2 ? 4 : 5) void chksum_chain_kernel(
                 const uint32_t a_hi = (uint32_t)__builtin_amdgcn_ds_permute(to, (int)(uint32_t)(a >> 32));
                 const uint32_t l_p = (uint32_t)__builtin_amdgcn_ds_permute(to, (int)lv);
                 const uint32_t s_p = sum_gathered_chunks<SU, NT>(
-                    ((uint64_t)a_hi << 32) | a_lo, l_p, lane, &lds_gather[wave_in_block], nullptr);
+                    ((uint64_t)a_hi << 32) | a_lo, l_p, lane, &lds_gather[wave_in_block], nullptr,
+                    edge_nt);
                 sums = (uint32_t)__builtin_amdgcn_ds_bpermute(to, (int)s_p);
             } else {
                 sums = sum_gathered_chunks<SU, NT>(a, lv, lane, &lds_gather[wave_in_block],
-                                                   nullptr);
+                                                   nullptr, edge_nt);
             }
             uint32_t r = fold16(sums);
             if ((uint32_t)(a & 1) == q)
@@ -1090,7 +1104,7 @@ extern "C" int aipstack_chksum_batch_chain(const uint64_t *d_chunk_addr,
     if (!d_chunk_addr || !d_chunk_len || !d_chunk_index || !d_out) return AIPSTACK_CHKSUM_EINVAL;
     if (n > (1ull << 40)) return AIPSTACK_CHKSUM_EINVAL;
     return chain_batch(d_chunk_addr, d_chunk_len, d_chunk_index, d_states, nullptr, n, d_out,
-                       flags & AIPSTACK_CHKSUM_FINAL, stream);
+                       flags & (AIPSTACK_CHKSUM_FINAL | AIPSTACK_CHKSUM_JUST_WRITTEN), stream);
 }
 
 extern "C" int aipstack_chksum_batch_chain_fill(const uint64_t *d_chunk_addr,
@@ -1104,6 +1118,7 @@ extern "C" int aipstack_chksum_batch_chain_fill(const uint64_t *d_chunk_addr,
         return AIPSTACK_CHKSUM_EINVAL;
     if (n > (1ull << 40)) return AIPSTACK_CHKSUM_EINVAL;
     return chain_batch(d_chunk_addr, d_chunk_len, d_chunk_index, d_states, d_field_addr, n,
-                       d_out, AIPSTACK_CHKSUM_FINAL | (flags & AIPSTACK_CHKSUM_ZERO_AS_FFFF),
+                       d_out, AIPSTACK_CHKSUM_FINAL |
+                                  (flags & (AIPSTACK_CHKSUM_ZERO_AS_FFFF | AIPSTACK_CHKSUM_JUST_WRITTEN)),
                        stream);
 }

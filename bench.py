@@ -158,7 +158,8 @@ def parse():
                         "(hipMemcpyAsync device -> device). Only the checksum launches are timed "
                         "(an event pair around each); the line carries 'fresh'")
     p.add_argument("--just-written", action="store_true",
-                   help="pass the AIPSTACK_CHKSUM_JUST_WRITTEN hint (strided batches)")
+                   help="pass the AIPSTACK_CHKSUM_JUST_WRITTEN hint (strided, ring-slot and "
+                        "chain batches)")
     return p.parse_args()
 
 
@@ -741,7 +742,8 @@ def main():
         elif layout == "rxslot":
             A.rx_verify_slotted(fbufs[k % len(fbufs)], 2048, d_lens, out=status, stream=stream)
         elif layout == "csrslot":
-            A.chksum_batch_slotted(fbufs[k % len(fbufs)], 2048, d_lens, out=out, stream=stream)
+            A.chksum_batch_slotted(fbufs[k % len(fbufs)], 2048, d_lens, out=out, stream=stream,
+                                   just_written=args.just_written)
         elif layout == "txslot":  # idempotent, as the CSR fill
             A.tx_fill_slotted(fbufs[k % len(fbufs)], 2048, d_lens, out=status, stream=stream,
                               split=args.tx_split, workspace=tx_ws if args.tx_split else None)
@@ -749,10 +751,12 @@ def main():
             cc = chain if k % rot == 0 else chain_rot[k % rot - 1]
             if args.chain_fill:
                 A.chksum_chain_fill(cc["addr"], chain["len"], chain["index"], chain["states"],
-                                    cc["fields"], out=out, stream=stream)
+                                    cc["fields"], out=out, stream=stream,
+                                    just_written=args.just_written)
             else:
                 A.chksum_batch_chain(cc["addr"], chain["len"], chain["index"], chain["states"],
-                                     out=out, final=True, stream=stream)
+                                     out=out, final=True, stream=stream,
+                                     just_written=args.just_written)
         else:  # tx: idempotent (the filled fields are excluded from their own sums)
             A.tx_fill(fbufs[k % len(fbufs)], d_off, out=status, stream=stream,
                       split=args.tx_split, workspace=tx_ws)

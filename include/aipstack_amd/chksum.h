@@ -59,8 +59,10 @@ extern "C" {
  * costs the memory side far more than a streaming one, so the batch is then read without
  * touching any of its lines through the L2-allocating path (config A: 242-258 us against
  * 285-312 for the default form; the default form is faster on bytes that arrived by DMA or
- * streaming stores, and on bytes read before). Honoured by aipstack_chksum_batch_strided for
- * back-to-back packets of >= 1 KiB (column runs); ignored elsewhere. */
+ * streaming stores, and on bytes read before). Honoured by aipstack_chksum_batch_strided
+ * (back-to-back packets of >= 1 KiB: boundary segments captured from the stream; packets at a
+ * stride: their edge segments read nontemporal), aipstack_chksum_batch_slotted and the chain
+ * batches (edge segments nontemporal); ignored elsewhere. */
 #define AIPSTACK_CHKSUM_JUST_WRITTEN 4u
 
 /* ---- 1. per-packet host hook ----------------------------------------------------- */

@@ -448,6 +448,40 @@ def test_gapped_columns_overlapping_and_zero_strides(oracle, chunk):
         _tune("chunk_packets", 0)
 
 
+def test_just_written_hint_every_form(oracle, golden):
+    """The AIPSTACK_CHKSUM_JUST_WRITTEN hint changes how a batch is read, never the
+    result: gapped strided packets (A2K's form, odd and even starts), ring slots of mixed
+    lengths (C2K's form) and chains (the reference fixtures' scatter chains), each against the
+    same call without the hint and the oracle."""
+    buf = torch.empty(1 << 22, dtype=torch.uint8, device=DEV)
+    synth.fill_device(buf, 97)
+    hb = _np(buf)
+    for stride, plen, base in ((2048, 1500, 0), (2048, 1500, 7), (1504, 1500, 3), (64, 33, 1)):
+        n = min(1500, (buf.numel() - base - plen) // stride + 1)
+        want = oracle.batch_strided(hb[base:], stride, plen, n)
+        for jw in (False, True):
+            got = _np(A.chksum_batch_strided(buf, stride, plen, n, byte_offset=base,
+                                             just_written=jw))
+            assert np.array_equal(got, want), (stride, plen, base, jw)
+    rng = np.random.default_rng(98)
+    lens = rng.integers(0, 2049, 1500).astype(np.uint32)
+    ring = torch.empty(1500 * 2048, dtype=torch.uint8, device=DEV)
+    synth.fill_device(ring, 99)
+    dl = _d(lens.view(np.int32))
+    a = _np(A.chksum_batch_slotted(ring, 2048, dl))
+    b = _np(A.chksum_batch_slotted(ring, 2048, dl, just_written=True))
+    rh = _np(ring)
+    want = np.array([oracle.inverted(rh, 2048 * i, int(lens[i])) for i in range(1500)],
+                    dtype=np.uint16)
+    assert np.array_equal(a, want) and np.array_equal(b, want)
+    db = _d(golden["blob"])
+    addr, ln, idx, st, want = _chain_tables(golden, db)
+    args = (_d(addr.view(np.int64)), _d(ln.view(np.int32)), _d(idx.view(np.int64)),
+            _d(st.view(np.int32)))
+    got = _np(A.chksum_batch_chain(*args, final=True, just_written=True))
+    assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
+
+
 def test_all_zero_and_all_ff_batches():
     for fill, want in ((0x00, 0x0000), (0xFF, 0xFFFF)):
         buf = torch.full((1500 * 4096,), fill, dtype=torch.uint8, device=DEV)

@@ -275,6 +275,55 @@ final_test)  # the round-end gate on this tree
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.log" 2>&1
   timeout -k 10 120 tests/cpp/build/engine_fault_test > "$out/engine_fault.log" 2>&1
   ;;
+hint6)  # the JUST_WRITTEN hint in the gathered and gapped forms and the chains (nontemporal
+        # edge loads): parity, fresh plain-written data with and without it; the chain fill with
+        # nontemporal field stores (lib_fieldnt)
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+      -k "just_written or chain or gapped or slotted or short_runs" > "$out/pytest.log" 2>&1
+  b() {  # b NAME ARGS...
+    name=$1; shift
+    timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-ceiling "$@" >> "$out/$name.json" 2>> "$out/$name.err"
+  }
+  for c in A2K C2K CHAIN; do
+    b fresh_$c --config $c --fresh plain
+    b fresh_$c --config $c --fresh plain --just-written
+    b fresh_$c --config $c --fresh dma --just-written
+    b steady_$c --config $c
+  done
+  for i in 1 2; do
+    b chainfill --config CHAIN --chain-fill
+    AIPSTACK_AMD_LIB=$PWD/tools/build/lib_fieldnt.so b chainfill_nt --config CHAIN --chain-fill
+  done
+  ;;
+hint6b)  # the hint on batches read before (steady state): chains and ring slots, alternating
+  b() {  # b NAME ARGS...
+    name=$1; shift
+    timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-ceiling "$@" >> "$out/$name.json" 2>> "$out/$name.err"
+  }
+  for i in 1 2; do
+    for c in CHAIN C2K; do
+      b steady_$c --config $c
+      b steady_hint_$c --config $c --just-written
+    done
+  done
+  b chainfill --config CHAIN --chain-fill
+  b chainfill_hint --config CHAIN --chain-fill --just-written
+  ;;
+txsplit6)  # the split Tx fills with nontemporal field stores in the scatter pass (lib_txnt:
+           # every field store nontemporal) against ordinary ones, and the one-pass fills
+  b() {  # b NAME ARGS...
+    name=$1; shift
+    timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-ceiling "$@" >> "$out/$name.json" 2>> "$out/$name.err"
+  }
+  for i in 1 2; do
+    for c in TX TX2K; do
+      b ${c}_split --config $c --tx-split
+      AIPSTACK_AMD_LIB=$PWD/tools/build/lib_txnt.so b ${c}_split_nt --config $c --tx-split
+      b ${c}_one --config $c
+      AIPSTACK_AMD_LIB=$PWD/tools/build/lib_txnt.so b ${c}_one_nt --config $c
+    done
+  done
+  ;;
 *)
   echo "unknown mode $mode"; exit 2 ;;
 esac
