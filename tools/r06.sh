@@ -324,6 +324,10 @@ txsplit6)  # the split Tx fills with nontemporal field stores in the scatter pas
     done
   done
   ;;
+driver)  # the driver's exact command on a fresh box, twice, and the N = 2 rehearsal
+  timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 > "$out/n1_a.json" 2> "$out/n1_a.err"
+  timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 > "$out/n1_b.json" 2> "$out/n1_b.err"
+  ;;
 *)
   echo "unknown mode $mode"; exit 2 ;;
 esac
