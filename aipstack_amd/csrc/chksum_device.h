@@ -996,6 +996,27 @@ __device__ __forceinline__ uint32_t sum_own_short_chunk(uint64_t a, uint32_t l, 
     return acc;
 }
 
+// The same with the chunk's first two segments already loaded (x0, x1: issued early, so that
+// their latency hides behind other loads); segments 2.. are loaded here.
+__device__ __forceinline__ uint32_t sum_short_chunk_from(const u32x4 &x0, const u32x4 &x1,
+                                                         uint64_t a, uint32_t l, uint32_t kmax) {
+    typedef __attribute__((address_space(1))) const u32x4 gseg;
+    const uint32_t rs = (uint32_t)a & 15u;
+    const uint32_t nsg = l ? (rs + l + 15u) >> 4 : 0u;
+    const uint32_t te = ((rs + l - 1u) & 15u) + 1u;
+    const gseg *p = (const gseg *)(a & ~(uint64_t)15);
+    uint32_t acc = 0;
+    for (uint32_t k = 0; k < kmax; ++k) {
+        if (k < nsg) {
+            const u32x4 x = k == 0 ? x0 : k == 1 ? x1 : __builtin_nontemporal_load(p + k);
+            const int lo = k == 0 ? (int)rs : 0, hi = k + 1 == nsg ? (int)te : 16;
+#pragma unroll
+            for (int d = 0; d < 4; ++d) acc = halves(x[d] & dword_keep(lo - 4 * d, hi - 4 * d), acc);
+        }
+    }
+    return acc;
+}
+
 // ---------------------------------------------------------------------------------
 // Gathered stream (the chain kernel): up to 64 chunks anywhere in memory (lane j: chunk
 // [a_j, a_j + l_j), l_j <= 65535, empty chunks allowed) read as ONE stream of just their
@@ -1482,9 +1503,13 @@ __device__ __forceinline__ uint32_t sum_stream_chunk(uint64_t S, uint64_t E, int
 constexpr int kColMaxPackets = 16;
 constexpr uint32_t kColSegTab = (kColMaxPackets + 1) * kWave;  // dword offset of the segments
 typedef uint32_t ColRows[(kColMaxPackets + 1) * kWave + (kColMaxPackets + 1) * 4];
+// MAXP: boundaries per run at most MAXP + 1 (rows of MAXP + 1 columns, then MAXP + 1 segments)
+template <int MAXP>
+using ColRowsN = uint32_t[(MAXP + 1) * kWave + (MAXP + 1) * 4];
 
-// U: windows per group (8; 6 for chunks of one long packet, launch_short_runs).
-template <bool NT, int U = 8, bool CAPTURE = false>
+// U: windows per group (8; 6 for chunks of one long packet, launch_short_runs). MAXP: the
+// most packets a run holds (rows: a ColRowsN<MAXP>); cpk = 64 / (64 lanes / MAXP per packet).
+template <bool NT, int U = 8, bool CAPTURE = false, int MAXP = kColMaxPackets>
 __device__ __forceinline__ uint32_t sum_column_chunk(uint64_t S, uint64_t E, int lane, int cnt,
                                                      uint32_t voff, uint32_t cpk, uint32_t *rows) {
     const uint64_t X1 = readlane64(E, cnt - 1);  // end of the chunk's last packet
@@ -1498,7 +1523,7 @@ __device__ __forceinline__ uint32_t sum_column_chunk(uint64_t S, uint64_t E, int
         reinterpret_cast<void *>(A), (short)0, (int)(nseg * 16u), 0x00020000);
     const uint32_t rel = (uint32_t)(S - A);  // lane j: boundary j's byte in the run
     const uint32_t o = rel & 15u;
-    uint32_t *const segs = rows + kColSegTab;  // (CAPTURE) boundary j's segment: entry j
+    uint32_t *const segs = rows + (MAXP + 1) * kWave;  // (CAPTURE) boundary j's segment: entry j
     u32x4 bseg = {0u, 0u, 0u, 0u};            // boundary j's segment (lanes 0..cnt, o != 0)
     if (!CAPTURE && lane <= cnt && o != 0u)
         bseg = load_segment<kEdgeNT>(rsrc, (rel >> 4) * 16u, 0u);
@@ -1558,7 +1583,7 @@ __device__ __forceinline__ uint32_t sum_column_chunk(uint64_t S, uint64_t E, int
         bseg = *reinterpret_cast<const u32x4 *>(segs + (uint32_t)lane * 4u);
     const uint32_t P = halves_below_seg(bseg, o);
     // packet j = lane >> ql: its 2^ql lanes add cpk column differences each
-    const uint32_t ql = 6u - (uint32_t)__builtin_ctz(cpk);  // cpk: a power of two <= 16
+    const uint32_t ql = 6u - (uint32_t)__builtin_ctz(cpk);  // cpk: a power of two <= MAXP
     const uint32_t j = (uint32_t)lane >> ql, part = (uint32_t)lane & ((1u << ql) - 1u);
     uint32_t acc = 0;
     if (j < (uint32_t)cnt) {

@@ -252,6 +252,23 @@ __device__ __forceinline__ uint32_t parity_below(uint64_t mask, uint32_t s) {  /
 #define AIPSTACK_CHAIN_RUNS 0
 #endif
 constexpr bool kChainRuns = AIPSTACK_CHAIN_RUNS != 0;
+// Chain column runs (round 6; A/B build switch AIPSTACK_CHAIN_COLS): as chain runs, but the
+// run chunks -- every non-empty chunk that is not a lone short one (the short_first rule:
+// header nodes apart from the payload), in table order -- are read as column runs of at most
+// kColMaxPackets chunks each (sum_column_chunk: no per-window scan, no owner lookup), and the
+// lone short ones each by its own lane. Any other layout: the gathered stream below.
+#ifndef AIPSTACK_CHAIN_COLS
+#define AIPSTACK_CHAIN_COLS 0
+#endif
+constexpr bool kChainCols = AIPSTACK_CHAIN_COLS != 0;
+#ifndef AIPSTACK_CHAIN_COLS_MAXP
+#define AIPSTACK_CHAIN_COLS_MAXP 32
+#endif
+constexpr int kChainColMax = AIPSTACK_CHAIN_COLS_MAXP;  // run chunks per column run (16 or 32)
+#ifndef AIPSTACK_CHAIN_COLS_U
+#define AIPSTACK_CHAIN_COLS_U 6
+#endif
+constexpr int kChainColU = AIPSTACK_CHAIN_COLS_U;  // windows per group in those runs
 template <bool NT, int SU>
 __global__ __launch_bounds__(kBlock, SU > 2 ? 4 : 5) void chksum_chain_kernel(
     const uint64_t *__restrict__ chunk_addr, const uint32_t *__restrict__ chunk_len,
@@ -260,7 +277,12 @@ __global__ __launch_bounds__(kBlock, SU > 2 ? 4 : 5) void chksum_chain_kernel(
     uint32_t flags, uint32_t short_first) {
     __shared__ uint64_t lds_acc[kWavesPerBlock][kWave];  // per-chain sum of chunk sums
     __shared__ int lds_mark[kWavesPerBlock][kWave];      // chain starting at chunk lane
-    __shared__ GatherLds lds_gather[kWavesPerBlock];                  // gathered stream owners
+    constexpr bool kCols = kChainCols && SU > 2;
+    // gathered stream owners (chain column runs: in the wave's column rows, which a slice that
+    // takes the gathered stream does not use)
+    __shared__ typename std::conditional<kCols, char, GatherLds[kWavesPerBlock]>::type lds_gather;
+    alignas(16) __shared__
+        typename std::conditional<kCols, ColRowsN<kChainColMax>[kWavesPerBlock], char>::type col_rows;
     const int lane = threadIdx.x & (kWave - 1);
     const uint32_t wave_in_block = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerBlock + wave_in_block;
@@ -273,6 +295,12 @@ __global__ __launch_bounds__(kBlock, SU > 2 ? 4 : 5) void chksum_chain_kernel(
     uint64_t *acc = lds_acc[wave_in_block];
     int *mark = lds_mark[wave_in_block];
     const uint32_t voff = (uint32_t)lane * 16u;  // (chain runs: this lane's segment in a window)
+    auto gather_lds = [&]() -> GatherLds * {
+        if constexpr (kCols)
+            return reinterpret_cast<GatherLds *>(col_rows[wave_in_block]);
+        else
+            return &lds_gather[wave_in_block];
+    };
     CsrDesc idx_desc{0, index};  // the chain index walks like CSR offsets
 
     for (; c < c_end; ++c) {
@@ -375,6 +403,74 @@ __global__ __launch_bounds__(kBlock, SU > 2 ? 4 : 5) void chksum_chain_kernel(
                     done = true;
                 }
             }
+            if constexpr (kCols) {
+                if (short_first != 0u) {
+                    // lone short chunks (the short_first rule below), run chunks, empty ones
+                    const uint32_t line_s = (uint32_t)(a >> 7);
+                    const uint32_t line_e = (uint32_t)((a + lv - 1u) >> 7);
+                    const uint32_t prev_e =
+                        (uint32_t)__builtin_amdgcn_ds_bpermute((lane - 1) << 2, (int)line_e);
+                    const uint32_t next_s =
+                        (uint32_t)__builtin_amdgcn_ds_bpermute((lane + 1) << 2, (int)line_s);
+                    const bool sc = lv != 0 && lv <= short_first && prev_e != line_s &&
+                                    next_s != line_e;
+                    const bool rc = lv != 0 && !sc;
+                    const uint64_t rm = __builtin_amdgcn_ballot_w64(rc);
+                    const uint64_t sm = __builtin_amdgcn_ballot_w64(sc);
+                    const uint32_t nr = (uint32_t)__builtin_popcountll(rm);
+                    const uint32_t ns_ = (uint32_t)__builtin_popcountll(sm);
+                    const uint32_t below_r = __builtin_amdgcn_mbcnt_hi(
+                        (uint32_t)(rm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)rm, 0u));
+                    const uint32_t below_s = __builtin_amdgcn_mbcnt_hi(
+                        (uint32_t)(sm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
+                    // run chunks in lanes 0..nr-1 (table order), then the short ones, then
+                    // the empty ones
+                    const uint32_t rank = rc ? below_r
+                                          : sc ? nr + below_s
+                                               : nr + ns_ + (uint32_t)lane - below_r - below_s;
+                    const int to = (int)(rank << 2);
+                    const uint32_t a_lo = (uint32_t)__builtin_amdgcn_ds_permute(to, (int)(uint32_t)a);
+                    const uint32_t a_hi = (uint32_t)__builtin_amdgcn_ds_permute(to, (int)(uint32_t)(a >> 32));
+                    const uint32_t l_p = (uint32_t)__builtin_amdgcn_ds_permute(to, (int)lv);
+                    const uint64_t a_p = ((uint64_t)a_hi << 32) | a_lo;
+                    if (stream_ok(a_p, a_p + l_p, lane, (int)nr)) {  // back to back
+                        // the short ones' first two segments go out ahead of the runs
+                        typedef __attribute__((address_space(1))) const u32x4 gseg;
+                        const bool mine = (uint32_t)lane >= nr && (uint32_t)lane < nr + ns_;
+                        const uint32_t nsg = mine ? (((uint32_t)a_p & 15u) + l_p + 15u) >> 4 : 0u;
+                        const gseg *hp = (const gseg *)(a_p & ~(uint64_t)15);
+                        u32x4 h0 = {0u, 0u, 0u, 0u}, h1 = {0u, 0u, 0u, 0u};
+                        if (nsg > 0u) h0 = __builtin_nontemporal_load(hp);
+                        if (nsg > 1u) h1 = __builtin_nontemporal_load(hp + 1);
+                        uint32_t s_p = 0;
+                        // (cpk as a run-time value: the column differences' loop stays rolled)
+                        const uint32_t cpk = (uint32_t)kChainColMax | (flags & 0x80000000u);
+                        for (uint32_t r0 = 0; r0 < nr; r0 += (uint32_t)kChainColMax) {
+                            const int cnt_r = (int)min(nr - r0, (uint32_t)kChainColMax);
+                            const int src = (int)((((uint32_t)lane + r0) & 63u) << 2);
+                            const uint64_t S = ((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)a_hi) << 32) |
+                                               (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)a_lo);
+                            const uint64_t E = S + (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)l_p);
+                            const uint32_t sr =
+                                edge_nt ? sum_column_chunk<NT, kChainColU, true, kChainColMax>(
+                                              S, E, lane, cnt_r, voff, cpk,
+                                              col_rows[wave_in_block])
+                                        : sum_column_chunk<NT, kChainColU, false, kChainColMax>(
+                                              S, E, lane, cnt_r, voff, cpk,
+                                              col_rows[wave_in_block]);
+                            const uint32_t back = (uint32_t)__builtin_amdgcn_ds_bpermute(
+                                (int)((((uint32_t)lane - r0) & 63u) << 2), (int)sr);
+                            if ((uint32_t)lane >= r0 && (uint32_t)lane < r0 + (uint32_t)cnt_r)
+                                s_p = back;
+                        }
+                        const uint32_t kmax = (uint32_t)__builtin_amdgcn_readlane(
+                            wave_max_scan((int)nsg), kWave - 1);
+                        if (mine) s_p = sum_short_chunk_from(h0, h1, a_p, l_p, kmax);
+                        sums = (uint32_t)__builtin_amdgcn_ds_bpermute(to, (int)s_p);
+                        done = true;
+                    }
+                }
+            }
             if (done) {
             } else if (short_first) {
                 // a short chunk goes first only if it shares no line with its neighbours in
@@ -398,11 +494,11 @@ __global__ __launch_bounds__(kBlock, SU > 2 ? 4 : 5) void chksum_chain_kernel(
                 const uint32_t a_hi = (uint32_t)__builtin_amdgcn_ds_permute(to, (int)(uint32_t)(a >> 32));
                 const uint32_t l_p = (uint32_t)__builtin_amdgcn_ds_permute(to, (int)lv);
                 const uint32_t s_p = sum_gathered_chunks<SU, NT>(
-                    ((uint64_t)a_hi << 32) | a_lo, l_p, lane, &lds_gather[wave_in_block], nullptr,
+                    ((uint64_t)a_hi << 32) | a_lo, l_p, lane, gather_lds(), nullptr,
                     edge_nt);
                 sums = (uint32_t)__builtin_amdgcn_ds_bpermute(to, (int)s_p);
             } else {
-                sums = sum_gathered_chunks<SU, NT>(a, lv, lane, &lds_gather[wave_in_block],
+                sums = sum_gathered_chunks<SU, NT>(a, lv, lane, gather_lds(),
                                                    nullptr, edge_nt);
             }
             uint32_t r = fold16(sums);

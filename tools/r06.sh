@@ -227,6 +227,35 @@ chain6)  # chain runs (long chunks back to back as one stream-prefix run, short 
       --pmc FETCH_SIZE -- python3 bench.py --config CHAIN --steps 20 --warmup 5 --no-cpu-baseline \
       --no-parity > "$out/fetch_CHAIN.log" 2>&1
   ;;
+ccols)  # chain column runs (lib_chaincols: run chunks as column runs of <= 32, lib_chaincols16:
+        # <= 16; lone short ones per lane) against the gathered stream (product): the chain tests
+        # on the variants, then alternating benches, the chain fill, fresh plain-written data
+  for v in ${VARS:-chaincols chaincols16}; do
+    AIPSTACK_AMD_LIB=$PWD/tools/build/lib_$v.so timeout -k 10 600 python -u -m pytest tests \
+        -m gpu -x -v --timeout 120 --timeout-method thread -k "chain" > "$out/pytest_$v.log" 2>&1
+  done
+  b() {  # b LIB NAME ARGS...
+    lib=$1; name=$2; shift 2
+    if [ $lib = product ]; then L=$PWD/aipstack_amd/lib/libaipstack_chksum.so; else L=$PWD/tools/build/lib_$lib.so; fi
+    AIPSTACK_AMD_LIB=$L timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline \
+        "$@" >> "$out/${name}_$lib.json" 2>> "$out/${name}_$lib.err"
+  }
+  for i in 1 2; do
+    for v in product ${VARS:-chaincols chaincols16}; do b $v CHAIN --config CHAIN --per-launch --no-ceiling; done
+  done
+  for v in product ${VARS:-chaincols chaincols16}; do
+    b $v CHAINFILL --config CHAIN --chain-fill --no-ceiling
+    b $v CHAIN_plain --config CHAIN --fresh plain --no-ceiling
+    b $v CHAIN_plain_hint --config CHAIN --fresh plain --just-written --no-ceiling
+    b $v CHAIN_dma --config CHAIN --fresh dma --no-ceiling
+  done
+  for v in ${VARS:-chaincols}; do
+    AIPSTACK_AMD_LIB=$PWD/tools/build/lib_$v.so timeout -s KILL 120 rocprofv3 --kernel-trace \
+        --output-format csv -d "$out/pmc_$v" -o run --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU \
+        SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY -- python3 bench.py --config CHAIN --steps 20 --warmup 5 \
+        --no-cpu-baseline --no-parity --no-ceiling > "$out/pmc_$v.log" 2>&1
+  done
+  ;;
 final_bench)  # every config under the driver's protocol (A first, as the box's first GPU
               # process), with the CPU baseline, the read probe and the Tx / records / slot ceilings
   for c in A B C A2K C2K CHAIN RX RX2K TXREC TX TX2K; do
