@@ -252,11 +252,16 @@ __device__ __forceinline__ uint32_t parity_below(uint64_t mask, uint32_t s) {  /
 #define AIPSTACK_CHAIN_RUNS 0
 #endif
 constexpr bool kChainRuns = AIPSTACK_CHAIN_RUNS != 0;
-// Chain column runs (round 6; A/B build switch AIPSTACK_CHAIN_COLS): as chain runs, but the
-// run chunks -- every non-empty chunk that is not a lone short one (the short_first rule:
-// header nodes apart from the payload), in table order -- are read as column runs of at most
-// kColMaxPackets chunks each (sum_column_chunk: no per-window scan, no owner lookup), and the
-// lone short ones each by its own lane. Any other layout: the gathered stream below.
+// Chain column runs (round 6; COLS): as chain runs, but the run chunks -- every non-empty
+// chunk that is not a lone short one (the short_first rule: header nodes apart from the
+// payload), in table order -- are read as column runs of at most kChainColMax chunks each
+// (sum_column_chunk, capture form: no per-window scan, no owner lookup, no line read through
+// the L2-allocating path), and the lone short ones each by its own lane (their first two
+// segments loaded before the runs). Any other layout: the gathered stream below. The kernel
+// for AIPSTACK_CHKSUM_JUST_WRITTEN (launch_chain): on plain-written CHAIN 323.5 against the
+// gathered stream's 367.3 us; on bytes read before, 279-283 against 253-255 (more per-boundary
+// work at 45 segments per boundary, 4 waves per SIMD against 5), so not the default
+// (profiles/r06/ccols/). AIPSTACK_CHAIN_COLS=1: every launch (A/B build switch).
 #ifndef AIPSTACK_CHAIN_COLS
 #define AIPSTACK_CHAIN_COLS 0
 #endif
@@ -269,7 +274,7 @@ constexpr int kChainColMax = AIPSTACK_CHAIN_COLS_MAXP;  // run chunks per column
 #define AIPSTACK_CHAIN_COLS_U 6
 #endif
 constexpr int kChainColU = AIPSTACK_CHAIN_COLS_U;  // windows per group in those runs
-template <bool NT, int SU>
+template <bool NT, int SU, bool COLS = false>
 __global__ __launch_bounds__(kBlock, SU > 2 ? 4 : 5) void chksum_chain_kernel(
     const uint64_t *__restrict__ chunk_addr, const uint32_t *__restrict__ chunk_len,
     const uint64_t *__restrict__ index, const uint32_t *__restrict__ states, uint64_t n,
@@ -277,7 +282,7 @@ __global__ __launch_bounds__(kBlock, SU > 2 ? 4 : 5) void chksum_chain_kernel(
     uint32_t flags, uint32_t short_first) {
     __shared__ uint64_t lds_acc[kWavesPerBlock][kWave];  // per-chain sum of chunk sums
     __shared__ int lds_mark[kWavesPerBlock][kWave];      // chain starting at chunk lane
-    constexpr bool kCols = kChainCols && SU > 2;
+    constexpr bool kCols = (COLS || kChainCols) && SU > 2;
     // gathered stream owners (chain column runs: in the wave's column rows, which a slice that
     // takes the gathered stream does not use)
     __shared__ typename std::conditional<kCols, char, GatherLds[kWavesPerBlock]>::type lds_gather;
@@ -451,13 +456,13 @@ __global__ __launch_bounds__(kBlock, SU > 2 ? 4 : 5) void chksum_chain_kernel(
                             const uint64_t S = ((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)a_hi) << 32) |
                                                (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)a_lo);
                             const uint64_t E = S + (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)l_p);
-                            const uint32_t sr =
-                                edge_nt ? sum_column_chunk<NT, kChainColU, true, kChainColMax>(
-                                              S, E, lane, cnt_r, voff, cpk,
-                                              col_rows[wave_in_block])
-                                        : sum_column_chunk<NT, kChainColU, false, kChainColMax>(
-                                              S, E, lane, cnt_r, voff, cpk,
-                                              col_rows[wave_in_block]);
+                            uint32_t sr;
+                            if (COLS || edge_nt)  // (the COLS kernel runs for the hint alone)
+                                sr = sum_column_chunk<NT, kChainColU, true, kChainColMax>(
+                                    S, E, lane, cnt_r, voff, cpk, col_rows[wave_in_block]);
+                            else
+                                sr = sum_column_chunk<NT, kChainColU, false, kChainColMax>(
+                                    S, E, lane, cnt_r, voff, cpk, col_rows[wave_in_block]);
                             const uint32_t back = (uint32_t)__builtin_amdgcn_ds_bpermute(
                                 (int)((((uint32_t)lane - r0) & 63u) << 2), (int)sr);
                             if ((uint32_t)lane >= r0 && (uint32_t)lane < r0 + (uint32_t)cnt_r)
@@ -941,9 +946,20 @@ int launch_chain(const uint64_t *d_addr, const uint32_t *d_len, const uint64_t *
     const uint64_t waves = (nchunks + cpw - 1) / cpw;
     const uint64_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
     if (blocks > 0x7FFFFFFFull || cpw > 0xFFFFFFFFull) return AIPSTACK_CHKSUM_EINVAL;
-    hipLaunchKernelGGL((chksum_chain_kernel<NT, SU>), dim3((unsigned)blocks), dim3(kBlock),
-                       tuning_lds_pad(0), stream, d_addr, d_len, d_index, d_states, n, (uint32_t)cpw, cpg, d_out,
-                       flags, (uint32_t)tuning_chain_short());
+    // just-written bytes: the column-run kernel (SU 4 only; see chksum_chain_kernel)
+    bool cols = false;
+    if constexpr (SU > 2) {
+        cols = (flags & AIPSTACK_CHKSUM_JUST_WRITTEN) && tuning_chain_short() != 0;
+        if (cols)
+            hipLaunchKernelGGL((chksum_chain_kernel<NT, SU, true>), dim3((unsigned)blocks),
+                               dim3(kBlock), tuning_lds_pad(0), stream, d_addr, d_len, d_index,
+                               d_states, n, (uint32_t)cpw, cpg, d_out, flags,
+                               (uint32_t)tuning_chain_short());
+    }
+    if (!cols)
+        hipLaunchKernelGGL((chksum_chain_kernel<NT, SU>), dim3((unsigned)blocks), dim3(kBlock),
+                           tuning_lds_pad(0), stream, d_addr, d_len, d_index, d_states, n,
+                           (uint32_t)cpw, cpg, d_out, flags, (uint32_t)tuning_chain_short());
     if (d_fields) {  // chain fill: the field stores as a pass of their own
         const int st = check_hip(hipGetLastError());
         if (st != AIPSTACK_CHKSUM_OK) return st;

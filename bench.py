@@ -772,6 +772,11 @@ def main():
             targets = fbufs
         writer = fresh_writer(args.fresh, targets, stream)
 
+    def step_w():  # a step after the timing, on the timed steps' terms (fresh: rewrite first)
+        if writer:
+            writer(step_no[0])
+        step()
+
     for _ in range(args.warmup):
         if writer:
             writer(step_no[0])
@@ -871,7 +876,7 @@ def main():
         # every copy processed at least once (the Tx fills write each in place); the last
         # step's outputs are checked below, and the copies must equal copy 0 afterwards
         while step_no[0] < len(fbufs) or (step_no[0] - 1) % len(fbufs) != 0:
-            step()
+            step_w()
         torch.cuda.synchronize()
         if not args.no_parity:
             same = all(torch.equal(fbufs[0], b) for b in fbufs[1:])
@@ -906,7 +911,7 @@ def main():
             # fill, the same headers afterwards). A fill sums its field, so two fills restore
             # it: every copy must have been filled equally often (step count a multiple of R)
             while step_no[0] < rot or step_no[0] % rot != 0:
-                step()
+                step_w()
             ref = A.chksum_batch_chain(chain["addr"], chain["len"], chain["index"],
                                        chain["states"], final=True, stream=stream)
             same = True
@@ -927,7 +932,7 @@ def main():
         # every rotation batch was read at least once (outside the timing if the run was
         # shorter than the rotation), and each is checked below
         while step_no[0] < rot:
-            step()
+            step_w()
         torch.cuda.synchronize()
         host_out = out.cpu().numpy()
         rot_parity = None

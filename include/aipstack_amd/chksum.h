@@ -61,8 +61,10 @@ extern "C" {
  * 285-312 for the default form; the default form is faster on bytes that arrived by DMA or
  * streaming stores, and on bytes read before). Honoured by aipstack_chksum_batch_strided
  * (back-to-back packets of >= 1 KiB: boundary segments captured from the stream; packets at a
- * stride: their edge segments read nontemporal), aipstack_chksum_batch_slotted and the chain
- * batches (edge segments nontemporal); ignored elsewhere. */
+ * stride: their edge segments read nontemporal), aipstack_chksum_batch_slotted (edge segments
+ * nontemporal) and the chain batches (payload pieces that lie back to back read as column runs
+ * with their boundary segments captured from the stream, CHAIN 322.5 against 365.3 us on
+ * plain-written chains; other layouts: edge segments nontemporal); ignored elsewhere. */
 #define AIPSTACK_CHKSUM_JUST_WRITTEN 4u
 
 /* ---- 1. per-packet host hook ----------------------------------------------------- */

@@ -135,6 +135,71 @@ def test_random_chains(oracle, seed):
 
 
 @pytest.mark.parametrize("seed", range(SCENARIOS // 2))
+def test_random_tx_chains(oracle, seed):
+    """TCP-Tx-shaped chains (tcp/IpTcpProto_output.h:1251-1277): a header node in a header
+    area, then payload pieces cut back to back from one send buffer -- the layout the chain
+    kernel reads as column runs under AIPSTACK_CHKSUM_JUST_WRITTEN (chksum_chain_kernel COLS)
+    -- with short and empty pieces, long pieces (up to 65535), headers that are not lone
+    short chunks, chains without a header or without payload, and now and then a piece taken
+    from elsewhere (the slice falls back to the gathered stream). With and without the hint,
+    through the chained batch and the chain fill, against the oracle."""
+    rng = np.random.default_rng(4000 + seed)
+    n = int(rng.integers(1, 2000))
+    hstride = int(rng.choice([20, 24, 32, 40, 64]))
+    hbytes = hstride * n + 256
+    pieces, total = [], 0
+    for i in range(n):
+        k = int(rng.integers(0, 5))
+        ps = []
+        for _ in range(k):
+            r = rng.random()
+            ln = (int(rng.integers(0, 3)) if r < 0.05 else int(rng.integers(1, 129)) if r < 0.25
+                  else int(rng.integers(20000, 65536)) if r < 0.27 else int(rng.integers(129, 1500)))
+            ps.append(ln)
+            total += ln
+        pieces.append(ps)
+    blob = _blob(rng, hbytes + total + 4096)
+    hoff = int(rng.integers(0, 16))
+    poff = hbytes + int(rng.integers(0, 16))
+    d = _d(blob)
+    base = d.data_ptr()
+    addr, clen, index, flat_all = [], [], [0], []
+    p = poff
+    for i in range(n):
+        flat = []
+        if rng.random() < 0.95:  # the header node (sometimes long, sometimes elsewhere)
+            hl = int(rng.integers(1, hstride + 1)) if rng.random() < 0.97 else int(rng.integers(129, 400))
+            ho = hoff + hstride * i if hl <= hstride else int(rng.integers(0, hbytes - hl))
+            addr.append(base + ho); clen.append(hl); flat.append((ho, hl))
+        for ln in pieces[i]:
+            if rng.random() < 0.01:  # a piece from elsewhere: not back to back
+                o = int(rng.integers(0, blob.size - ln))
+                addr.append(base + o); clen.append(ln); flat.append((o, ln))
+            else:
+                addr.append(base + p); clen.append(ln); flat.append((p, ln))
+            p += ln
+        index.append(len(addr))
+        flat_all.append(flat)
+    states = rng.integers(0, 1 << 32, size=n, dtype=np.uint64).astype(np.uint32)
+    want = np.array([oracle.chain(int(states[i]), blob, flat_all[i]) for i in range(n)],
+                    dtype=np.uint16)
+    da = _d(np.array(addr or [0], dtype=np.uint64).view(np.int64))
+    dl = _d(np.array(clen or [0], dtype=np.uint32).view(np.int32))
+    di = _d(np.array(index, dtype=np.uint64).view(np.int64))
+    ds = _d(states.view(np.int32))
+    for jw in (False, True):
+        got = _np(A.chksum_batch_chain(da, dl, di, ds, final=True, just_written=jw))
+        assert np.array_equal(got, want), (seed, jw, np.nonzero(got != want)[0][:8])
+    # the chain fill (fields in a separate buffer, zero before the fill)
+    fbuf = torch.zeros(2 * n, dtype=torch.uint8, device=DEV)
+    fields = _d((fbuf.data_ptr() + 2 * np.arange(n, dtype=np.uint64)).view(np.int64))
+    got = _np(A.chksum_chain_fill(da, dl, di, ds, fields, just_written=True))
+    assert np.array_equal(got, want), (seed, np.nonzero(got != want)[0][:8])
+    stored = _np(fbuf).reshape(n, 2)
+    assert np.array_equal(stored[:, 0].astype(np.uint16) << 8 | stored[:, 1], want)
+
+
+@pytest.mark.parametrize("seed", range(SCENARIOS // 2))
 def test_random_frames(oracle, seed):
     """Frame batches of random size and payload cap, Tx-filled on the GPU (one pass and
     split) and in ring slots, then corrupted and Rx-verified, all against the frame oracle."""

@@ -256,6 +256,24 @@ ccols)  # chain column runs (lib_chaincols: run chunks as column runs of <= 32, 
         --no-cpu-baseline --no-parity --no-ceiling > "$out/pmc_$v.log" 2>&1
   done
   ;;
+ccols2)  # the column-run chain kernel for AIPSTACK_CHKSUM_JUST_WRITTEN in the product build:
+         # chain tests (the Tx-shaped random chains included), the hint's fresh-data rates
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+      -k "chain or just_written" > "$out/pytest.log" 2>&1
+  b() {  # b NAME ARGS...
+    name=$1; shift
+    timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-ceiling "$@" \
+        >> "$out/$name.json" 2>> "$out/$name.err"
+  }
+  b CHAIN --config CHAIN --per-launch
+  b CHAIN_hint --config CHAIN --per-launch --just-written
+  b CHAIN_plain --config CHAIN --fresh plain
+  b CHAIN_plain_hint --config CHAIN --fresh plain --just-written
+  b CHAIN_dma_hint --config CHAIN --fresh dma --just-written
+  b CHAINFILL --config CHAIN --chain-fill
+  b CHAINFILL_hint --config CHAIN --chain-fill --just-written
+  b CHAINFILL_plain_hint --config CHAIN --chain-fill --fresh plain --just-written
+  ;;
 final_bench)  # every config under the driver's protocol (A first, as the box's first GPU
               # process), with the CPU baseline, the read probe and the Tx / records / slot ceilings
   for c in A B C A2K C2K CHAIN RX RX2K TXREC TX TX2K; do
