@@ -312,6 +312,10 @@ final_misc)  # small batches, end to end, the chain fill, fresh A, the 8-rank la
   done
   timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --fresh plain \
       --just-written >> "$out/fresh_A.json" 2>> "$out/fresh_A.err"
+  for h in "" --just-written; do
+    timeout -k 10 300 python3 bench.py --config CHAIN --steps 20 --warmup 5 --no-cpu-baseline \
+        --fresh plain $h >> "$out/fresh_CHAIN.json" 2>> "$out/fresh_CHAIN.err"
+  done
   AIPSTACK_BENCH_FORCE_DEVICE=0 timeout -k 10 400 python3 -m torch.distributed.run --nnodes=1 \
       --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29631 bench.py --gpus 8 \
       --steps 20 --warmup 5 --cpu-reps 3 > "$out/bench8_A.json" 2> "$out/bench8_A.err"
