@@ -1045,6 +1045,46 @@ def test_chain_chunks_in_separate_allocations(oracle):
     assert np.array_equal(got, np.array(want, dtype=np.uint16))
 
 
+def test_chain_back_to_back_pieces_every_form(oracle):
+    """Chains whose payload pieces are cut back to back from one buffer -- the layout the
+    JUST_WRITTEN chain kernel reads as column runs -- at its limits: 64 KiB - 1
+    pieces (runs of 32 of them, 2 MiB), slices of 64 run chunks and no header nodes, header
+    nodes in an area of their own, the first piece at its allocation's first byte and the last
+    ending at its last byte, in device and in pinned host memory. Both kernels (with and
+    without the hint) against the oracle."""
+    rng = np.random.default_rng(7070)
+
+    def layout(n, hdr, piece_len):
+        # (state, [(0, offset, length), ...]) with headers (if any) first in the blob
+        hbytes = 32 * n if hdr else 0
+        chains, p = [], hbytes
+        for i in range(n):
+            ch = [(0, 32 * i, hdr)] if hdr else []
+            for ln in piece_len(i):
+                ch.append((0, p, ln))
+                p += ln
+            chains.append((int(rng.integers(0, 2**32)), ch))
+        return chains, p
+
+    cases = [
+        layout(40, 20, lambda i: [65535, 65535]),
+        layout(300, 0, lambda i: [int(rng.integers(1, 3001))]),
+        layout(500, 20, lambda i: [int(x) for x in rng.integers(1, 2000, int(rng.integers(0, 4)))]),
+        layout(200, int(rng.integers(1, 33)), lambda i: [int(rng.integers(1, 129)), 1460]),
+    ]
+    for k, (chains, size) in enumerate(cases):
+        host = rng.integers(0, 256, size=size, dtype=np.uint8)
+        for where in ("device", "pinned"):
+            t = _d(host) if where == "device" else torch.from_numpy(host).pin_memory()
+            addr, ln, idx, st = _chain_batch(chains, lambda b, o: t.data_ptr() + o)
+            want = np.array([oracle.chain(s, host, [(o, l) for _, o, l in ch if l])
+                             for s, ch in chains], dtype=np.uint16)
+            for jw in (False, True):
+                got = _np(A.chksum_batch_chain(addr, ln, idx, st, final=True, just_written=jw))
+                assert np.array_equal(got, want), (k, where, jw, np.nonzero(got != want)[0][:8])
+            torch.cuda.synchronize()
+
+
 # ---- frame-level batches: Tx fill / Rx verify (SURVEY 8(f) rows 2-3) ----------------------
 
 def _corrupt(buf, off, frac, seed):
