@@ -446,10 +446,13 @@ def column_chunk_model(buf, S, E, cnt, cpk, edge_loads=False):
     """sum_column_chunk, step for step: each lane's column sum C_L over the windows consumed,
     the boundary rows written when boundary j's window is consumed (the rest after the last
     window), then packet j = sum_L (X_{j+1,L} - X_{j,L}), all mod 2^32; the reduction as the
-    kernel does it (64 / cpk lanes per packet, cpk columns each). Round 6 (default):
-    X_{j,L} = C_L + (L < B_j ? s_L : L == B_j ? the bytes of the segment below o_j : 0), the
-    partial segment taken from the stream. Round 5 (edge_loads): X_{j,L} = C_L + (L < B_j ?
-    s_L : 0), and the partial P_j from a separate load of boundary j's segment, + P_{j+1} - P_j."""
+    kernel does it (64 / cpk lanes per packet, cpk columns each). edge_loads (the kernel's
+    arithmetic in both its forms): X_{j,L} = C_L + (L < B_j ? s_L : 0), and P_j, the bytes of
+    boundary j's segment below o_j, added as + P_{j+1} - P_j -- that segment from a separate
+    default-policy load (the default) or captured from the stream into LDS (CAPTURE, the
+    JUST_WRITTEN hint): the same bytes. Without edge_loads: the window-prefix variant measured
+    in round 6 and not kept, X_{j,L} = C_L + (L < B_j ? s_L : L == B_j ? the bytes of the
+    segment below o_j : 0) (halves_below_uniform)."""
     X1 = int(E[cnt - 1])
     b = [int(S[j]) if j < cnt else X1 for j in range(64)]
     A = b[0] & ~15
@@ -518,6 +521,86 @@ def test_column_model_matches_oracle(oracle, case, cpk, edge_loads):
         got[p0:p0 + cnt] = finish(column_chunk_model(buf, S, E, cnt, cpk, edge_loads)[:cnt], S)
     want = oracle.batch_csr(buf, off)
     assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
+
+
+# ---- chain column runs (round 6, chksum_chain_kernel COLS: the JUST_WRITTEN chains) -----
+
+def chain_cols_model(buf, a, l, short_first=128, maxp=32):
+    """One 64-chunk slice of the chain kernel's column-run form: the lone short chunks (at most
+    short_first bytes, sharing no 128-byte line with their table neighbours -- lanes wrap as
+    ds_bpermute does), the run chunks (every other non-empty one) in lanes 0.. in table order,
+    the rest (empty) last; the run chunks must lie back to back (stream_ok), else None (the
+    slice takes the gathered stream). Runs of at most maxp chunks by column_chunk_model (the
+    kernel's edge-load arithmetic), the short chunks summed whole. Returns each chunk's
+    halves-sum (mod 2^32) in table order."""
+    k = len(a)
+    a = [int(x) for x in a] + [0] * (64 - k)
+    l = [int(x) for x in l] + [0] * (64 - k)
+    M64 = (1 << 64) - 1
+    line_s = [(x >> 7) & M32 for x in a]
+    line_e = [(((a[j] + l[j] - 1) & M64) >> 7) & M32 for j in range(64)]
+    sc = [l[j] != 0 and l[j] <= short_first and line_e[(j - 1) % 64] != line_s[j]
+          and line_s[(j + 1) % 64] != line_e[j] for j in range(64)]
+    run = [j for j in range(64) if l[j] and not sc[j]]
+    for r in range(len(run)):
+        j = run[r]
+        if l[j] > (1 << 17) - 1:
+            return None
+        if r + 1 < len(run) and a[j] + l[j] != a[run[r + 1]]:
+            return None
+    out = [0] * 64
+    for r0 in range(0, len(run), maxp):
+        part = run[r0:r0 + maxp]
+        S = [a[j] for j in part]
+        E = [a[j] + l[j] for j in part]
+        sums = column_chunk_model(buf, S, E, len(part), maxp, edge_loads=True)
+        for i, j in enumerate(part):
+            out[j] = sums[i]
+    for j in range(64):
+        if sc[j]:
+            out[j] = _exact_halves(buf, a[j], a[j] + l[j]) & M32
+    return out[:k]
+
+
+@pytest.mark.parametrize("case", ["tx", "tx_short_pieces", "no_headers", "max_pieces",
+                                  "adjacent_headers", "displaced"])
+def test_chain_cols_model_matches_oracle(oracle, case):
+    """The JUST_WRITTEN chain kernel's column-run form (chksum_kernels.hip, COLS) on TCP-Tx
+    layouts: each chunk's sum folded and oriented as the kernel does, against the oracle."""
+    rng = np.random.default_rng(hash(("cc", case)) % 2**32)
+    buf = rng.integers(0, 256, size=(1 << 21) + 4096, dtype=np.uint8)
+    buf[600000:620000] = 0xFF
+    a, l = [], []
+    pay = 300000 + int(rng.integers(0, 16))
+    i = 0
+    while len(a) < 64:
+        if case != "no_headers" and case != "max_pieces":
+            a.append(100 + (20 if case == "adjacent_headers" else 32) * i)
+            l.append(20)
+        pieces = ([65535, 65535] if case == "max_pieces" else
+                  [int(rng.integers(1, 3000))] if case == "no_headers" else
+                  [int(rng.integers(1, 129)), int(rng.integers(1, 1460))] if case == "tx_short_pieces"
+                  else [int(rng.integers(1, 1460)), int(rng.integers(1, 1460))])
+        for ln in pieces:
+            a.append(pay)
+            l.append(ln)
+            pay += ln
+        i += 1
+    a, l = a[:64], l[:64]
+    if case == "max_pieces":
+        pay = 10
+        for j in range(64):
+            a[j], l[j] = pay, 30000
+            pay += 30000
+    sums = chain_cols_model(buf, a, l)
+    if case == "displaced":
+        a[40] += 1  # a run chunk moved: not back to back any more
+        assert chain_cols_model(buf, a, l) is None
+        return
+    assert sums is not None, case
+    for j in range(64):
+        r = finish([sums[j]], [a[j]])[0]
+        assert r == oracle.inverted(buf, a[j], l[j]), (case, j, a[j], l[j])
 
 
 # ---- slot windows (round 5, sum_slot_windows) ------------------------------------------
