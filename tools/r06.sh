@@ -274,6 +274,15 @@ ccols2)  # the column-run chain kernel for AIPSTACK_CHKSUM_JUST_WRITTEN in the p
   b CHAINFILL_hint --config CHAIN --chain-fill --just-written
   b CHAINFILL_plain_hint --config CHAIN --chain-fill --fresh plain --just-written
   ;;
+chshape)  # chain groups per wave (AIPSTACK_CHKSUM_CHUNKS_PER_WAVE; default: one group of 32
+          # chains per wave) at steady state, alternating processes
+  for i in 1 2; do
+    for w in 0 2 4 8; do
+      AIPSTACK_CHKSUM_CHUNKS_PER_WAVE=$w timeout -k 10 300 python3 bench.py --config CHAIN --steps 20 \
+          --warmup 5 --no-cpu-baseline --no-ceiling >> "$out/CHAIN_cpw$w.json" 2>> "$out/CHAIN_cpw$w.err"
+    done
+  done
+  ;;
 final_bench)  # every config under the driver's protocol (A first, as the box's first GPU
               # process), with the CPU baseline, the read probe and the Tx / records / slot ceilings
   for c in A B C A2K C2K CHAIN RX RX2K TXREC TX TX2K; do
